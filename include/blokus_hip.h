@@ -1,0 +1,161 @@
+/*
+ * blokus_hip.h -- C ABI of the MI355X-native Blokus hot path.
+ *
+ * The reference (TGALLOWAY1/ReinforcementLearning_Blokus) is pure Python and has
+ * no FFI; its hot path is reached through Python calls.  Every entry point below
+ * names the reference function it replaces (file:line in the reference tree).
+ * The Python host layer `reinforcementlearning_blokus_amd` binds these symbols
+ * with ctypes (see INTEGRATION.md for the binding a maintainer would add).
+ *
+ * Conventions
+ *   - plain C types only; no torch / HIP types in the signatures
+ *   - every call returns int status: 0 = ok, < 0 = error (bk_last_error has text)
+ *   - buffers are caller-owned; `mem` says whether pointers are host or device
+ *   - a handle owns one HIP stream (or borrows the caller's) plus scratch; use one
+ *     handle per host thread (the library never calls exit()).
+ */
+#ifndef BLOKUS_HIP_H
+#define BLOKUS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BK_ABI_VERSION 1
+#define BK_BOARD 20
+#define BK_CELLS 400
+#define BK_PLAYERS 4
+#define BK_PIECES 21
+#define BK_ORIENTS 91   /* ALL_PIECE_ORIENTATIONS total, engine/pieces.py:257 */
+#define BK_MASK_WORDS 7 /* 400 bits as 7 x u64, bit = r*20+c (engine/bitboard.py:19) */
+
+/* Status codes */
+#define BK_OK 0
+#define BK_EINVAL -1
+#define BK_EHIP -2
+#define BK_ENOMEM -3
+#define BK_EOVERFLOW -4
+
+/* Pointer residency for buffer arguments */
+#define BK_MEM_HOST 0
+#define BK_MEM_DEVICE 1
+
+/*
+ * Packed game state: 256 bytes, POD, little-endian.
+ * Mirrors engine/board.py:54-78 (Board.__init__): player_bits[p] as 400-bit
+ * little-endian integers, player_pieces_used, player_first_move, current_player,
+ * move_count.  Frontier sets are NOT part of the state: the legal-move SET does
+ * not depend on them, only the reference list ORDER does, and the
+ * host orders results with the live frontier (bk_movegen returns dense masks).
+ */
+typedef struct bk_state {
+    uint64_t planes[BK_PLAYERS][BK_MASK_WORDS]; /* 224 B: Board.player_bits[p]            */
+    uint32_t used[BK_PLAYERS];                  /*  16 B: bit (piece_id-1) = piece used     */
+    uint8_t first_move;     /* bit p: Board.player_first_move[p] (engine/board.py:65)        */
+    uint8_t current_player; /* 0..3 = Player.value-1 (engine/board.py:18-23)                 */
+    uint8_t out_mask;       /* bit p: p is known to have no legal move (monotone, may be 0)  */
+    uint8_t flags;          /* reserved, 0                                                   */
+    uint16_t move_count;    /* Board.move_count                                              */
+    uint16_t reserved16;
+    uint32_t reserved[2];
+} bk_state;
+
+/* Playout semantics */
+#define BK_SEM_ARENA 0  /* B: pass when stuck, terminal when nobody can move;
+                           analytics/tournament/arena_runner.py:652-697 + engine/game.py:182-349 */
+#define BK_SEM_ROLLOUT 1 /* A: MCTSAgent._rollout, mcts/mcts_agent.py:470-554 (cap, break, delta) */
+
+/* Legal-move list order used to turn a random index into a move */
+#define BK_ORDER_NAIVE 0    /* piece asc, orientation asc, anchor row-major:
+                               LegalMoveGenerator._get_legal_moves_naive, move_generator.py:153 */
+#define BK_ORDER_FRONTIER 1 /* reference default frontier order (move_generator.py:261) -- not yet
+                               available on the GPU path; bk_rollout returns BK_EINVAL */
+
+/* Random streams */
+#define BK_RNG_PHILOX 0   /* native: Philox4x32-10 keyed (seed, playout), counter = draw */
+#define BK_RNG_NUMPY_MT 1 /* compat: numpy RandomState(seed).randint(0, n) per seat
+                             (agents/random_agent.py:29,49); MT19937 + masked rejection   */
+
+typedef struct bk_rollout_cfg {
+    int32_t semantics;  /* BK_SEM_*                                                       */
+    int32_t order;      /* BK_ORDER_*                                                     */
+    int32_t rng;        /* BK_RNG_*                                                       */
+    int32_t max_plies;  /* BK_SEM_ROLLOUT cap (MCTSAgent max_rollout_moves, default 50);
+                           BK_SEM_ARENA: max turns (arena max_turns, default 2500)         */
+    uint64_t seed;      /* BK_RNG_PHILOX key                                              */
+    int32_t seats_share_stream; /* compat: 1 = one RandomAgent for every seat (MCTSAgent
+                                   rollout_agent), 0 = one RandomAgent per seat (arena)   */
+    int32_t reserved;
+} bk_rollout_cfg;
+
+/* One playout result: 32 bytes */
+typedef struct bk_result {
+    int16_t scores[BK_PLAYERS]; /* ARENA: BlokusGame.get_score (board + corner + centre bonus);
+                                   ROLLOUT: Board.get_score (engine/board.py:562)             */
+    uint8_t winner_mask;        /* bit p: p in GameResult.winner_ids (engine/game.py:216)    */
+    uint8_t status;             /* 0 ok; bit0: rng stream overflow (compat mode)             */
+    uint16_t plies;             /* moves placed during the playout                          */
+    uint16_t passes;            /* arena passes (arena_runner.py:660-664)                   */
+    uint16_t turns;             /* arena turn_count                                         */
+    int32_t reward;             /* ROLLOUT: final - initial Board.get_score of root player  */
+    uint32_t draws;             /* random numbers consumed                                  */
+    uint32_t reserved[2];
+} bk_result;
+
+typedef struct bk_handle_s* bk_handle;
+
+/* ---- lifecycle ------------------------------------------------------------------ */
+int bk_abi_version(void);
+int bk_tables_version(void);
+/* device = HIP device ordinal; flags reserved (0) */
+int bk_create(int device, uint32_t flags, bk_handle* out);
+int bk_destroy(bk_handle h);
+/* Borrow a caller stream (hipStream_t as void*); NULL restores the handle's own stream */
+int bk_set_stream(bk_handle h, void* stream);
+int bk_synchronize(bk_handle h);
+int bk_last_error(bk_handle h, char* buf, size_t len);
+
+/* ---- tables ------------------------------------------------------------------------ */
+/* Orientation table, global orientation id g in [0, 91): piece_id, orientation index,
+   cell count and sorted normalized offsets (engine/pieces.py:147-253).  offs = 10 ints. */
+int bk_orient_info(int g, int32_t* piece_id, int32_t* orient, int32_t* ncells, int32_t* offs);
+
+/* ---- hot path ------------------------------------------------------------------------ */
+/*
+ * Batched legal-move generation.  Replaces LegalMoveGenerator.get_legal_moves
+ * (engine/move_generator.py:130) for n (state, player) pairs.
+ *   out_rows  : n x 91 x 20 uint32, bit c of row r = anchor (r, c) legal for that
+ *               orientation (anchor = top-left of the orientation's bounding box,
+ *               exactly Move.anchor_row/anchor_col); may be NULL (counts only)
+ *   out_count : n uint32 total legal moves (len(get_legal_moves)); may be NULL
+ * players[i] in 0..3.  All pointers share residency `mem`.
+ */
+int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int32_t n,
+               uint32_t* out_rows, uint32_t* out_count, int mem);
+
+/* has_legal_moves for all 4 players of n states (move_generator.py:961): out_mask4[i]
+   bit p set if player p has a legal move. */
+int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_mask4, int mem);
+
+/*
+ * Random playouts.  For playout i = 0..n_playouts-1 start from
+ * roots[root_index[i]] (root_index may be NULL: i % n_roots) and play to the end
+ * under cfg.  compat_seeds (BK_RNG_NUMPY_MT only): n_playouts x 4 uint32 seeds, one
+ * numpy RandomState seed per seat (seats_share_stream: entry 0 is used).
+ * Replaces the inner loops of mcts/mcts_agent.py:470-554 and the arena game loop.
+ */
+int bk_rollout(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index,
+               int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
+               bk_result* out, int mem);
+
+/* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
+   stream, measured with HIP events around that launch. */
+int bk_last_kernel_ms(bk_handle h, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLOKUS_HIP_H */

@@ -1,0 +1,229 @@
+"""ctypes binding of the CPU restatement (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+The product path (reinforcementlearning_blokus_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "_build", "liboracle.so")
+
+SET_MAX = 1024
+
+
+class PySet(C.Structure):
+    _fields_ = [("mask", C.c_int32), ("fill", C.c_int32), ("used", C.c_int32),
+                ("key", C.c_int16 * SET_MAX), ("hash", C.c_int64 * SET_MAX)]
+
+
+class Board(C.Structure):
+    _fields_ = [("grid", C.c_int8 * 400), ("used", C.c_uint32 * 4), ("first", C.c_uint8 * 4),
+                ("cur", C.c_int32), ("move_count", C.c_int32), ("game_over", C.c_int32),
+                ("fr", PySet * 4)]
+
+
+class State(C.Structure):
+    _fields_ = [("planes", (C.c_uint64 * 7) * 4), ("used", C.c_uint32 * 4), ("first_move", C.c_uint8),
+                ("current_player", C.c_uint8), ("out_mask", C.c_uint8), ("flags", C.c_uint8),
+                ("move_count", C.c_uint16), ("reserved16", C.c_uint16), ("reserved", C.c_uint32 * 2)]
+
+
+class Result(C.Structure):
+    _fields_ = [("scores", C.c_int16 * 4), ("winner_mask", C.c_uint8), ("status", C.c_uint8),
+                ("plies", C.c_uint16), ("passes", C.c_uint16), ("turns", C.c_uint16),
+                ("reward", C.c_int32), ("draws", C.c_uint32), ("reserved", C.c_uint32 * 2)]
+
+
+class MT(C.Structure):
+    _fields_ = [("mt", C.c_uint32 * 624), ("mti", C.c_int32)]
+
+
+assert C.sizeof(State) == 256 and C.sizeof(Result) == 32
+
+ORDER_NAIVE, ORDER_FRONTIER = 0, 1
+SEM_ARENA, SEM_ROLLOUT = 0, 1
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = C.CDLL(_SO)
+        P = C.POINTER
+        sig = {
+            "or_init": (C.c_int, []),
+            "or_num_orients": (C.c_int, []),
+            "or_orient": (C.c_int, [C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
+            "or_board_init": (None, [P(Board)]),
+            "or_board_copy": (None, [P(Board), P(Board)]),
+            "or_place_cells": (C.c_int, [P(Board), C.c_int, C.c_int, P(C.c_int32), C.c_int]),
+            "or_place_move": (C.c_int, [P(Board), C.c_int, C.c_int]),
+            "or_legal_moves": (C.c_int, [P(Board), C.c_int, C.c_int, P(C.c_int32), C.c_int]),
+            "or_has_moves": (C.c_int, [P(Board), C.c_int]),
+            "or_board_score": (C.c_int, [P(Board), C.c_int]),
+            "or_game_scores": (None, [P(Board), P(C.c_int32), P(C.c_int32)]),
+            "or_frontier_list": (C.c_int, [P(Board), C.c_int, P(C.c_int32), C.c_int]),
+            "or_pack_state": (None, [P(Board), P(State)]),
+            "or_unpack_state": (C.c_int, [P(Board), P(State), P(C.c_int32), P(C.c_int32)]),
+            "or_mt_seed_numpy": (None, [P(MT), C.c_uint32]),
+            "or_mt_seed_python": (None, [P(MT), P(C.c_uint32), C.c_int]),
+            "or_mt_next": (C.c_uint32, [P(MT)]),
+            "or_np_randint": (C.c_int64, [P(MT), C.c_int64]),
+            "or_np_uint64": (C.c_uint64, [P(MT)]),
+            "or_py_random": (C.c_double, [P(MT)]),
+            "or_py_randbelow": (C.c_int64, [P(MT), C.c_int64]),
+            "or_gen_state": (C.c_int, [P(Board), C.c_int, C.c_int64, P(C.c_int32), C.c_int]),
+            "or_playout_arena": (C.c_int, [P(Board), P(C.c_uint32), C.c_int, C.c_int, P(Result),
+                                           P(C.c_int32), C.c_int]),
+            "or_rollout_a": (C.c_int, [P(Board), C.c_int, C.c_uint32, C.c_int, C.c_int,
+                                       P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
+            "or_fastmcts": (C.c_int, [P(Board), C.c_int, C.c_int64, C.c_int, C.c_int, P(C.c_int32),
+                                      P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_double), C.c_int]),
+            "or_zobrist_table": (None, [C.c_int64, P(C.c_uint64)]),
+            "or_zobrist_hash": (C.c_uint64, [P(Board), P(C.c_uint64)]),
+            "or_batch_playouts": (C.c_int, [P(State), C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
+                                            C.c_int, P(Result)]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        assert L.or_init() == 0
+        _lib = L
+    return _lib
+
+
+def _i32(n):
+    return (C.c_int32 * n)()
+
+
+def new_board():
+    b = Board()
+    lib().or_board_init(C.byref(b))
+    return b
+
+
+def copy_board(b):
+    d = Board()
+    lib().or_board_copy(C.byref(d), C.byref(b))
+    return d
+
+
+def legal_moves(b, player, order=ORDER_FRONTIER):
+    buf = _i32(91 * 400)
+    n = lib().or_legal_moves(C.byref(b), player, order, buf, 91 * 400)
+    return list(buf[:n])
+
+
+def frontier(b, player):
+    buf = _i32(SET_MAX)
+    n = lib().or_frontier_list(C.byref(b), player, buf, SET_MAX)
+    return list(buf[:n])
+
+
+def place_cells(b, player, piece_id, cells):
+    arr = (C.c_int32 * len(cells))(*cells)
+    lib().or_place_cells(C.byref(b), player, piece_id, arr, len(cells))
+
+
+def place_move(b, player, move):
+    lib().or_place_move(C.byref(b), player, move)
+
+
+def gen_state(num_moves, seed):
+    b = Board()
+    log = _i32(4096)
+    n = lib().or_gen_state(C.byref(b), num_moves, seed, log, 4096)
+    return b, list(log[:n])
+
+
+def pack(b):
+    s = State()
+    lib().or_pack_state(C.byref(b), C.byref(s))
+    return s
+
+
+def unpack(s, frontier_lists=None):
+    b = Board()
+    if frontier_lists is None:
+        lib().or_unpack_state(C.byref(b), C.byref(s), None, None)
+    else:
+        flat = [c for fl in frontier_lists for c in fl]
+        arr = (C.c_int32 * max(1, len(flat)))(*flat)
+        lens = (C.c_int32 * 4)(*[len(fl) for fl in frontier_lists])
+        lib().or_unpack_state(C.byref(b), C.byref(s), arr, lens)
+    return b
+
+
+def states_array(boards):
+    arr = (State * len(boards))()
+    for i, b in enumerate(boards):
+        lib().or_pack_state(C.byref(b), C.byref(arr[i]))
+    return arr
+
+
+def states_to_numpy(arr):
+    return np.frombuffer(bytes(arr), dtype=np.uint8).reshape(len(arr), 256).copy()
+
+
+def game_scores(b):
+    sc = _i32(4)
+    wm = C.c_int32()
+    lib().or_game_scores(C.byref(b), sc, C.byref(wm))
+    return list(sc), wm.value
+
+
+def board_score(b, p):
+    return lib().or_board_score(C.byref(b), p)
+
+
+def playout_arena(b, seeds, order=ORDER_FRONTIER, max_turns=2500):
+    res = Result()
+    tr = _i32(4096)
+    s = (C.c_uint32 * 4)(*seeds)
+    n = lib().or_playout_arena(C.byref(b), s, order, max_turns, C.byref(res), tr, 4096)
+    return res, list(tr[:n])
+
+
+def rollout_a(b, player, seed, order=ORDER_FRONTIER, max_moves=50):
+    rw, pl, dr = C.c_int32(), C.c_int32(), C.c_int32()
+    lib().or_rollout_a(C.byref(b), player, seed, order, max_moves, C.byref(rw), C.byref(pl), C.byref(dr))
+    return rw.value, pl.value
+
+
+def fastmcts(b, player, seed, iterations, order=ORDER_FRONTIER, top=10):
+    mv, nodes = C.c_int32(), C.c_int32()
+    tm, tv, tq = _i32(top), _i32(top), (C.c_double * top)()
+    k = lib().or_fastmcts(C.byref(b), player, seed, iterations, order, C.byref(mv), C.byref(nodes),
+                          tm, tv, tq, top)
+    return mv.value, nodes.value, [(tm[i], tv[i], tq[i]) for i in range(k)]
+
+
+def orient_table():
+    out = []
+    for g in range(lib().or_num_orients()):
+        pid, o, n = C.c_int32(), C.c_int32(), C.c_int32()
+        offs = _i32(10)
+        lib().or_orient(g, C.byref(pid), C.byref(o), C.byref(n), offs)
+        out.append((pid.value, o.value, [(offs[2 * k], offs[2 * k + 1]) for k in range(n.value)]))
+    return out
+
+
+def batch_playouts(states, n_playouts, seed, semantics=SEM_ARENA, max_plies=2500, threads=1):
+    out = (Result * n_playouts)()
+    lib().or_batch_playouts(states, len(states), n_playouts, seed, semantics, max_plies, threads, out)
+    return out
