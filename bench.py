@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Headline benchmark: MCTS random-rollout simulations/sec (20x20, 4 players).
+
+One "step" = one batch of the config-3 workload (BASELINE.json configs[2]):
+256 concurrent self-play games, 1,024 random rollouts per game-move, i.e. 262,144
+terminal random playouts (arena semantics: pass when stuck, game over when nobody
+can move, GameResult scoring) from 256 synthetic mid-game positions (20 random
+plies from the empty board), all resident in HBM before the timed region.
+
+N>1: one process per GPU (torchrun), each rank plays its own 256 games (weak
+scaling, no data-path collective); after the timed region the per-rank result
+checksums are all-gathered over RCCL.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MCTS random-rollout simulations/sec (20x20, 4p) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# VALU int32 peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one 32-bit op per lane-cycle)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--games", type=int, default=256)
+    ap.add_argument("--rollouts", type=int, default=1024)
+    ap.add_argument("--root-plies", type=int, default=20)
+    ap.add_argument("--seed", type=int, default=20260301)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(roots_np, seconds: float):
+    """Oracle (C restatement, reference frontier algorithm + game-over check after every
+    move) timed on this host's cores on a bounded sample of the same workload."""
+    from oracle import pyoracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    st = (O.State * len(roots_np)).from_buffer_copy(roots_np.tobytes())
+    n = 16 * threads
+    t0 = time.perf_counter()
+    O.batch_playouts(st, n, 1, threads=threads)
+    dt = time.perf_counter() - t0
+    # scale the sample to ~`seconds` of wall time
+    n2 = max(n, int(n * seconds / max(dt, 1e-3)))
+    t0 = time.perf_counter()
+    O.batch_playouts(st, n2, 2, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port",
+            "sample": f"{n2} arena playouts from the same {len(roots_np)} roots, "
+                      f"oracle/blokus_oracle.c (reference frontier movegen order), {threads} threads, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU, empty_state
+
+    gpu = BlokusGPU(local)
+    dev = torch.device("cuda", local)
+    seed = args.seed + 1_000_003 * rank
+    # synthetic mid-game roots, generated on the GPU (BK_SEM_ADVANCE from the empty board)
+    roots_np = gpu.advance(empty_state(), args.games, args.root_plies, seed=seed,
+                           root_index=np.zeros(args.games, dtype=np.int32))
+    roots = torch.from_numpy(roots_np.view(np.uint8).reshape(args.games, 256)).to(dev)
+    n = args.games * args.rollouts
+    idx = torch.arange(n, dtype=torch.int32, device=dev) % args.games
+    out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+
+    def step(k):
+        gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k, root_index=idx,
+                    out=out)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = []
+    plies = 0
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(1000 + k)
+        kernel_ms.append(gpu.last_kernel_ms())
+        plies += int(out.view(-1, 32)[:, 10:12].contiguous().view(torch.int16).to(torch.int64).sum().item())
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tot = torch.tensor([n * args.steps, plies], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        # RCCL gather of terminal-result checksums (32 B/playout results stay on device)
+        chk = out.view(torch.int32).to(torch.int64).sum().view(1)
+        gathered = [torch.zeros_like(chk) for _ in range(world)]
+        dist.all_gather(gathered, chk)
+    elapsed = float(t.item())
+    sims, all_plies = float(tot[0].item()), float(tot[1].item())
+    value = sims / elapsed
+
+    if rank == 0:
+        avg_ms = sum(kernel_ms) / len(kernel_ms)
+        plies_per_sim = all_plies / sims
+        # SURVEY 8(d) algorithmic bytes: 256 B state read + 256 B write per ply, 32 B result
+        bytes_per_sim = 512.0 * plies_per_sim + 32.0
+        achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
+        traffic = None
+        tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+        if os.path.exists(tpath):
+            try:
+                traffic = json.load(open(tpath)).get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        # VALU view: measured int ops per movegen x movegens per launch
+        ops_per_movegen = 20_000.0
+        movegens = n * (plies_per_sim + 4)
+        valu_tops = movegens * ops_per_movegen / (avg_ms * 1e-3) / 1e12
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "sims/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "config3: 256 concurrent games x 1024 random rollouts (arena semantics, "
+                                   "naive move order, Philox RNG) from GPU-generated 20-ply positions",
+                       "games": args.games, "rollouts_per_game": args.rollouts, "root_plies": args.root_plies,
+                       "playouts_per_step": n, "parallelism": f"dp{world} (independent games per rank)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_rollout", "kernel_ms": avg_ms, "plies_per_sim": plies_per_sim},
+            "compute_roofline": {"bound": "valu_int32", "achieved": valu_tops, "peak": VALU_PEAK_TOPS,
+                                 "unit": "Tops/s", "frac": valu_tops / VALU_PEAK_TOPS,
+                                 "ops_per_movegen": ops_per_movegen},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(roots_np, args.cpu_seconds)
+            line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -67,6 +67,9 @@ typedef struct bk_state {
 #define BK_SEM_ARENA 0  /* B: pass when stuck, terminal when nobody can move;
                            analytics/tournament/arena_runner.py:652-697 + engine/game.py:182-349 */
 #define BK_SEM_ROLLOUT 1 /* A: MCTSAgent._rollout, mcts/mcts_agent.py:470-554 (cap, break, delta) */
+#define BK_SEM_ADVANCE 2 /* play max_plies random moves (pass when stuck, stop early when nobody
+                            can move) and return the reached state: the batched analogue of
+                            tests/utils_game_states.py:12-57 generate_random_valid_state      */
 
 /* Legal-move list order used to turn a random index into a move */
 #define BK_ORDER_NAIVE 0    /* piece asc, orientation asc, anchor row-major:
@@ -150,6 +153,12 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
 int bk_rollout(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index,
                int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
                bk_result* out, int mem);
+
+/* BK_SEM_ADVANCE: like bk_rollout but writes the final state of every playout to
+   out_states (n_playouts records); out may be NULL. */
+int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index,
+               int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
+               bk_state* out_states, int mem);
 
 /* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
    stream, measured with HIP events around that launch. */

@@ -1,0 +1,199 @@
+"""ctypes binding of the HIP C-ABI (include/blokus_hip.h).
+
+The shared library is built in-tree (``_lib/libblokus_hip.so``) by
+``reinforcementlearning_blokus_amd.build.build_native()`` / ``__graft_entry__.build()``.
+There is no CPU fallback: if the library or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libblokus_hip.so")
+
+OK, EINVAL, EHIP, ENOMEM, EOVERFLOW = 0, -1, -2, -3, -4
+MEM_HOST, MEM_DEVICE = 0, 1
+SEM_ARENA, SEM_ROLLOUT, SEM_ADVANCE = 0, 1, 2
+ORDER_NAIVE, ORDER_FRONTIER = 0, 1
+RNG_PHILOX, RNG_NUMPY_MT = 0, 1
+N_ORIENTS = 91
+
+# every symbol include/blokus_hip.h declares
+EXPORTS = (
+    "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream",
+    "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
+    "bk_rollout", "bk_advance", "bk_last_kernel_ms",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    """The HIP library is not built / cannot be loaded / no GPU.  Never silently bypassed."""
+
+
+class BkState(C.Structure):
+    _fields_ = [("planes", (C.c_uint64 * 7) * 4), ("used", C.c_uint32 * 4), ("first_move", C.c_uint8),
+                ("current_player", C.c_uint8), ("out_mask", C.c_uint8), ("flags", C.c_uint8),
+                ("move_count", C.c_uint16), ("reserved16", C.c_uint16), ("reserved", C.c_uint32 * 2)]
+
+
+class BkResult(C.Structure):
+    _fields_ = [("scores", C.c_int16 * 4), ("winner_mask", C.c_uint8), ("status", C.c_uint8),
+                ("plies", C.c_uint16), ("passes", C.c_uint16), ("turns", C.c_uint16),
+                ("reward", C.c_int32), ("draws", C.c_uint32), ("reserved", C.c_uint32 * 2)]
+
+
+class BkRolloutCfg(C.Structure):
+    _fields_ = [("semantics", C.c_int32), ("order", C.c_int32), ("rng", C.c_int32), ("max_plies", C.c_int32),
+                ("seed", C.c_uint64), ("seats_share_stream", C.c_int32), ("reserved", C.c_int32)]
+
+
+assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRolloutCfg) == 32
+
+# numpy views of the same records
+import numpy as np  # noqa: E402
+
+STATE_DTYPE = np.dtype([("planes", "<u8", (4, 7)), ("used", "<u4", (4,)), ("first_move", "u1"),
+                        ("current_player", "u1"), ("out_mask", "u1"), ("flags", "u1"),
+                        ("move_count", "<u2"), ("reserved16", "<u2"), ("reserved", "<u4", (2,))])
+RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("status", "u1"),
+                         ("plies", "<u2"), ("passes", "<u2"), ("turns", "<u2"), ("reward", "<i4"),
+                         ("draws", "<u4"), ("reserved", "<u4", (2,))])
+assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load():
+    """Load libblokus_hip.so and declare the C signatures.  Raises NativeUnavailable."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeUnavailable(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        try:
+            L = C.CDLL(LIB_PATH)
+        except OSError as e:  # pragma: no cover - environment specific
+            raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        P, vp = C.POINTER, C.c_void_p
+        sigs = {
+            "bk_abi_version": (C.c_int, []),
+            "bk_tables_version": (C.c_int, []),
+            "bk_create": (C.c_int, [C.c_int, C.c_uint32, P(vp)]),
+            "bk_destroy": (C.c_int, [vp]),
+            "bk_set_stream": (C.c_int, [vp, vp]),
+            "bk_synchronize": (C.c_int, [vp]),
+            "bk_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
+            "bk_orient_info": (C.c_int, [C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
+            "bk_movegen": (C.c_int, [vp, vp, vp, C.c_int32, vp, vp, C.c_int]),
+            "bk_has_moves": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int]),
+            "bk_rollout": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
+            "bk_advance": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
+            "bk_last_kernel_ms": (C.c_int, [vp, P(C.c_float)]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+        return L
+
+
+def orient_table():
+    """[(piece_id, orientation, [(dr, dc), ...])] for g = 0..90 (host-side table query)."""
+    L = load()
+    out = []
+    for g in range(N_ORIENTS):
+        pid, o, n = C.c_int32(), C.c_int32(), C.c_int32()
+        offs = (C.c_int32 * 10)()
+        if L.bk_orient_info(g, C.byref(pid), C.byref(o), C.byref(n), offs) != OK:
+            raise NativeUnavailable("bk_orient_info failed")
+        out.append((pid.value, o.value, [(offs[2 * k], offs[2 * k + 1]) for k in range(n.value)]))
+    return out
+
+
+class Handle:
+    """One bk_handle: a HIP stream + scratch on one device.  Use one per host thread."""
+
+    def __init__(self, device: int = 0):
+        L = load()
+        h = C.c_void_p()
+        rc = L.bk_create(device, 0, C.byref(h))
+        if rc != OK or not h.value:
+            raise NativeUnavailable(f"bk_create(device={device}) failed with {rc} (no usable GPU?)")
+        self._L, self._h, self.device = L, h, device
+        self._lock = threading.Lock()
+
+    def close(self):
+        if self._h is not None and self._h.value:
+            self._L.bk_destroy(self._h)
+        self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ptr(self):
+        return self._h
+
+    def error(self) -> str:
+        buf = C.create_string_buffer(512)
+        self._L.bk_last_error(self._h, buf, 512)
+        return buf.value.decode(errors="replace")
+
+    def check(self, rc: int, what: str):
+        if rc != OK:
+            raise RuntimeError(f"{what} failed ({rc}): {self.error()}")
+
+    def set_stream(self, stream_ptr: int | None):
+        self.check(self._L.bk_set_stream(self._h, C.c_void_p(stream_ptr or 0)), "bk_set_stream")
+
+    def synchronize(self):
+        self.check(self._L.bk_synchronize(self._h), "bk_synchronize")
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        self.check(self._L.bk_last_kernel_ms(self._h, C.byref(ms)), "bk_last_kernel_ms")
+        return float(ms.value)
+
+    # -- hot path -------------------------------------------------------------------
+    def movegen(self, states_ptr, players_ptr, n, rows_ptr, count_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_movegen(self._h, C.c_void_p(states_ptr), C.c_void_p(players_ptr), n,
+                                    C.c_void_p(rows_ptr or 0), C.c_void_p(count_ptr or 0), mem)
+        self.check(rc, "bk_movegen")
+
+    def has_moves(self, states_ptr, n, out_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_has_moves(self._h, C.c_void_p(states_ptr), n, C.c_void_p(out_ptr), mem)
+        self.check(rc, "bk_has_moves")
+
+    def rollout(self, roots_ptr, n_roots, index_ptr, n_playouts, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_rollout(self._h, C.c_void_p(roots_ptr), n_roots, C.c_void_p(index_ptr or 0),
+                                    n_playouts, C.byref(cfg), C.c_void_p(seeds_ptr or 0), C.c_void_p(out_ptr), mem)
+        self.check(rc, "bk_rollout")
+
+    def advance(self, roots_ptr, n_roots, index_ptr, n, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_advance(self._h, C.c_void_p(roots_ptr), n_roots, C.c_void_p(index_ptr or 0), n,
+                                    C.byref(cfg), C.c_void_p(seeds_ptr or 0), C.c_void_p(out_ptr), mem)
+        self.check(rc, "bk_advance")
+
+
+_default = {}
+
+
+def default_handle(device: int = 0) -> Handle:
+    key = (threading.get_ident(), device)
+    h = _default.get(key)
+    if h is None:
+        h = Handle(device)
+        _default[key] = h
+    return h

@@ -1,0 +1,966 @@
+// blokus_kernels.hip -- MI355X (gfx950) kernels + C-ABI for the Blokus hot path.
+//
+// Replaces, for batches of independent 20x20 4-player boards:
+//   engine/move_generator.py:130-559  LegalMoveGenerator.get_legal_moves (legal SET)
+//   engine/move_generator.py:961-1054 has_legal_moves
+//   mcts/mcts_agent.py:470-554        MCTSAgent._rollout          (BK_SEM_ROLLOUT)
+//   analytics/tournament/arena_runner.py:652-697 game loop        (BK_SEM_ARENA)
+//   engine/game.py:182-349            game over / GameResult scoring
+//
+// Design (DESIGN.md has the full story):
+//   * one lane = one board (one game); 64 games per wave, all control flow uniform
+//     except per-game data.  No MFMA: this is integer bit work on the VALU.
+//   * board rows are 32-bit words with column x at bit (31 - x) ("reversed" layout);
+//     the 12 low bits model the off-board columns 20..31.  A legal anchor set of one
+//     orientation for all 20 anchor columns of one anchor row is then
+//         ok[r] = ~OR_cells(B[r+d] << c) & OR_cells(C[r+d] << c)
+//     with B = blocked cells (occupied | orth-adjacent-to-own | off-board) and
+//     C = corner cells (frontier).  Each cell term is ONE v_lshl_or_b32.
+//   * the 20 board rows live in VGPRs (static index); the orientation/cell loop is a
+//     runtime loop over a __constant__ stencil table with uniform (SGPR) operands; the
+//     only runtime-row index (cell row d in 0..4) is resolved by a uniform switch.
+//   * per-orientation prefix counts go to LDS ([orient][lane], u16) so that a
+//     uniform random index can be mapped back to (orientation, row, column) in the
+//     reference's naive list order without storing any mask.
+//   * the rollout kernel is persistent: each lane pulls playouts from a global
+//     counter, keeps its board in a lane-strided scratch slab (L2-resident rows),
+//     and never returns to the host between plies.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <new>
+
+#include "../../include/blokus_hip.h"
+#include "orient_table.h"
+
+#define BK_TABLES_VERSION 1
+#define WAVE 64
+#define BLOCK 256
+#define ROWMASK 0xFFFFF000u  // columns 0..19 in reversed layout
+#define OFFBOARD 0x00000FFFu // columns 20..31
+
+__constant__ uint32_t kInfo[BK_NUM_ORIENTS] = BK_ORIENT_INFO_INIT;
+__constant__ uint32_t kCells[BK_NUM_ORIENTS][5] = BK_ORIENT_CELLS_INIT;
+__constant__ uint32_t kRows[BK_NUM_ORIENTS][5] = BK_ORIENT_ROWS_INIT;
+
+// ------------------------------------------------------------------------------------
+// state <-> rows
+// ------------------------------------------------------------------------------------
+// Extract row R (bits 20R..20R+19 of the 400-bit little-endian player int) and reverse
+// it: column c -> bit 31-c.
+__device__ __forceinline__ uint32_t plane_row(const uint64_t* w, int R) {
+    const int bit = 20 * R, word = bit >> 6, off = bit & 63;
+    uint64_t v = w[word] >> off;
+    if (off > 44) v |= w[word + 1] << (64 - off);
+    return __builtin_bitreverse32((uint32_t)(v & 0xFFFFFull));
+}
+
+// Slab: one contiguous 464-byte record per lane (own planes, occupancy, compat RNG).
+// All offsets are compile-time immediates from one per-lane base (the mover plane
+// adds one per-lane term), rows move as dwordx4; the record stays L1/L2-resident.
+#define SLAB_FIELDS 5
+#define SLAB_RNG_BASE (SLAB_FIELDS * 20)
+#define SLAB_WORDS (SLAB_RNG_BASE + 16)
+struct Slab {
+    uint32_t* base;  // = slab + slot * SLAB_WORDS (16-byte aligned)
+    __device__ __forceinline__ uint32_t& at(int f, int R) const { return base[f * 20 + R]; }
+    __device__ __forceinline__ uint32_t& word(int w) const { return base[w]; }
+};
+
+// ------------------------------------------------------------------------------------
+// derive the mover's blocked / corner rows (engine/board.py:136-220 rules,
+// frontier definition engine/board.py:247-313)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void derive_rows(const uint32_t (&own)[20], const uint32_t (&occ)[20],
+                                            bool first, int p, uint32_t (&B)[20], uint32_t (&C)[20]) {
+    // start corners: RED (0,0) BLUE (0,19) YELLOW (19,19) GREEN (19,0)
+    const int crow = (p == 0 || p == 1) ? 0 : 19;
+    const uint32_t cbit = (p == 0 || p == 3) ? 0x80000000u : 0x00001000u;
+#pragma unroll
+    for (int R = 0; R < 20; ++R) {
+        const uint32_t up = R > 0 ? own[R - 1] : 0u;
+        const uint32_t dn = R < 19 ? own[R + 1] : 0u;
+        const uint32_t orth = own[R] | (own[R] << 1) | (own[R] >> 1) | up | dn;
+        const uint32_t vd = up | dn;
+        const uint32_t diag = ((vd << 1) | (vd >> 1)) & ROWMASK;
+        const uint32_t blocked = occ[R] | orth | OFFBOARD;
+        B[R] = blocked;
+        const uint32_t cf = (R == crow) ? (cbit & ~occ[R]) : 0u;
+        C[R] = first ? cf : (diag & ~blocked);
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// the stencil scan
+// ------------------------------------------------------------------------------------
+template <int D>
+__device__ __forceinline__ void acc_cell(uint32_t (&ab)[20], uint32_t (&ac)[20], const uint32_t (&B)[20],
+                                         const uint32_t (&C)[20], uint32_t c) {
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        if (r + D < 20) {
+            ab[r] |= B[r + D] << c;
+            ac[r] |= C[r + D] << c;
+        } else {
+            ab[r] = 0xFFFFFFFFu;  // a cell would fall below row 19
+        }
+    }
+}
+
+// cells of piece row D (uniform word w = ncells << 16 | col_j << 3j), j >= j0
+template <int D>
+__device__ __forceinline__ void acc_row(uint32_t (&ab)[20], uint32_t (&ac)[20], const uint32_t (&B)[20],
+                                        const uint32_t (&C)[20], uint32_t w, int j0) {
+    const int m = (int)(w >> 16);
+#pragma unroll 1
+    for (int j = j0; j < m; ++j) acc_cell<D>(ab, ac, B, C, (w >> (3 * j)) & 7u);
+}
+
+// Legal-anchor scan of one orientation g (uniform).  ok[r] = legal anchors of anchor
+// row r, reversed layout.  The piece-row index D is a template parameter of five
+// separate uniform loops (no switch: a switch gets tail-merged by the compiler into
+// register copies that cost as much as the stencil work itself).
+__device__ __forceinline__ void scan_orient(int g, const uint32_t (&B)[20], const uint32_t (&C)[20],
+                                            uint32_t (&ok)[20]) {
+    uint32_t ab[20], ac[20];
+    const uint32_t w0 = kRows[g][0];
+    const uint32_t c0 = w0 & 7u;  // piece row 0 is never empty
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        ab[r] = B[r] << c0;
+        ac[r] = C[r] << c0;
+    }
+    acc_row<0>(ab, ac, B, C, w0, 1);
+    acc_row<1>(ab, ac, B, C, kRows[g][1], 0);
+    acc_row<2>(ab, ac, B, C, kRows[g][2], 0);
+    acc_row<3>(ab, ac, B, C, kRows[g][3], 0);
+    acc_row<4>(ab, ac, B, C, kRows[g][4], 0);
+#pragma unroll
+    for (int r = 0; r < 20; ++r) ok[r] = ac[r] & ~ab[r];
+}
+
+// Full movegen for one board-player: per-orientation prefix counts to LDS
+// (cnt[g * WAVE + lane] = number of legal moves in orientations 0..g).
+__device__ __forceinline__ uint32_t movegen_prefix(const uint32_t (&B)[20], const uint32_t (&C)[20],
+                                                   uint32_t avail, uint16_t* cnt, int lane) {
+    uint32_t total = 0;
+#pragma unroll 1
+    for (int g = 0; g < BK_NUM_ORIENTS; ++g) {
+        uint32_t ok[20];
+        scan_orient(g, B, C, ok);
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < 20; ++r) c += __builtin_popcount(ok[r]);
+        const uint32_t piece = kInfo[g] & 0xFFu;
+        total += ((avail >> (piece - 1)) & 1u) ? c : 0u;
+        cnt[g * WAVE + lane] = (uint16_t)total;
+    }
+    return total;
+}
+
+// Recompute orientation gs (per-lane, divergent) row r_ok values with per-lane
+// row selects, then locate the kk-th legal move in naive order (anchor row-major).
+__device__ __forceinline__ void locate_move(int gs, uint32_t kk, const uint32_t (&B)[20],
+                                            const uint32_t (&C)[20], int& out_r, int& out_c) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    uint32_t cd[5], cc[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k];
+        cd[k] = cell >> 8;
+        cc[k] = cell & 0xFFu;
+    }
+    int found_r = -1, found_c = 0;
+    uint32_t rem = kk;
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        uint32_t ab = 0, ac = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k < n) {
+                const uint32_t d = cd[k];
+                uint32_t b = 0xFFFFFFFFu, cv = 0u;
+#pragma unroll
+                for (int dd = 0; dd < 5; ++dd)
+                    if (r + dd < 20 && d == (uint32_t)dd) { b = B[r + dd]; cv = C[r + dd]; }
+                ab |= b << cc[k];
+                ac |= cv << cc[k];
+            }
+        }
+        const uint32_t ok = ac & ~ab;
+        const uint32_t pc = __builtin_popcount(ok);
+        if (found_r < 0) {
+            if (rem < pc) {
+                // rem-th set bit from the top (column ascending)
+                uint32_t x = ok;
+                for (uint32_t j = 0; j < rem; ++j) x &= ~(0x80000000u >> __builtin_clz(x));
+                found_r = r;
+                found_c = __builtin_clz(x);
+            } else {
+                rem -= pc;
+            }
+        }
+    }
+    out_r = found_r;
+    out_c = found_c;
+}
+
+// ------------------------------------------------------------------------------------
+// random streams
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t philox_u32(uint32_t c0, uint32_t c1, uint64_t key) {
+    uint32_t x0 = c0, x1 = c1, x2 = 0x5bd1e995u, x3 = 0u;
+    uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, x0), lo0 = 0xD2511F53u * x0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, x2), lo1 = 0xCD9E8D57u * x2;
+        const uint32_t y0 = hi1 ^ x1 ^ k0, y2 = hi0 ^ x3 ^ k1;
+        x0 = y0; x1 = lo1; x2 = y2; x3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return x0;
+}
+
+__device__ __forceinline__ uint32_t mask_for(uint32_t rng) {
+    uint32_t m = rng;
+    m |= m >> 1; m |= m >> 2; m |= m >> 4; m |= m >> 8; m |= m >> 16;
+    return m;
+}
+
+__device__ __forceinline__ uint32_t mt_init_step(uint32_t x, uint32_t j) {
+    return 1812433253u * (x ^ (x >> 30)) + j;
+}
+
+// numpy RandomState(seed) MT19937 stream restricted to its first 227 outputs, which
+// need only the init_genrand sequence (no stored 624-word state): output i =
+// temper(mt[i+397] ^ twist(mt[i], mt[i+1])).  (agents/random_agent.py:29,49)
+struct MtCursor {
+    uint32_t i, a, b, c;  // a = mt[i], b = mt[i+1], c = mt[i+397]
+};
+
+__device__ __forceinline__ MtCursor mt_cursor_init(uint32_t seed) {
+    MtCursor m;
+    m.i = 0; m.a = seed;
+    m.b = mt_init_step(seed, 1);
+    uint32_t x = m.b;
+    for (uint32_t j = 2; j <= 397; ++j) x = mt_init_step(x, j);
+    m.c = x;
+    return m;
+}
+
+__device__ __forceinline__ uint32_t mt_cursor_next(MtCursor& m, bool& overflow) {
+    if (m.i >= 227u) overflow = true;
+    const uint32_t y = (m.a & 0x80000000u) | (m.b & 0x7fffffffu);
+    uint32_t v = m.c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    v ^= v >> 11; v ^= (v << 7) & 0x9d2c5680u; v ^= (v << 15) & 0xefc60000u; v ^= v >> 18;
+    m.i += 1;
+    m.a = m.b;
+    m.b = mt_init_step(m.b, m.i + 1);
+    m.c = mt_init_step(m.c, m.i + 397);
+    return v;
+}
+
+// ------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------
+struct MovegenArgs {
+    const bk_state* states;
+    const uint8_t* players;  // NULL: all 4 players of each state (has_moves mode)
+    int32_t n;
+    uint32_t* out_rows;      // n x 91 x 20 (normal layout, bit c = column c) or NULL
+    uint32_t* out_count;     // n or NULL
+    uint8_t* out_mask4;      // has_moves mode
+};
+
+__device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&own)[4][20], uint32_t (&occ)[20]) {
+#pragma unroll
+    for (int R = 0; R < 20; ++R) occ[R] = 0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            own[p][R] = plane_row(s->planes[p], R);
+            occ[R] |= own[p][R];
+        }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
+    __shared__ uint16_t cnt[BK_NUM_ORIENTS * WAVE * (BLOCK / WAVE)];
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    uint16_t* my = cnt + wv * BK_NUM_ORIENTS * WAVE;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool live = i < a.n;
+    const int idx = live ? i : 0;
+    const bk_state* s = a.states + idx;
+    const int p = a.players ? (a.players[idx] & 3) : 0;
+    uint32_t B[20], C[20], own[20], occ[20];
+#pragma unroll
+    for (int R = 0; R < 20; ++R) { occ[R] = 0; own[R] = 0; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            const uint32_t row = plane_row(s->planes[q], R);
+            occ[R] |= row;
+            own[R] |= (q == p) ? row : 0u;
+        }
+    derive_rows(own, occ, (s->first_move >> p) & 1u, p, B, C);
+    const uint32_t avail = ~s->used[p] & 0x1FFFFFu;
+    if (a.out_rows == nullptr) {
+        const uint32_t total = movegen_prefix(B, C, avail, my, lane);
+        if (live && a.out_count) a.out_count[i] = total;
+        return;
+    }
+    uint32_t total = 0;
+#pragma unroll 1
+    for (int g = 0; g < BK_NUM_ORIENTS; ++g) {
+        uint32_t ok[20];
+        scan_orient(g, B, C, ok);
+        const uint32_t piece = kInfo[g] & 0xFFu;
+        const bool av = (avail >> (piece - 1)) & 1u;
+        uint32_t c = 0;
+        uint4* dst = reinterpret_cast<uint4*>(a.out_rows + ((size_t)idx * BK_NUM_ORIENTS + g) * 20);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            uint4 v;
+            v.x = av ? __builtin_bitreverse32(ok[4 * q + 0]) : 0u;
+            v.y = av ? __builtin_bitreverse32(ok[4 * q + 1]) : 0u;
+            v.z = av ? __builtin_bitreverse32(ok[4 * q + 2]) : 0u;
+            v.w = av ? __builtin_bitreverse32(ok[4 * q + 3]) : 0u;
+            c += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) +
+                 __builtin_popcount(v.w);
+            if (live) dst[q] = v;
+        }
+        total += c;
+    }
+    if (live && a.out_count) a.out_count[i] = total;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
+    __shared__ uint16_t cnt[BK_NUM_ORIENTS * WAVE * (BLOCK / WAVE)];
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    uint16_t* my = cnt + wv * BK_NUM_ORIENTS * WAVE;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool live = i < a.n;
+    const bk_state* s = a.states + (live ? i : 0);
+    uint32_t own[4][20], occ[20];
+    load_state_rows(s, own, occ);
+    uint8_t mask = 0;
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+        uint32_t ow[20], B[20], C[20];
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            uint32_t v = own[0][R];
+            v = p == 1 ? own[1][R] : v;
+            v = p == 2 ? own[2][R] : v;
+            v = p == 3 ? own[3][R] : v;
+            ow[R] = v;
+        }
+        derive_rows(ow, occ, (s->first_move >> p) & 1u, p, B, C);
+        const uint32_t total = movegen_prefix(B, C, ~s->used[p] & 0x1FFFFFu, my, lane);
+        mask |= (uint8_t)((total > 0) << p);
+    }
+    if (live) a.out_mask4[i] = mask;
+}
+
+struct RolloutArgs {
+    const bk_state* roots;
+    int32_t n_roots;
+    const int32_t* root_index;
+    int32_t n_playouts;
+    bk_rollout_cfg cfg;
+    const uint32_t* compat_seeds;
+    bk_result* out;
+    uint32_t* slab;
+    uint32_t nslots;
+    uint32_t* counter;  // [0] = next playout; [1] = error word
+    uint32_t max_iters; // safety valve: loop iterations any lane can need
+    bk_state* out_states; // BK_SEM_ADVANCE
+};
+
+// four per-player scalars (kept as separate SSA values: an array indexed by a
+// per-lane player would be demoted to scratch memory)
+struct Quad {
+    uint32_t v0, v1, v2, v3;
+    __device__ __forceinline__ uint32_t get(int q) const {
+        return q == 0 ? v0 : (q == 1 ? v1 : (q == 2 ? v2 : v3));
+    }
+    __device__ __forceinline__ void set(int q, uint32_t x) {
+        v0 = q == 0 ? x : v0; v1 = q == 1 ? x : v1; v2 = q == 2 ? x : v2; v3 = q == 3 ? x : v3;
+    }
+};
+
+struct Game {
+    int32_t pid;        // playout id, -1 = none
+    Quad used;
+    uint32_t first;     // bit p
+    uint32_t out;       // bit p: known no legal move
+    int32_t cur;
+    Quad cells;         // squares covered per player
+    int32_t plies, passes, turns, since_move;
+    int32_t root_player, root_score;
+    uint32_t draws;
+    uint32_t pcount;    // philox counter
+    uint32_t move_count0;
+    bool overflow;
+};
+
+__device__ __forceinline__ int board_score_q(const Game& g, int q) {  // q static
+    return (int)g.cells.get(q) + ((g.used.get(q) == 0x1FFFFFu) ? 15 : 0);
+}
+__device__ __forceinline__ int board_score(const Game& g, int p) {  // p per-lane
+    return (int)g.cells.get(p) + ((g.used.get(p) == 0x1FFFFFu) ? 15 : 0);
+}
+
+// write the lane's board back as a bk_state (BK_SEM_ADVANCE)
+__device__ __forceinline__ void store_state(const RolloutArgs& a, const Game& g, const Slab& slab) {
+    bk_state* o = a.out_states + g.pid;
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+        uint64_t w[7] = {0, 0, 0, 0, 0, 0, 0};
+        const uint32_t* pl = slab.base + p * 20;
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            const uint64_t v = __builtin_bitreverse32(pl[R]);  // column c -> bit c
+            const int bit = 20 * R, word = bit >> 6, off = bit & 63;
+            w[word] |= v << off;
+            if (off > 44) w[word + 1] |= v >> (64 - off);
+        }
+#pragma unroll
+        for (int k = 0; k < 7; ++k) o->planes[p][k] = w[k];
+        o->used[p] = g.used.get(p);
+    }
+    o->first_move = (uint8_t)g.first;
+    o->current_player = (uint8_t)g.cur;
+    o->out_mask = (uint8_t)g.out;
+    o->flags = 0;
+    o->move_count = (uint16_t)(g.move_count0 + g.plies);
+    o->reserved16 = 0;
+    o->reserved[0] = o->reserved[1] = 0;
+}
+
+__device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot) {
+    if (a.cfg.semantics == BK_SEM_ADVANCE) {
+        store_state(a, g, slab);
+        if (a.out == nullptr) { g.pid = -1; return; }
+    }
+    bk_result r;
+    memset(&r, 0, sizeof r);
+    if (a.cfg.semantics != BK_SEM_ROLLOUT) {
+        int best = -1000000;
+        Quad sc{0, 0, 0, 0};
+#pragma unroll 1
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t* pl = slab.base + p * 20;
+            const uint32_t r0 = pl[0], r19 = pl[19];
+            int s = board_score(g, p);
+            s += 5 * (int)(((r0 >> 31) & 1u) + ((r0 >> 12) & 1u) + ((r19 >> 31) & 1u) + ((r19 >> 12) & 1u));
+            uint32_t centre = 0;
+#pragma unroll
+            for (int R = 8; R < 12; ++R) centre += __builtin_popcount(pl[R] & 0x00F00000u);
+            s += 2 * (int)centre;
+            sc.set(p, (uint32_t)s);
+            best = s > best ? s : best;
+        }
+        uint8_t wm = 0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            r.scores[p] = (int16_t)(int)sc.get(p);
+            wm |= (uint8_t)(((int)sc.get(p) == best) << p);
+        }
+        r.winner_mask = wm;
+        // passes detected lazily after the final move are not counted by the reference,
+        // whose game-over check runs right after each move (engine/game.py:182-214)
+        r.passes = (uint16_t)(g.passes - g.since_move);
+        r.turns = (uint16_t)(g.turns - g.since_move);
+    } else {
+        int best = -1000000;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            r.scores[p] = (int16_t)board_score_q(g, p);
+            best = r.scores[p] > best ? r.scores[p] : best;
+        }
+        r.reward = board_score(g, g.root_player) - g.root_score;
+        r.turns = (uint16_t)g.turns;
+    }
+    r.plies = (uint16_t)g.plies;
+    r.draws = g.draws;
+    r.status = g.overflow ? 1 : 0;
+    a.out[g.pid] = r;
+    g.pid = -1;
+}
+
+__device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot, int32_t pid) {
+    const int32_t ri = a.root_index ? a.root_index[pid] : (pid % a.n_roots);
+    const bk_state* s = a.roots + ri;
+    g.pid = pid;
+    uint32_t occ[20];
+#pragma unroll
+    for (int R = 0; R < 20; ++R) occ[R] = 0;
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {  // runtime loop: keeps only one player's words live
+        uint32_t cells = 0;
+        uint64_t w[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) w[k] = s->planes[p][k];
+        uint32_t* dst = slab.base + p * 20;
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            const uint32_t row = plane_row(w, R);
+            dst[R] = row;
+            occ[R] |= row;
+            cells += __builtin_popcount(row);
+        }
+        g.cells.set(p, cells);
+        g.used.set(p, s->used[p] & 0x1FFFFFu);
+    }
+#pragma unroll
+    for (int R = 0; R < 20; ++R) slab.at(4, R) = occ[R];
+    g.first = s->first_move & 0xFu;
+    g.out = a.cfg.semantics != BK_SEM_ROLLOUT ? (s->out_mask & 0xFu) : 0u;
+    g.move_count0 = s->move_count;
+    g.cur = s->current_player & 3;
+    g.plies = g.passes = g.turns = g.since_move = 0;
+    g.root_player = g.cur;
+    g.root_score = board_score(g, g.cur);
+    g.draws = 0;
+    g.pcount = 0;
+    g.overflow = false;
+    if (a.cfg.rng == BK_RNG_NUMPY_MT) {
+        const int nstreams = a.cfg.seats_share_stream ? 1 : 4;
+        for (int q = 0; q < nstreams; ++q) {
+            const MtCursor m = mt_cursor_init(a.compat_seeds[(size_t)pid * 4 + q]);
+            slab.word(SLAB_RNG_BASE + 4 * q + 0) = m.i;
+            slab.word(SLAB_RNG_BASE + 4 * q + 1) = m.a;
+            slab.word(SLAB_RNG_BASE + 4 * q + 2) = m.b;
+            slab.word(SLAB_RNG_BASE + 4 * q + 3) = m.c;
+        }
+    }
+}
+
+// uniform index in [0, n) for the current mover; numpy legacy masked rejection
+__device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot,
+                                               uint32_t n) {
+    const uint32_t rng = n - 1u;
+    if (rng == 0u) return 0u;  // randint(0, 1) consumes no draw
+    const uint32_t mask = mask_for(rng);
+    uint32_t v;
+    if (a.cfg.rng == BK_RNG_NUMPY_MT) {
+        const int q = a.cfg.seats_share_stream ? 0 : g.cur;
+        uint32_t* base = slab.base + SLAB_RNG_BASE + 4 * q;
+        MtCursor m;
+        m.i = base[0]; m.a = base[1]; m.b = base[2]; m.c = base[3];
+        do {
+            v = mt_cursor_next(m, g.overflow) & mask;
+            g.draws++;
+        } while (v > rng && !g.overflow);
+        base[0] = m.i; base[1] = m.a; base[2] = m.b; base[3] = m.c;
+        if (v > rng) v = 0;
+    } else {
+        do {
+            v = philox_u32(g.pcount++, (uint32_t)g.pid, a.cfg.seed) & mask;
+            g.draws++;
+        } while (v > rng);
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_rollout(RolloutArgs a) {
+    __shared__ uint16_t cnt[BK_NUM_ORIENTS * WAVE * (BLOCK / WAVE)];
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    uint16_t* my = cnt + wv * BK_NUM_ORIENTS * WAVE;
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
+    const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
+    const bool advance = a.cfg.semantics == BK_SEM_ADVANCE;
+    const int32_t cap = a.cfg.max_plies;
+
+    Game g;
+    g.pid = -1;
+    bool done = false;
+    for (uint32_t iter = 0;; ++iter) {
+        // ---- make sure this lane has a game whose current player may still move
+        for (int guard = 0; guard < 3 && !done; ++guard) {
+            if (g.pid < 0) {
+                const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
+                if (next >= a.n_playouts) { done = true; break; }
+                start_game(a, g, slab, slot, next);
+            }
+            if (arena) {
+#pragma unroll 1
+                for (int s = 0; s < 4 && ((g.out >> g.cur) & 1u) && g.out != 0xFu; ++s) {
+                    g.passes++; g.turns++; g.since_move++;
+                    g.cur = (g.cur + 1) & 3;
+                }
+                if (g.out == 0xFu || (advance ? g.plies : g.turns) >= cap) {
+                    finish_game(a, g, slab, slot);
+                    continue;
+                }
+            } else if (g.plies >= cap) {
+                finish_game(a, g, slab, slot);
+                continue;
+            }
+            break;
+        }
+        if (__ballot(!done) == 0ull) break;
+        if (iter > a.max_iters) {  // safety valve: never spin forever
+            if (lane == 0) atomicOr(&a.counter[1], 1u);
+            break;
+        }
+        // ---- derive + movegen for every active lane (uniform work)
+        const bool idle = done || g.pid < 0;
+        const int p = idle ? 0 : g.cur;
+        uint32_t own[20], occ[20], B[20], C[20];
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            own[R] = idle ? 0u : slab.at(p, R);
+            occ[R] = idle ? 0u : slab.at(4, R);
+        }
+        derive_rows(own, occ, (g.first >> p) & 1u, p, B, C);
+        const uint32_t avail = idle ? 0u : (~g.used.get(p) & 0x1FFFFFu);
+        const uint32_t total = movegen_prefix(B, C, avail, my, lane);
+        if (idle) continue;
+        if (total == 0u) {
+            if (arena) {
+                g.out |= 1u << p;
+                g.passes++; g.turns++; g.since_move++;
+                g.cur = (g.cur + 1) & 3;
+            } else {
+                finish_game(a, g, slab, slot);  // MCTSAgent._rollout breaks
+            }
+            continue;
+        }
+        const uint32_t k = draw_index(a, g, slab, slot, total);
+        // orientation: first g with prefix > k
+        int lo = 0, hi = BK_NUM_ORIENTS - 1;
+#pragma unroll
+        for (int it = 0; it < 7; ++it) {
+            const int mid = (lo + hi) >> 1;
+            if ((uint32_t)my[mid * WAVE + lane] > k) hi = mid; else lo = mid + 1;
+        }
+        const int gs = lo;
+        const uint32_t before = gs > 0 ? (uint32_t)my[(gs - 1) * WAVE + lane] : 0u;
+        int ar, ac;
+        locate_move(gs, k - before, B, C, ar, ac);
+        // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
+        const uint32_t info = kInfo[gs];
+        const int n = (int)((info >> 8) & 0xFFu);
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+            if (q < n) {
+                const uint32_t cell = kCells[gs][q];
+                const int R = ar + (int)(cell >> 8);
+                const uint32_t bit = 0x80000000u >> (ac + (int)(cell & 0xFFu));
+                slab.at(p, R) |= bit;
+                slab.at(4, R) |= bit;
+            }
+        }
+        g.cells.set(p, g.cells.get(p) + (uint32_t)n);
+        g.used.set(p, g.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
+        g.first &= ~(1u << p);
+        g.plies++; g.turns++; g.since_move = 0;
+        g.cur = (g.cur + 1) & 3;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------
+struct bk_handle_s {
+    int device = 0;
+    hipStream_t own = nullptr, cur = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    char err[512] = {0};
+    // device staging / scratch
+    void* d_in = nullptr; size_t d_in_cap = 0;
+    void* d_out = nullptr; size_t d_out_cap = 0;
+    void* d_aux = nullptr; size_t d_aux_cap = 0;
+    void* d_aux2 = nullptr; size_t d_aux2_cap = 0;
+    void* d_slab = nullptr; size_t d_slab_cap = 0;
+    uint32_t* d_counter = nullptr;
+    int num_cu = 0;
+    int rollout_blocks_per_cu = 0;
+};
+
+static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
+    if (h) snprintf(h->err, sizeof h->err, fmt, detail ? detail : "");
+    return code;
+}
+
+#define HIPCHK(h, call)                                                                 \
+    do {                                                                                \
+        hipError_t _e = (call);                                                         \
+        if (_e != hipSuccess) return set_err((h), BK_EHIP, #call ": %s", hipGetErrorString(_e)); \
+    } while (0)
+
+static int grow(bk_handle h, void** p, size_t* cap, size_t need) {
+    if (need <= *cap) return BK_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr; *cap = 0;
+    size_t n = need + need / 4 + 256;
+    HIPCHK(h, hipMalloc(p, n));
+    *cap = n;
+    return BK_OK;
+}
+
+extern "C" {
+
+int bk_abi_version(void) { return BK_ABI_VERSION; }
+int bk_tables_version(void) { return BK_TABLES_VERSION; }
+
+int bk_orient_info(int g, int32_t* piece_id, int32_t* orient, int32_t* ncells, int32_t* offs) {
+    if (g < 0 || g >= BK_NUM_ORIENTS || !piece_id || !orient || !ncells || !offs) return BK_EINVAL;
+    *piece_id = (int32_t)(kOrientInfoHost[g] & 0xFF);
+    *orient = kOrientIndexHost[g];
+    *ncells = (int32_t)((kOrientInfoHost[g] >> 8) & 0xFF);
+    for (int k = 0; k < 5; ++k) {
+        offs[2 * k] = (int32_t)(kOrientCellsHost[g][k] >> 8);
+        offs[2 * k + 1] = (int32_t)(kOrientCellsHost[g][k] & 0xFF);
+    }
+    return BK_OK;
+}
+
+int bk_create(int device, uint32_t flags, bk_handle* out) {
+    (void)flags;
+    if (!out) return BK_EINVAL;
+    *out = nullptr;
+    bk_handle h = new (std::nothrow) bk_handle_s();
+    if (!h) return BK_ENOMEM;
+    h->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->own, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&h->ev0);
+    if (e == hipSuccess) e = hipEventCreate(&h->ev1);
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_counter, 4 * sizeof(uint32_t));
+    hipDeviceProp_t prop;
+    if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
+    if (e != hipSuccess) {
+        fprintf(stderr, "bk_create: %s\n", hipGetErrorString(e));
+        delete h;
+        return BK_EHIP;
+    }
+    h->num_cu = prop.multiProcessorCount;
+    int bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_rollout, BLOCK, 0) != hipSuccess || bpc < 1) bpc = 1;
+    h->rollout_blocks_per_cu = bpc;
+    h->cur = h->own;
+    *out = h;
+    return BK_OK;
+}
+
+int bk_destroy(bk_handle h) {
+    if (!h) return BK_EINVAL;
+    (void)hipSetDevice(h->device);
+    if (h->own) (void)hipStreamSynchronize(h->own);
+    void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_counter};
+    for (void* b : bufs) if (b) (void)hipFree(b);
+    if (h->ev0) (void)hipEventDestroy(h->ev0);
+    if (h->ev1) (void)hipEventDestroy(h->ev1);
+    if (h->own) (void)hipStreamDestroy(h->own);
+    delete h;
+    return BK_OK;
+}
+
+int bk_set_stream(bk_handle h, void* stream) {
+    if (!h) return BK_EINVAL;
+    h->cur = stream ? (hipStream_t)stream : h->own;
+    return BK_OK;
+}
+
+int bk_synchronize(bk_handle h) {
+    if (!h) return BK_EINVAL;
+    HIPCHK(h, hipStreamSynchronize(h->cur));
+    return BK_OK;
+}
+
+int bk_last_error(bk_handle h, char* buf, size_t len) {
+    if (!h || !buf || len == 0) return BK_EINVAL;
+    snprintf(buf, len, "%s", h->err);
+    return BK_OK;
+}
+
+int bk_last_kernel_ms(bk_handle h, float* ms) {
+    if (!h || !ms) return BK_EINVAL;
+    if (!h->timed) return set_err(h, BK_EINVAL, "no timed kernel on this handle%s", "");
+    HIPCHK(h, hipEventSynchronize(h->ev1));
+    HIPCHK(h, hipEventElapsedTime(ms, h->ev0, h->ev1));
+    return BK_OK;
+}
+
+static int stage_in(bk_handle h, const void* src, size_t bytes, int mem, void** dev, void** buf, size_t* cap) {
+    if (mem == BK_MEM_DEVICE) { *dev = const_cast<void*>(src); return BK_OK; }
+    int rc = grow(h, buf, cap, bytes);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(*buf, src, bytes, hipMemcpyHostToDevice, h->cur));
+    *dev = *buf;
+    return BK_OK;
+}
+
+int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int32_t n, uint32_t* out_rows,
+               uint32_t* out_count, int mem) {
+    if (!h || !states || !players || n < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
+        return set_err(h, BK_EINVAL, "bk_movegen: invalid arguments%s", "");
+    if (n == 0) return BK_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    void *d_states, *d_players;
+    int rc = stage_in(h, states, sizeof(bk_state) * (size_t)n, mem, &d_states, &h->d_in, &h->d_in_cap);
+    if (rc) return rc;
+    rc = stage_in(h, players, (size_t)n, mem, &d_players, &h->d_aux, &h->d_aux_cap);
+    if (rc) return rc;
+    uint32_t* d_rows = out_rows;
+    uint32_t* d_count = out_count;
+    const size_t rows_bytes = sizeof(uint32_t) * (size_t)n * BK_NUM_ORIENTS * 20;
+    if (mem == BK_MEM_HOST) {
+        rc = grow(h, &h->d_out, &h->d_out_cap, (out_rows ? rows_bytes : 0) + sizeof(uint32_t) * (size_t)n);
+        if (rc) return rc;
+        d_count = (uint32_t*)h->d_out;
+        d_rows = out_rows ? (uint32_t*)((char*)h->d_out + sizeof(uint32_t) * (size_t)n + 0) : nullptr;
+        // keep 16-byte alignment of the rows block
+        if (d_rows) d_rows = (uint32_t*)(((uintptr_t)d_rows + 15) & ~(uintptr_t)15);
+        if (d_rows) { rc = grow(h, &h->d_out, &h->d_out_cap, rows_bytes + sizeof(uint32_t) * (size_t)n + 16);
+                      if (rc) return rc;
+                      d_count = (uint32_t*)h->d_out;
+                      d_rows = (uint32_t*)(((uintptr_t)((char*)h->d_out + sizeof(uint32_t) * (size_t)n) + 15) & ~(uintptr_t)15); }
+    } else if (out_rows && ((uintptr_t)out_rows & 15)) {
+        return set_err(h, BK_EINVAL, "bk_movegen: out_rows must be 16-byte aligned%s", "");
+    }
+    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr};
+    const int grid = (n + BLOCK - 1) / BLOCK;
+    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    hipLaunchKernelGGL(k_movegen, dim3(grid), dim3(BLOCK), 0, h->cur, a);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
+    h->timed = true;
+    if (mem == BK_MEM_HOST) {
+        if (out_count) HIPCHK(h, hipMemcpyAsync(out_count, d_count, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, h->cur));
+        if (out_rows) HIPCHK(h, hipMemcpyAsync(out_rows, d_rows, rows_bytes, hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipStreamSynchronize(h->cur));
+    }
+    return BK_OK;
+}
+
+int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_mask4, int mem) {
+    if (!h || !states || !out_mask4 || n < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
+        return set_err(h, BK_EINVAL, "bk_has_moves: invalid arguments%s", "");
+    if (n == 0) return BK_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    void* d_states;
+    int rc = stage_in(h, states, sizeof(bk_state) * (size_t)n, mem, &d_states, &h->d_in, &h->d_in_cap);
+    if (rc) return rc;
+    uint8_t* d_mask = out_mask4;
+    if (mem == BK_MEM_HOST) {
+        rc = grow(h, &h->d_out, &h->d_out_cap, (size_t)n);
+        if (rc) return rc;
+        d_mask = (uint8_t*)h->d_out;
+    }
+    MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask};
+    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    hipLaunchKernelGGL(k_has_moves, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->cur, a);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
+    h->timed = true;
+    if (mem == BK_MEM_HOST) {
+        HIPCHK(h, hipMemcpyAsync(out_mask4, d_mask, (size_t)n, hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipStreamSynchronize(h->cur));
+    }
+    return BK_OK;
+}
+
+static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index,
+                           int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
+                           bk_result* out, bk_state* out_states, int mem) {
+    if (!h || !roots || !cfg || n_roots <= 0 || n_playouts < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
+        return set_err(h, BK_EINVAL, "bk_rollout: invalid arguments%s", "");
+    if (cfg->semantics != BK_SEM_ARENA && cfg->semantics != BK_SEM_ROLLOUT && cfg->semantics != BK_SEM_ADVANCE)
+        return set_err(h, BK_EINVAL, "bk_rollout: unknown semantics%s", "");
+    if ((cfg->semantics == BK_SEM_ADVANCE) != (out_states != nullptr))
+        return set_err(h, BK_EINVAL, "bk_rollout: out_states goes with BK_SEM_ADVANCE only%s", "");
+    if (!out && !out_states) return set_err(h, BK_EINVAL, "bk_rollout: no output%s", "");
+    if (cfg->order != BK_ORDER_NAIVE)
+        return set_err(h, BK_EINVAL, "bk_rollout: only BK_ORDER_NAIVE is implemented on the GPU%s", "");
+    if (cfg->rng != BK_RNG_PHILOX && cfg->rng != BK_RNG_NUMPY_MT)
+        return set_err(h, BK_EINVAL, "bk_rollout: unknown rng%s", "");
+    if (cfg->rng == BK_RNG_NUMPY_MT && !compat_seeds)
+        return set_err(h, BK_EINVAL, "bk_rollout: compat rng needs compat_seeds%s", "");
+    if (cfg->max_plies <= 0) return set_err(h, BK_EINVAL, "bk_rollout: max_plies must be > 0%s", "");
+    if (n_playouts == 0) return BK_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    void *d_roots, *d_idx = nullptr, *d_seeds = nullptr;
+    int rc = stage_in(h, roots, sizeof(bk_state) * (size_t)n_roots, mem, &d_roots, &h->d_in, &h->d_in_cap);
+    if (rc) return rc;
+    if (root_index) {
+        rc = stage_in(h, root_index, sizeof(int32_t) * (size_t)n_playouts, mem, &d_idx, &h->d_aux, &h->d_aux_cap);
+        if (rc) return rc;
+    }
+    if (cfg->rng == BK_RNG_NUMPY_MT) {
+        rc = stage_in(h, compat_seeds, sizeof(uint32_t) * 4 * (size_t)n_playouts, mem, &d_seeds, &h->d_aux2,
+                      &h->d_aux2_cap);
+        if (rc) return rc;
+    }
+    bk_result* d_out = out;
+    bk_state* d_states = out_states;
+    if (mem == BK_MEM_HOST) {
+        const size_t rb = out ? sizeof(bk_result) * (size_t)n_playouts : 0;
+        const size_t sb = out_states ? sizeof(bk_state) * (size_t)n_playouts : 0;
+        rc = grow(h, &h->d_out, &h->d_out_cap, rb + sb);
+        if (rc) return rc;
+        d_out = out ? (bk_result*)h->d_out : nullptr;
+        d_states = out_states ? (bk_state*)((char*)h->d_out + rb) : nullptr;
+    }
+    // persistent grid: every resident slot pulls playouts from the counter
+    int blocks = h->num_cu * h->rollout_blocks_per_cu;
+    const int need = (n_playouts + BLOCK - 1) / BLOCK;
+    if (blocks > need) blocks = need;
+    if (blocks < 1) blocks = 1;
+    const uint32_t nslots = (uint32_t)blocks * BLOCK;
+    rc = grow(h, &h->d_slab, &h->d_slab_cap, sizeof(uint32_t) * SLAB_WORDS * (size_t)nslots);
+    if (rc) return rc;
+    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
+    const uint64_t per_lane = ((uint64_t)n_playouts + nslots - 1) / nslots + 1;
+    const uint64_t per_game = (cfg->semantics == BK_SEM_ROLLOUT ? (uint64_t)cfg->max_plies + 2u : 100u);
+    const uint64_t iters = per_lane * per_game + 64u;
+    RolloutArgs a{(const bk_state*)d_roots, n_roots, (const int32_t*)d_idx, n_playouts, *cfg,
+                  (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
+                  (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states};
+    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    hipLaunchKernelGGL(k_rollout, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
+    h->timed = true;
+    if (mem == BK_MEM_HOST) {
+        if (out)
+            HIPCHK(h, hipMemcpyAsync(out, d_out, sizeof(bk_result) * (size_t)n_playouts, hipMemcpyDeviceToHost, h->cur));
+        if (out_states)
+            HIPCHK(h, hipMemcpyAsync(out_states, d_states, sizeof(bk_state) * (size_t)n_playouts,
+                                     hipMemcpyDeviceToHost, h->cur));
+        uint32_t ctr[4];
+        HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipStreamSynchronize(h->cur));
+        if (ctr[1]) return set_err(h, BK_EOVERFLOW, "bk_rollout: iteration guard tripped%s", "");
+    }
+    return BK_OK;
+}
+
+int bk_rollout(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index, int32_t n_playouts,
+               const bk_rollout_cfg* cfg, const uint32_t* compat_seeds, bk_result* out, int mem) {
+    if (!out) return set_err(h, BK_EINVAL, "bk_rollout: out is NULL%s", "");
+    if (cfg && cfg->semantics == BK_SEM_ADVANCE) return set_err(h, BK_EINVAL, "bk_rollout: use bk_advance%s", "");
+    return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, out, nullptr, mem);
+}
+
+int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index, int32_t n_playouts,
+               const bk_rollout_cfg* cfg, const uint32_t* compat_seeds, bk_state* out_states, int mem) {
+    if (!out_states || !cfg || cfg->semantics != BK_SEM_ADVANCE)
+        return set_err(h, BK_EINVAL, "bk_advance: needs out_states and BK_SEM_ADVANCE%s", "");
+    return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, nullptr, out_states, mem);
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+"""Batched GPU entry points (thin Python layer over the C-ABI).
+
+Inputs may be numpy arrays (host; the library stages them) or torch tensors already
+on the GPU (device pointers, launched on torch's current stream).  There is no CPU
+implementation behind any of these functions.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native as N
+
+STATE_DTYPE = N.STATE_DTYPE
+RESULT_DTYPE = N.RESULT_DTYPE
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _as_host(x, dtype):
+    a = np.ascontiguousarray(x)
+    if dtype is not None and a.dtype != dtype:
+        a = a.view(dtype) if a.dtype.itemsize == 1 and dtype.itemsize != 1 else a.astype(dtype)
+    return a
+
+
+class BlokusGPU:
+    """Owns one bk_handle (one HIP stream + scratch) on `device`."""
+
+    def __init__(self, device: int = 0):
+        self.handle = N.Handle(device)
+        self.device = device
+
+    # ------------------------------------------------------------------ helpers
+    def _stream_from_torch(self):
+        import torch
+        self.handle.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def last_kernel_ms(self) -> float:
+        return self.handle.last_kernel_ms()
+
+    def synchronize(self):
+        self.handle.synchronize()
+
+    # ------------------------------------------------------------------ movegen
+    def movegen(self, states, players, rows: bool = True):
+        """Legal-move masks + counts for (state, player) pairs.
+
+        states: n bk_state records (numpy STATE_DTYPE / uint8[n,256], or a torch uint8
+        cuda tensor [n,256]); players: n uint8 in 0..3.
+        Returns (counts[n] uint32, rows[n,91,20] uint32 or None); rows[i,g,r] bit c =
+        anchor (r, c) legal for global orientation g (move_generator.py:130 set).
+        """
+        if _is_torch(states):
+            import torch
+            n = states.shape[0]
+            cnt = torch.empty(n, dtype=torch.int32, device=states.device)
+            out = torch.empty((n, N.N_ORIENTS, 20), dtype=torch.int32, device=states.device) if rows else None
+            self._stream_from_torch()
+            self.handle.movegen(states.data_ptr(), players.data_ptr(), n, out.data_ptr() if rows else 0,
+                                cnt.data_ptr(), N.MEM_DEVICE)
+            return cnt, out
+        st = np.ascontiguousarray(states).view(np.uint8).reshape(-1, 256)
+        pl = np.ascontiguousarray(players, dtype=np.uint8)
+        n = st.shape[0]
+        assert pl.shape[0] == n
+        cnt = np.zeros(n, dtype=np.uint32)
+        out = np.zeros((n, N.N_ORIENTS, 20), dtype=np.uint32) if rows else None
+        self.handle.set_stream(None)
+        self.handle.movegen(st.ctypes.data, pl.ctypes.data, n, out.ctypes.data if rows else 0, cnt.ctypes.data,
+                            N.MEM_HOST)
+        return cnt, out
+
+    def has_moves(self, states):
+        """uint8 mask per state: bit p set iff player p has a legal move (move_generator.py:961)."""
+        if _is_torch(states):
+            import torch
+            n = states.shape[0]
+            out = torch.empty(n, dtype=torch.uint8, device=states.device)
+            self._stream_from_torch()
+            self.handle.has_moves(states.data_ptr(), n, out.data_ptr(), N.MEM_DEVICE)
+            return out
+        st = np.ascontiguousarray(states).view(np.uint8).reshape(-1, 256)
+        out = np.zeros(st.shape[0], dtype=np.uint8)
+        self.handle.set_stream(None)
+        self.handle.has_moves(st.ctypes.data, st.shape[0], out.ctypes.data, N.MEM_HOST)
+        return out
+
+    # ------------------------------------------------------------------ rollouts
+    def rollout(self, roots, n_playouts: int, *, semantics: int = N.SEM_ARENA, rng: int = N.RNG_PHILOX,
+                seed: int = 0, max_plies: int | None = None, compat_seeds=None, root_index=None,
+                order: int = N.ORDER_NAIVE, seats_share_stream: bool = False, out=None):
+        """Random playouts from roots (see bk_rollout in include/blokus_hip.h).
+
+        Host numpy in -> numpy RESULT_DTYPE out; torch cuda in -> torch uint8 [n,32] out.
+        """
+        if max_plies is None:
+            max_plies = 2500 if semantics == N.SEM_ARENA else 50
+        cfg = N.BkRolloutCfg(semantics, order, rng, max_plies, seed & (2**64 - 1), int(seats_share_stream), 0)
+        if _is_torch(roots):
+            import torch
+            dev = roots.device
+            if out is None:
+                out = torch.empty((n_playouts, 32), dtype=torch.uint8, device=dev)
+            self._stream_from_torch()
+            self.handle.rollout(roots.data_ptr(), roots.shape[0],
+                                root_index.data_ptr() if root_index is not None else 0, n_playouts, cfg,
+                                compat_seeds.data_ptr() if compat_seeds is not None else 0, out.data_ptr(),
+                                N.MEM_DEVICE)
+            return out
+        st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
+        res = np.zeros(n_playouts, dtype=RESULT_DTYPE)
+        idx = np.ascontiguousarray(root_index, dtype=np.int32) if root_index is not None else None
+        seeds = np.ascontiguousarray(compat_seeds, dtype=np.uint32).reshape(-1, 4) if compat_seeds is not None else None
+        if seeds is not None:
+            assert seeds.shape[0] >= n_playouts
+        self.handle.set_stream(None)
+        self.handle.rollout(st.ctypes.data, st.shape[0], idx.ctypes.data if idx is not None else 0, n_playouts, cfg,
+                            seeds.ctypes.data if seeds is not None else 0, res.ctypes.data, N.MEM_HOST)
+        return res
+
+    # ------------------------------------------------------------------ positions
+    def advance(self, roots, n: int, plies: int, *, seed: int = 0, root_index=None):
+        """Play `plies` uniformly random moves (naive order, Philox stream) from each root
+        and return the reached states (BK_SEM_ADVANCE).  Batched analogue of
+        tests/utils_game_states.py:12 generate_random_valid_state (different RNG)."""
+        cfg = N.BkRolloutCfg(N.SEM_ADVANCE, N.ORDER_NAIVE, N.RNG_PHILOX, plies, seed & (2**64 - 1), 0, 0)
+        if _is_torch(roots):
+            import torch
+            out = torch.empty((n, 256), dtype=torch.uint8, device=roots.device)
+            self._stream_from_torch()
+            self.handle.advance(roots.data_ptr(), roots.shape[0],
+                                root_index.data_ptr() if root_index is not None else 0, n, cfg, 0,
+                                out.data_ptr(), N.MEM_DEVICE)
+            return out
+        st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
+        out = np.zeros(n, dtype=STATE_DTYPE)
+        idx = np.ascontiguousarray(root_index, dtype=np.int32) if root_index is not None else None
+        self.handle.set_stream(None)
+        self.handle.advance(st.ctypes.data, st.shape[0], idx.ctypes.data if idx is not None else 0, n, cfg, 0,
+                            out.ctypes.data, N.MEM_HOST)
+        return out
+
+
+def empty_state() -> np.ndarray:
+    """The initial position (engine/board.py:54-78): nobody has moved, RED to play."""
+    s = np.zeros(1, dtype=STATE_DTYPE)
+    s["first_move"] = 0xF
+    return s
+
+
+def winners(results) -> np.ndarray:
+    """winner_ids as a 4-bit mask per playout (GameResult.winner_ids)."""
+    return np.asarray(results["winner_mask"])

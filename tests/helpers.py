@@ -1,0 +1,50 @@
+"""Shared test helpers: rebuild reference positions through the oracle and pack them."""
+import numpy as np
+
+from oracle import pyoracle as O
+from reinforcementlearning_blokus_amd import _native as N
+from tests.conftest import load_golden
+
+POS = load_golden("positions.json")
+
+
+def replay(rec):
+    """Rebuild the reference Board of a positions.json record by replaying its
+    place_piece log (cell order kept, so the frontier-set layout is the reference's)."""
+    b = O.new_board()
+    for player_value, piece_id, cells in rec["log"]:
+        while b.cur != player_value - 1:
+            b.cur = (b.cur + 1) & 3
+        O.place_cells(b, player_value - 1, piece_id, [r * 20 + c for r, c in cells])
+    b.cur = rec["state"]["current_player"] - 1
+    return b
+
+
+def pack_many(boards):
+    arr = O.states_array(boards)
+    return np.frombuffer(bytes(arr), dtype=N.STATE_DTYPE).copy()
+
+
+def oracle_states(n, seed0=0, lo=16, hi=40):
+    """n synthetic mid-game positions: generate_random_valid_state(m, seed) with m
+    uniform in [lo, hi] (config 2), restated by the oracle."""
+    rng = np.random.RandomState(seed0)
+    boards = []
+    for i in range(n):
+        m = int(rng.randint(lo, hi + 1))
+        b, _ = O.gen_state(m, seed0 + i)
+        boards.append(b)
+    return boards
+
+
+def rows_to_moves(rows):
+    """Dense [91,20] mask -> naive-order move ints (g*400 + r*20 + c)."""
+    out = []
+    for g in range(91):
+        for r in range(20):
+            w = int(rows[g, r])
+            while w:
+                c = (w & -w).bit_length() - 1
+                out.append(g * 400 + r * 20 + c)
+                w &= w - 1
+    return out
