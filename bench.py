@@ -33,8 +33,8 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--games", type=int, default=256)
     ap.add_argument("--rollouts", type=int, default=1024)
     ap.add_argument("--root-plies", type=int, default=20)
@@ -89,31 +89,44 @@ def main():
                            root_index=np.zeros(args.games, dtype=np.int32))
     roots = torch.from_numpy(roots_np.view(np.uint8).reshape(args.games, 256)).to(dev)
     n = args.games * args.rollouts
-    idx = torch.arange(n, dtype=torch.int32, device=dev) % args.games
+    # game j's rollouts are contiguous (one wave plays 64 rollouts of the same game)
+    idx = torch.arange(n, dtype=torch.int32, device=dev) // args.rollouts
     out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+
+    stream = torch.cuda.Stream(dev)  # our kernels and the timing events share this stream
+    plies_acc = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def step(k):
         gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k, root_index=idx,
                     out=out)
 
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kernel_ms = []
-    plies = 0
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(1000 + k)
-        kernel_ms.append(gpu.last_kernel_ms())
-        plies += int(out.view(-1, 32)[:, 10:12].contiguous().view(torch.int16).to(torch.int64).sum().item())
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def count_plies():
+        plies_acc.add_(out[:, 10:12].contiguous().view(torch.int16).to(torch.int64).sum())
+
+    with torch.cuda.stream(stream):
+        for k in range(args.warmup):
+            step(k)
+            count_plies()
+        plies_acc.zero_()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            events[k][0].record(stream)
+            step(1000 + k)
+            events[k][1].record(stream)
+            count_plies()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
+    plies = int(plies_acc.item())
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     tot = torch.tensor([n * args.steps, plies], dtype=torch.float64, device=dev)
     if dist:

@@ -116,7 +116,9 @@ int bk_tables_version(void);
 /* device = HIP device ordinal; flags reserved (0) */
 int bk_create(int device, uint32_t flags, bk_handle* out);
 int bk_destroy(bk_handle h);
-/* Borrow a caller stream (hipStream_t as void*); NULL restores the handle's own stream */
+/* Launch on a caller stream (hipStream_t as void*; NULL = the HIP null stream, which is
+   torch's default stream); BK_STREAM_OWN restores the handle's own stream. */
+#define BK_STREAM_OWN ((void*)~(uintptr_t)0)
 int bk_set_stream(bk_handle h, void* stream);
 int bk_synchronize(bk_handle h);
 int bk_last_error(bk_handle h, char* buf, size_t len);

@@ -19,6 +19,7 @@ SEM_ARENA, SEM_ROLLOUT, SEM_ADVANCE = 0, 1, 2
 ORDER_NAIVE, ORDER_FRONTIER = 0, 1
 RNG_PHILOX, RNG_NUMPY_MT = 0, 1
 N_ORIENTS = 91
+STREAM_OWN = (1 << 64) - 1  # BK_STREAM_OWN
 
 # every symbol include/blokus_hip.h declares
 EXPORTS = (
@@ -152,7 +153,9 @@ class Handle:
             raise RuntimeError(f"{what} failed ({rc}): {self.error()}")
 
     def set_stream(self, stream_ptr: int | None):
-        self.check(self._L.bk_set_stream(self._h, C.c_void_p(stream_ptr or 0)), "bk_set_stream")
+        """stream_ptr: a hipStream_t value (0 = null stream) or None for the handle's own."""
+        v = STREAM_OWN if stream_ptr is None else stream_ptr
+        self.check(self._L.bk_set_stream(self._h, C.c_void_p(v)), "bk_set_stream")
 
     def synchronize(self):
         self.check(self._L.bk_synchronize(self._h), "bk_synchronize")

@@ -29,6 +29,7 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -45,7 +46,7 @@
 
 __constant__ uint32_t kInfo[BK_NUM_ORIENTS] = BK_ORIENT_INFO_INIT;
 __constant__ uint32_t kCells[BK_NUM_ORIENTS][5] = BK_ORIENT_CELLS_INIT;
-__constant__ uint32_t kRows[BK_NUM_ORIENTS][5] = BK_ORIENT_ROWS_INIT;
+__constant__ uint32_t kSten[BK_NUM_ORIENTS][12] = BK_STENCIL_INIT;
 
 // ------------------------------------------------------------------------------------
 // state <-> rows
@@ -97,69 +98,143 @@ __device__ __forceinline__ void derive_rows(const uint32_t (&own)[20], const uin
 // ------------------------------------------------------------------------------------
 // the stencil scan
 // ------------------------------------------------------------------------------------
-template <int D>
-__device__ __forceinline__ void acc_cell(uint32_t (&ab)[20], uint32_t (&ac)[20], const uint32_t (&B)[20],
-                                         const uint32_t (&C)[20], uint32_t c) {
+// Mover planes.  B/C = blocked / corner rows; BP/CP = the same for a horizontal
+// pair of cells (BP[R] = B[R] | B[R] << 1): a run of two cells of a piece row costs one
+// term instead of two.  287 terms cover the 410 cells of the 91 orientations.
+struct Planes {
+    uint32_t B[20], C[20], BP[20], CP[20];
+};
+
+__device__ __forceinline__ void make_pairs(Planes& P) {
 #pragma unroll
-    for (int r = 0; r < 20; ++r) {
-        if (r + D < 20) {
-            ab[r] |= B[r + D] << c;
-            ac[r] |= C[r + D] << c;
-        } else {
-            ab[r] = 0xFFFFFFFFu;  // a cell would fall below row 19
+    for (int R = 0; R < 20; ++R) {
+        P.BP[R] = P.B[R] | (P.B[R] << 1);
+        P.CP[R] = P.C[R] | (P.C[R] << 1);
+    }
+}
+
+// Terms on piece row D (template: static register index), columns packed in the
+// uniform word w = count << 16 | col_j << 3j.  Each term is two v_lshl_or_b32 per row.
+template <int D>
+__device__ __forceinline__ void acc_terms(uint32_t (&ab)[20], uint32_t (&ac)[20], const uint32_t (&S)[20],
+                                          const uint32_t (&T)[20], uint32_t w) {
+    const int m = (int)(w >> 16);
+#pragma unroll 1
+    for (int j = 0; j < m; ++j) {
+        const uint32_t c = (w >> (3 * j)) & 7u;
+#pragma unroll
+        for (int r = 0; r < 20; ++r) {
+            if (r + D < 20) {
+                ab[r] |= S[r + D] << c;
+                ac[r] |= T[r + D] << c;
+            } else {
+                ab[r] = 0xFFFFFFFFu;  // a cell would fall below row 19
+            }
         }
     }
 }
 
-// cells of piece row D (uniform word w = ncells << 16 | col_j << 3j), j >= j0
-template <int D>
-__device__ __forceinline__ void acc_row(uint32_t (&ab)[20], uint32_t (&ac)[20], const uint32_t (&B)[20],
-                                        const uint32_t (&C)[20], uint32_t w, int j0) {
-    const int m = (int)(w >> 16);
-#pragma unroll 1
-    for (int j = j0; j < m; ++j) acc_cell<D>(ab, ac, B, C, (w >> (3 * j)) & 7u);
-}
-
-// Legal-anchor scan of one orientation g (uniform).  ok[r] = legal anchors of anchor
-// row r, reversed layout.  The piece-row index D is a template parameter of five
-// separate uniform loops (no switch: a switch gets tail-merged by the compiler into
-// register copies that cost as much as the stencil work itself).
-__device__ __forceinline__ void scan_orient(int g, const uint32_t (&B)[20], const uint32_t (&C)[20],
-                                            uint32_t (&ok)[20]) {
+// One orientation, stencil words w[0..10] (uniform).  ok[r] = legal anchors of anchor
+// row r (reversed layout).  PAIR_INIT: the init term on piece row 0 is a pair.
+template <bool PAIR_INIT>
+__device__ __forceinline__ void scan_words(const uint32_t (&w)[12], const Planes& P, uint32_t (&ok)[20]) {
     uint32_t ab[20], ac[20];
-    const uint32_t w0 = kRows[g][0];
-    const uint32_t c0 = w0 & 7u;  // piece row 0 is never empty
+    const uint32_t c0 = (w[0] >> 8) & 7u;
 #pragma unroll
     for (int r = 0; r < 20; ++r) {
-        ab[r] = B[r] << c0;
-        ac[r] = C[r] << c0;
+        ab[r] = (PAIR_INIT ? P.BP[r] : P.B[r]) << c0;
+        ac[r] = (PAIR_INIT ? P.CP[r] : P.C[r]) << c0;
     }
-    acc_row<0>(ab, ac, B, C, w0, 1);
-    acc_row<1>(ab, ac, B, C, kRows[g][1], 0);
-    acc_row<2>(ab, ac, B, C, kRows[g][2], 0);
-    acc_row<3>(ab, ac, B, C, kRows[g][3], 0);
-    acc_row<4>(ab, ac, B, C, kRows[g][4], 0);
+    acc_terms<0>(ab, ac, P.B, P.C, w[1]);
+    acc_terms<1>(ab, ac, P.B, P.C, w[2]);
+    acc_terms<2>(ab, ac, P.B, P.C, w[3]);
+    acc_terms<3>(ab, ac, P.B, P.C, w[4]);
+    acc_terms<4>(ab, ac, P.B, P.C, w[5]);
+    acc_terms<0>(ab, ac, P.BP, P.CP, w[6]);
+    acc_terms<1>(ab, ac, P.BP, P.CP, w[7]);
+    acc_terms<2>(ab, ac, P.BP, P.CP, w[8]);
+    acc_terms<3>(ab, ac, P.BP, P.CP, w[9]);
+    acc_terms<4>(ab, ac, P.BP, P.CP, w[10]);
 #pragma unroll
     for (int r = 0; r < 20; ++r) ok[r] = ac[r] & ~ab[r];
 }
 
-// Full movegen for one board-player: per-orientation prefix counts to LDS
-// (cnt[g * WAVE + lane] = number of legal moves in orientations 0..g).
-__device__ __forceinline__ uint32_t movegen_prefix(const uint32_t (&B)[20], const uint32_t (&C)[20],
-                                                   uint32_t avail, uint16_t* cnt, int lane) {
-    uint32_t total = 0;
-#pragma unroll 1
-    for (int g = 0; g < BK_NUM_ORIENTS; ++g) {
-        uint32_t ok[20];
-        scan_orient(g, B, C, ok);
-        uint32_t c = 0;
+__device__ __forceinline__ void load_words(int i, uint32_t (&w)[12]) {
 #pragma unroll
-        for (int r = 0; r < 20; ++r) c += __builtin_popcount(ok[r]);
-        const uint32_t piece = kInfo[g] & 0xFFu;
-        total += ((avail >> (piece - 1)) & 1u) ? c : 0u;
-        cnt[g * WAVE + lane] = (uint16_t)total;
+    for (int k = 0; k < 12; ++k) w[k] = kSten[i][k];
+}
+
+// LDS count slots: two u16 per dword, [g/2][lane]
+__device__ __forceinline__ uint32_t cnt_off(int g, int lane) { return (uint32_t)(((g >> 1) * WAVE + lane) * 2 + (g & 1)); }
+#define CNT_WORDS_PER_WAVE (((BK_NUM_ORIENTS + 1) / 2) * WAVE)
+
+// Per-orientation legal-move counts of one board-player (cnt[...] u16, indexed by the
+// global orientation id g); returns the total.  Orientations whose piece no lane of
+// the wave may still play are skipped with a uniform branch.
+template <bool PAIR_INIT>
+__device__ __forceinline__ uint32_t count_range(int i0, int i1, const Planes& P, uint32_t avail,
+                                                uint16_t* cnt, int lane) {
+    uint32_t total = 0;
+    uint32_t w[12], nx[12];
+    load_words(i0, w);
+#pragma unroll 1
+    for (int i = i0; i < i1; ++i) {
+        load_words(i + 1 < i1 ? i + 1 : i, nx);  // prefetch the next stencil
+        const uint32_t piece = w[0] & 0xFFu;
+        const int g = (int)(w[0] >> 16);
+        const bool av = (avail >> (piece - 1u)) & 1u;
+        uint32_t c = 0;
+        if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
+            uint32_t ok[20];
+            scan_words<PAIR_INIT>(w, P, ok);
+#pragma unroll
+            for (int r = 0; r < 20; ++r) c += __builtin_popcount(ok[r]);
+            c = av ? c : 0u;
+        }
+        cnt[cnt_off(g, lane)] = (uint16_t)c;
+        total += c;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) w[k] = nx[k];
     }
     return total;
+}
+
+__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint16_t* cnt, int lane) {
+    return count_range<true>(0, BK_STENCIL_PAIR_INIT, P, avail, cnt, lane) +
+           count_range<false>(BK_STENCIL_PAIR_INIT, BK_NUM_ORIENTS, P, avail, cnt, lane);
+}
+
+// Dense legal rows of every orientation (k_movegen): calls f(g, ok, available)
+template <bool PAIR_INIT, typename F>
+__device__ __forceinline__ void rows_range(int i0, int i1, const Planes& P, F&& f) {
+    uint32_t w[12];
+#pragma unroll 1
+    for (int i = i0; i < i1; ++i) {
+        load_words(i, w);
+        uint32_t ok[20];
+        scan_words<PAIR_INIT>(w, P, ok);
+        f((int)(w[0] >> 16), w[0] & 0xFFu, ok);
+    }
+}
+
+// orientation holding the k-th legal move (naive order: g ascending) and its rank in it
+__device__ __forceinline__ int pick_orient(const uint16_t* cnt, int lane, uint32_t k, uint32_t& kk) {
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(cnt);
+    uint32_t run = 0;
+    int gs = BK_NUM_ORIENTS - 1;
+    uint32_t before = 0;
+    bool found = false;
+#pragma unroll 1
+    for (int h = 0; h < (BK_NUM_ORIENTS + 1) / 2; ++h) {
+        const uint32_t v = c32[h * WAVE + lane];
+        const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
+        if (!found && k < run + lo) { gs = 2 * h; before = run; found = true; }
+        run += lo;
+        if (!found && k < run + hi) { gs = 2 * h + 1; before = run; found = true; }
+        run += hi;
+    }
+    kk = k - before;
+    return gs;
 }
 
 // Recompute orientation gs (per-lane, divergent) row r_ok values with per-lane
@@ -291,15 +366,15 @@ __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&ow
 }
 
 __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
-    __shared__ uint16_t cnt[BK_NUM_ORIENTS * WAVE * (BLOCK / WAVE)];
+    __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = cnt + wv * BK_NUM_ORIENTS * WAVE;
+    uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < a.n;
     const int idx = live ? i : 0;
     const bk_state* s = a.states + idx;
     const int p = a.players ? (a.players[idx] & 3) : 0;
-    uint32_t B[20], C[20], own[20], occ[20];
+    uint32_t own[20], occ[20];
 #pragma unroll
     for (int R = 0; R < 20; ++R) { occ[R] = 0; own[R] = 0; }
 #pragma unroll
@@ -310,21 +385,18 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
             occ[R] |= row;
             own[R] |= (q == p) ? row : 0u;
         }
-    derive_rows(own, occ, (s->first_move >> p) & 1u, p, B, C);
-    const uint32_t avail = ~s->used[p] & 0x1FFFFFu;
+    Planes P;
+    derive_rows(own, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
+    make_pairs(P);
+    const uint32_t avail = live ? (~s->used[p] & 0x1FFFFFu) : 0u;
     if (a.out_rows == nullptr) {
-        const uint32_t total = movegen_prefix(B, C, avail, my, lane);
+        const uint32_t total = movegen_counts(P, avail, my, lane);
         if (live && a.out_count) a.out_count[i] = total;
         return;
     }
     uint32_t total = 0;
-#pragma unroll 1
-    for (int g = 0; g < BK_NUM_ORIENTS; ++g) {
-        uint32_t ok[20];
-        scan_orient(g, B, C, ok);
-        const uint32_t piece = kInfo[g] & 0xFFu;
-        const bool av = (avail >> (piece - 1)) & 1u;
-        uint32_t c = 0;
+    auto emit = [&](int g, uint32_t piece, const uint32_t (&ok)[20]) {
+        const bool av = (avail >> (piece - 1u)) & 1u;
         uint4* dst = reinterpret_cast<uint4*>(a.out_rows + ((size_t)idx * BK_NUM_ORIENTS + g) * 20);
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
@@ -333,19 +405,20 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
             v.y = av ? __builtin_bitreverse32(ok[4 * q + 1]) : 0u;
             v.z = av ? __builtin_bitreverse32(ok[4 * q + 2]) : 0u;
             v.w = av ? __builtin_bitreverse32(ok[4 * q + 3]) : 0u;
-            c += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) +
-                 __builtin_popcount(v.w);
+            total += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) +
+                     __builtin_popcount(v.w);
             if (live) dst[q] = v;
         }
-        total += c;
-    }
+    };
+    rows_range<true>(0, BK_STENCIL_PAIR_INIT, P, emit);
+    rows_range<false>(BK_STENCIL_PAIR_INIT, BK_NUM_ORIENTS, P, emit);
     if (live && a.out_count) a.out_count[i] = total;
 }
 
 __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
-    __shared__ uint16_t cnt[BK_NUM_ORIENTS * WAVE * (BLOCK / WAVE)];
+    __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = cnt + wv * BK_NUM_ORIENTS * WAVE;
+    uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < a.n;
     const bk_state* s = a.states + (live ? i : 0);
@@ -354,7 +427,8 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
     uint8_t mask = 0;
 #pragma unroll 1
     for (int p = 0; p < 4; ++p) {
-        uint32_t ow[20], B[20], C[20];
+        uint32_t ow[20];
+        Planes P;
 #pragma unroll
         for (int R = 0; R < 20; ++R) {
             uint32_t v = own[0][R];
@@ -363,8 +437,9 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
             v = p == 3 ? own[3][R] : v;
             ow[R] = v;
         }
-        derive_rows(ow, occ, (s->first_move >> p) & 1u, p, B, C);
-        const uint32_t total = movegen_prefix(B, C, ~s->used[p] & 0x1FFFFFu, my, lane);
+        derive_rows(ow, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
+        make_pairs(P);
+        const uint32_t total = movegen_counts(P, live ? (~s->used[p] & 0x1FFFFFu) : 0u, my, lane);
         mask |= (uint8_t)((total > 0) << p);
     }
     if (live) a.out_mask4[i] = mask;
@@ -573,9 +648,9 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
 }
 
 __global__ __launch_bounds__(BLOCK) void k_rollout(RolloutArgs a) {
-    __shared__ uint16_t cnt[BK_NUM_ORIENTS * WAVE * (BLOCK / WAVE)];
+    __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = cnt + wv * BK_NUM_ORIENTS * WAVE;
+    uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
@@ -617,15 +692,19 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(RolloutArgs a) {
         // ---- derive + movegen for every active lane (uniform work)
         const bool idle = done || g.pid < 0;
         const int p = idle ? 0 : g.cur;
-        uint32_t own[20], occ[20], B[20], C[20];
+        Planes P;
+        {
+            uint32_t own[20], occ[20];
 #pragma unroll
-        for (int R = 0; R < 20; ++R) {
-            own[R] = idle ? 0u : slab.at(p, R);
-            occ[R] = idle ? 0u : slab.at(4, R);
+            for (int R = 0; R < 20; ++R) {
+                own[R] = idle ? 0u : slab.at(p, R);
+                occ[R] = idle ? 0u : slab.at(4, R);
+            }
+            derive_rows(own, occ, (g.first >> p) & 1u, p, P.B, P.C);
         }
-        derive_rows(own, occ, (g.first >> p) & 1u, p, B, C);
+        make_pairs(P);
         const uint32_t avail = idle ? 0u : (~g.used.get(p) & 0x1FFFFFu);
-        const uint32_t total = movegen_prefix(B, C, avail, my, lane);
+        const uint32_t total = movegen_counts(P, avail, my, lane);
         if (idle) continue;
         if (total == 0u) {
             if (arena) {
@@ -638,17 +717,10 @@ __global__ __launch_bounds__(BLOCK) void k_rollout(RolloutArgs a) {
             continue;
         }
         const uint32_t k = draw_index(a, g, slab, slot, total);
-        // orientation: first g with prefix > k
-        int lo = 0, hi = BK_NUM_ORIENTS - 1;
-#pragma unroll
-        for (int it = 0; it < 7; ++it) {
-            const int mid = (lo + hi) >> 1;
-            if ((uint32_t)my[mid * WAVE + lane] > k) hi = mid; else lo = mid + 1;
-        }
-        const int gs = lo;
-        const uint32_t before = gs > 0 ? (uint32_t)my[(gs - 1) * WAVE + lane] : 0u;
+        uint32_t kk;
+        const int gs = pick_orient(my, lane, k, kk);
         int ar, ac;
-        locate_move(gs, k - before, B, C, ar, ac);
+        locate_move(gs, kk, P.B, P.C, ar, ac);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
         const uint32_t info = kInfo[gs];
         const int n = (int)((info >> 8) & 0xFFu);
@@ -751,6 +823,10 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_rollout, BLOCK, 0) != hipSuccess || bpc < 1) bpc = 1;
     h->rollout_blocks_per_cu = bpc;
+    if (const char* env = getenv("BK_BLOCKS_PER_CU")) {  // tuning override
+        const int v = atoi(env);
+        if (v > 0 && v < bpc) h->rollout_blocks_per_cu = v;
+    }
     h->cur = h->own;
     *out = h;
     return BK_OK;
@@ -771,7 +847,7 @@ int bk_destroy(bk_handle h) {
 
 int bk_set_stream(bk_handle h, void* stream) {
     if (!h) return BK_EINVAL;
-    h->cur = stream ? (hipStream_t)stream : h->own;
+    h->cur = (stream == BK_STREAM_OWN) ? h->own : (hipStream_t)stream;
     return BK_OK;
 }
 
