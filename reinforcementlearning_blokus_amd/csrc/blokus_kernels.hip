@@ -46,7 +46,7 @@
 
 __constant__ uint32_t kInfo[BK_NUM_ORIENTS] = BK_ORIENT_INFO_INIT;
 __constant__ uint32_t kCells[BK_NUM_ORIENTS][5] = BK_ORIENT_CELLS_INIT;
-__constant__ uint32_t kSten[BK_NUM_ORIENTS][12] = BK_STENCIL_INIT;
+__constant__ uint32_t kSten[BK_NUM_ORIENTS][4] = BK_STENCIL_INIT;
 
 // ------------------------------------------------------------------------------------
 // state <-> rows
@@ -113,69 +113,86 @@ __device__ __forceinline__ void make_pairs(Planes& P) {
     }
 }
 
-// Terms on piece row D (template: static register index), columns packed in the
-// uniform word w = count << 16 | col_j << 3j.  Each term is two v_lshl_or_b32 per row.
-template <int D>
+// popcount-accumulate as ONE v_bcnt_u32_b32 (the compiler otherwise reassociates the
+// sum into bcnt(x,0) + v_add3 trees: +25% on the count epilogue)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
+
+// Terms on piece row D (template: static register index) for the NR valid anchor rows
+// of a height-H orientation, columns packed in the uniform word w = count << 16 |
+// col_j << 3j.  Each term is two v_lshl_or_b32 per anchor row.
+template <int D, int NR>
 __device__ __forceinline__ void acc_terms(uint32_t (&ab)[20], uint32_t (&ac)[20], const uint32_t (&S)[20],
                                           const uint32_t (&T)[20], uint32_t w) {
-    const int m = (int)(w >> 16);
+    const int m = (int)((w >> 6) & 3u);  // w: cols (3 bits each) | count << 6
 #pragma unroll 1
     for (int j = 0; j < m; ++j) {
         const uint32_t c = (w >> (3 * j)) & 7u;
 #pragma unroll
-        for (int r = 0; r < 20; ++r) {
-            if (r + D < 20) {
-                ab[r] |= S[r + D] << c;
-                ac[r] |= T[r + D] << c;
-            } else {
-                ab[r] = 0xFFFFFFFFu;  // a cell would fall below row 19
-            }
+        for (int r = 0; r < NR; ++r) {
+            ab[r] |= S[r + D] << c;
+            ac[r] |= T[r + D] << c;
         }
     }
 }
 
-// One orientation, stencil words w[0..10] (uniform).  ok[r] = legal anchors of anchor
-// row r (reversed layout).  PAIR_INIT: the init term on piece row 0 is a pair.
-template <bool PAIR_INIT>
-__device__ __forceinline__ void scan_words(const uint32_t (&w)[12], const Planes& P, uint32_t (&ok)[20]) {
+template <int D, int NR>
+__device__ __forceinline__ void acc_row(uint32_t (&ab)[20], uint32_t (&ac)[20], const Planes& P, uint32_t f) {
+    acc_terms<D, NR>(ab, ac, P.B, P.C, f & 0xFFu);         // singles on piece row D
+    acc_terms<D, NR>(ab, ac, P.BP, P.CP, (f >> 8) & 0xFFu); // pairs on piece row D
+}
+
+template <int H, int NR>
+__device__ __forceinline__ void acc_rows(uint32_t (&ab)[20], uint32_t (&ac)[20], const Planes& P,
+                                         const uint32_t (&w)[4]) {
+    acc_row<0, NR>(ab, ac, P, w[1]);
+    if constexpr (H > 1) acc_row<1, NR>(ab, ac, P, w[1] >> 16);
+    if constexpr (H > 2) acc_row<2, NR>(ab, ac, P, w[2]);
+    if constexpr (H > 3) acc_row<3, NR>(ab, ac, P, w[2] >> 16);
+    if constexpr (H > 4) acc_row<4, NR>(ab, ac, P, w[3]);
+}
+
+// One orientation of height H, stencil words w[0..10] (uniform).  ok[r] = legal anchors
+// of anchor row r (reversed layout), r < 21 - H; higher rows cannot hold the piece.
+// PAIR_INIT: the first term (piece row 0) is a pair.
+template <bool PAIR_INIT, int H>
+__device__ __forceinline__ void scan_words(const uint32_t (&w)[4], const Planes& P, uint32_t (&ok)[20]) {
+    constexpr int NR = 21 - H;
     uint32_t ab[20], ac[20];
     const uint32_t c0 = (w[0] >> 8) & 7u;
 #pragma unroll
-    for (int r = 0; r < 20; ++r) {
+    for (int r = 0; r < NR; ++r) {
         ab[r] = (PAIR_INIT ? P.BP[r] : P.B[r]) << c0;
         ac[r] = (PAIR_INIT ? P.CP[r] : P.C[r]) << c0;
     }
-    acc_terms<0>(ab, ac, P.B, P.C, w[1]);
-    acc_terms<1>(ab, ac, P.B, P.C, w[2]);
-    acc_terms<2>(ab, ac, P.B, P.C, w[3]);
-    acc_terms<3>(ab, ac, P.B, P.C, w[4]);
-    acc_terms<4>(ab, ac, P.B, P.C, w[5]);
-    acc_terms<0>(ab, ac, P.BP, P.CP, w[6]);
-    acc_terms<1>(ab, ac, P.BP, P.CP, w[7]);
-    acc_terms<2>(ab, ac, P.BP, P.CP, w[8]);
-    acc_terms<3>(ab, ac, P.BP, P.CP, w[9]);
-    acc_terms<4>(ab, ac, P.BP, P.CP, w[10]);
+    acc_rows<H, NR>(ab, ac, P, w);
 #pragma unroll
-    for (int r = 0; r < 20; ++r) ok[r] = ac[r] & ~ab[r];
+    for (int r = 0; r < 20; ++r) ok[r] = r < NR ? (ac[r] & ~ab[r]) : 0u;
 }
 
-__device__ __forceinline__ void load_words(int i, uint32_t (&w)[12]) {
+__device__ __forceinline__ void load_words(int i, uint32_t (&w)[4]) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) w[k] = kSten[i][k];
+    for (int k = 0; k < 4; ++k) w[k] = kSten[i][k];
 }
 
 // LDS count slots: two u16 per dword, [g/2][lane]
 __device__ __forceinline__ uint32_t cnt_off(int g, int lane) { return (uint32_t)(((g >> 1) * WAVE + lane) * 2 + (g & 1)); }
 #define CNT_WORDS_PER_WAVE (((BK_NUM_ORIENTS + 1) / 2) * WAVE)
 
-// Per-orientation legal-move counts of one board-player (cnt[...] u16, indexed by the
-// global orientation id g); returns the total.  Orientations whose piece no lane of
-// the wave may still play are skipped with a uniform branch.
-template <bool PAIR_INIT>
+// Per-orientation legal-move counts of one board-player for table entries [i0, i1)
+// (cnt[...] u16, indexed by global orientation id g); returns their sum.
+// Orientations whose piece no lane of the wave may still play are skipped with a
+// uniform branch.
+template <bool PAIR_INIT, int H>
 __device__ __forceinline__ uint32_t count_range(int i0, int i1, const Planes& P, uint32_t avail,
                                                 uint16_t* cnt, int lane) {
+    constexpr int NR = 21 - H;
     uint32_t total = 0;
-    uint32_t w[12], nx[12];
+    if (i0 >= i1) return 0;
+    uint32_t w[4], nx[4];
     load_words(i0, w);
 #pragma unroll 1
     for (int i = i0; i < i1; ++i) {
@@ -186,35 +203,60 @@ __device__ __forceinline__ uint32_t count_range(int i0, int i1, const Planes& P,
         uint32_t c = 0;
         if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
             uint32_t ok[20];
-            scan_words<PAIR_INIT>(w, P, ok);
+            scan_words<PAIR_INIT, H>(w, P, ok);
 #pragma unroll
-            for (int r = 0; r < 20; ++r) c += __builtin_popcount(ok[r]);
+            for (int r = 0; r < NR; ++r) c = bcnt_acc(ok[r], c);
             c = av ? c : 0u;
         }
         cnt[cnt_off(g, lane)] = (uint16_t)c;
         total += c;
 #pragma unroll
-        for (int k = 0; k < 12; ++k) w[k] = nx[k];
+        for (int k = 0; k < 4; ++k) w[k] = nx[k];
     }
     return total;
 }
 
+#define BK_RANGE(G) BK_GRP_##G
 __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint16_t* cnt, int lane) {
-    return count_range<true>(0, BK_STENCIL_PAIR_INIT, P, avail, cnt, lane) +
-           count_range<false>(BK_STENCIL_PAIR_INIT, BK_NUM_ORIENTS, P, avail, cnt, lane);
+    uint32_t t = 0;
+    t += count_range<true, 1>(BK_GRP_P1, P, avail, cnt, lane);
+    t += count_range<true, 2>(BK_GRP_P2, P, avail, cnt, lane);
+    t += count_range<true, 3>(BK_GRP_P3, P, avail, cnt, lane);
+    t += count_range<true, 4>(BK_GRP_P4, P, avail, cnt, lane);
+    t += count_range<true, 5>(BK_GRP_P5, P, avail, cnt, lane);
+    t += count_range<false, 1>(BK_GRP_S1, P, avail, cnt, lane);
+    t += count_range<false, 2>(BK_GRP_S2, P, avail, cnt, lane);
+    t += count_range<false, 3>(BK_GRP_S3, P, avail, cnt, lane);
+    t += count_range<false, 4>(BK_GRP_S4, P, avail, cnt, lane);
+    t += count_range<false, 5>(BK_GRP_S5, P, avail, cnt, lane);
+    return t;
 }
 
-// Dense legal rows of every orientation (k_movegen): calls f(g, ok, available)
-template <bool PAIR_INIT, typename F>
+// Dense legal rows of every orientation (k_movegen): calls f(g, piece, ok)
+template <bool PAIR_INIT, int H, typename F>
 __device__ __forceinline__ void rows_range(int i0, int i1, const Planes& P, F&& f) {
-    uint32_t w[12];
+    uint32_t w[4];
 #pragma unroll 1
     for (int i = i0; i < i1; ++i) {
         load_words(i, w);
         uint32_t ok[20];
-        scan_words<PAIR_INIT>(w, P, ok);
+        scan_words<PAIR_INIT, H>(w, P, ok);
         f((int)(w[0] >> 16), w[0] & 0xFFu, ok);
     }
+}
+
+template <typename F>
+__device__ __forceinline__ void all_rows(const Planes& P, F&& f) {
+    rows_range<true, 1>(BK_GRP_P1, P, f);
+    rows_range<true, 2>(BK_GRP_P2, P, f);
+    rows_range<true, 3>(BK_GRP_P3, P, f);
+    rows_range<true, 4>(BK_GRP_P4, P, f);
+    rows_range<true, 5>(BK_GRP_P5, P, f);
+    rows_range<false, 1>(BK_GRP_S1, P, f);
+    rows_range<false, 2>(BK_GRP_S2, P, f);
+    rows_range<false, 3>(BK_GRP_S3, P, f);
+    rows_range<false, 4>(BK_GRP_S4, P, f);
+    rows_range<false, 5>(BK_GRP_S5, P, f);
 }
 
 // orientation holding the k-th legal move (naive order: g ascending) and its rank in it
@@ -410,8 +452,7 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
             if (live) dst[q] = v;
         }
     };
-    rows_range<true>(0, BK_STENCIL_PAIR_INIT, P, emit);
-    rows_range<false>(BK_STENCIL_PAIR_INIT, BK_NUM_ORIENTS, P, emit);
+    all_rows(P, emit);
     if (live && a.out_count) a.out_count[i] = total;
 }
 
@@ -647,7 +688,7 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
     return v;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_rollout(RolloutArgs a) {
+__global__ __launch_bounds__(BLOCK, 3) void k_rollout(RolloutArgs a) {
     __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
