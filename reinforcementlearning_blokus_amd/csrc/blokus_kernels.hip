@@ -262,18 +262,24 @@ __device__ __forceinline__ void all_rows(const Planes& P, F&& f) {
 // orientation holding the k-th legal move (naive order: g ascending) and its rank in it
 __device__ __forceinline__ int pick_orient(const uint16_t* cnt, int lane, uint32_t k, uint32_t& kk) {
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(cnt);
+    constexpr int NW = (BK_NUM_ORIENTS + 1) / 2;
     uint32_t run = 0;
     int gs = BK_NUM_ORIENTS - 1;
     uint32_t before = 0;
     bool found = false;
 #pragma unroll 1
-    for (int h = 0; h < (BK_NUM_ORIENTS + 1) / 2; ++h) {
-        const uint32_t v = c32[h * WAVE + lane];
-        const uint32_t lo = v & 0xFFFFu, hi = v >> 16;
-        if (!found && k < run + lo) { gs = 2 * h; before = run; found = true; }
-        run += lo;
-        if (!found && k < run + hi) { gs = 2 * h + 1; before = run; found = true; }
-        run += hi;
+    for (int h0 = 0; h0 < NW; h0 += 8) {  // 8 LDS reads in flight per batch
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (h0 + j < NW) ? c32[(h0 + j) * WAVE + lane] : 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t lo = v[j] & 0xFFFFu, hi = v[j] >> 16;
+            if (!found && k < run + lo) { gs = 2 * (h0 + j); before = run; found = true; }
+            run += lo;
+            if (!found && k < run + hi) { gs = 2 * (h0 + j) + 1; before = run; found = true; }
+            run += hi;
+        }
     }
     kk = k - before;
     return gs;
@@ -765,14 +771,27 @@ __global__ __launch_bounds__(BLOCK, 3) void k_rollout(RolloutArgs a) {
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
         const uint32_t info = kInfo[gs];
         const int n = (int)((info >> 8) & 0xFFu);
+        {   // per piece row d: one mask; all row loads issued before any store
+            uint32_t m[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-            if (q < n) {
+            for (int q = 0; q < 5; ++q) {
                 const uint32_t cell = kCells[gs][q];
-                const int R = ar + (int)(cell >> 8);
-                const uint32_t bit = 0x80000000u >> (ac + (int)(cell & 0xFFu));
-                slab.at(p, R) |= bit;
-                slab.at(4, R) |= bit;
+                const uint32_t bit = q < n ? (0x80000000u >> (ac + (int)(cell & 0xFFu))) : 0u;
+#pragma unroll
+                for (int d = 0; d < 5; ++d) m[d] |= ((cell >> 8) == (uint32_t)d) ? bit : 0u;
+            }
+            uint32_t ow[5], oc[5];
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                ow[d] = m[d] ? slab.at(p, ar + d) : 0u;
+                oc[d] = m[d] ? slab.at(4, ar + d) : 0u;
+            }
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                if (m[d]) {
+                    slab.at(p, ar + d) = ow[d] | m[d];
+                    slab.at(4, ar + d) = oc[d] | m[d];
+                }
             }
         }
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
