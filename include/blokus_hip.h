@@ -162,6 +162,38 @@ int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_
                int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
                bk_state* out_states, int mem);
 
+/*
+ * FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256) for n_games independent
+ * roots, one wave per game.  Game i's root children are legal[legal_offset[i] ..
+ * legal_offset[i+1]) (any int payload; only the count and order matter: expansion pops
+ * the LAST entry first, fast_mcts_agent.py:62).  Each iteration expands an untried
+ * child or picks the UCB1 argmax (first max in child order; exploration term
+ * c*sqrt(2*log(root_visits)/visits) with log taken from log_table, which the host fills
+ * with CPython math.log(i) for i < log_len), then adds reward = base[i] +
+ * random()*0.1, random() being CPython random.Random's genrand_res53 from the state
+ * mt_state[i] (625 words: random.getstate()[1]); a NaN base[i] means reward 0.0 with no
+ * draw (empty cached legal list, fast_mcts_agent.py:255).  mt_state is in/out: the
+ * advanced state is written back.  Results per game in out; visits_out (optional, may
+ * be NULL) receives every root child's visit count at its legal index (flat, by
+ * legal_offset; 0 = never expanded).  Replaces the per-iteration
+ * Python loop of FastMCTSAgent.think (fast_mcts_agent.py:153-166).
+ */
+#define BK_FASTMCTS_TOP 10
+#define BK_FASTMCTS_MAX_CHILDREN 2048
+typedef struct bk_fastmcts_out {
+    int32_t best_index;   /* index into the game's legal list of the most visited child  */
+    int32_t iterations;   /* iterations run                                              */
+    int32_t n_children;   /* root children expanded                                      */
+    int32_t n_top;        /* entries used in top_*                                       */
+    int32_t top_index[BK_FASTMCTS_TOP];  /* by visits desc, ties in child order        */
+    int32_t top_visits[BK_FASTMCTS_TOP];
+    double top_q[BK_FASTMCTS_TOP];       /* total_reward / visits                       */
+} bk_fastmcts_out;
+
+int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,
+                const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
+                double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem);
+
 /* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
    stream, measured with HIP events around that launch. */
 int bk_last_kernel_ms(bk_handle h, float* ms);

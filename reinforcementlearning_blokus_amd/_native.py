@@ -10,6 +10,8 @@ import ctypes as C
 import os
 import threading
 
+import numpy as np
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libblokus_hip.so")
 
@@ -25,8 +27,10 @@ STREAM_OWN = (1 << 64) - 1  # BK_STREAM_OWN
 EXPORTS = (
     "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream",
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
-    "bk_rollout", "bk_advance", "bk_last_kernel_ms",
+    "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
 )
+FASTMCTS_TOP = 10
+FASTMCTS_MAX_CHILDREN = 2048
 
 
 class NativeUnavailable(RuntimeError):
@@ -50,10 +54,20 @@ class BkRolloutCfg(C.Structure):
                 ("seed", C.c_uint64), ("seats_share_stream", C.c_int32), ("reserved", C.c_int32)]
 
 
+class BkFastMctsOut(C.Structure):
+    _fields_ = [("best_index", C.c_int32), ("iterations", C.c_int32), ("n_children", C.c_int32),
+                ("n_top", C.c_int32), ("top_index", C.c_int32 * 10), ("top_visits", C.c_int32 * 10),
+                ("top_q", C.c_double * 10)]
+
+
+assert C.sizeof(BkFastMctsOut) == 176
+FASTMCTS_OUT_DTYPE = np.dtype([("best_index", "<i4"), ("iterations", "<i4"), ("n_children", "<i4"),
+                               ("n_top", "<i4"), ("top_index", "<i4", (10,)), ("top_visits", "<i4", (10,)),
+                               ("top_q", "<f8", (10,))])
+assert FASTMCTS_OUT_DTYPE.itemsize == 176
 assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRolloutCfg) == 32
 
 # numpy views of the same records
-import numpy as np  # noqa: E402
 
 STATE_DTYPE = np.dtype([("planes", "<u8", (4, 7)), ("used", "<u4", (4,)), ("first_move", "u1"),
                         ("current_player", "u1"), ("out_mask", "u1"), ("flags", "u1"),
@@ -94,6 +108,7 @@ def load():
             "bk_has_moves": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int]),
             "bk_rollout": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
             "bk_advance": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
+            "bk_fastmcts": (C.c_int, [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32, C.c_double, vp, vp, C.c_int]),
             "bk_last_kernel_ms": (C.c_int, [vp, P(C.c_float)]),
         }
         for name, (res, args) in sigs.items():
@@ -182,6 +197,14 @@ class Handle:
             rc = self._L.bk_rollout(self._h, C.c_void_p(roots_ptr), n_roots, C.c_void_p(index_ptr or 0),
                                     n_playouts, C.byref(cfg), C.c_void_p(seeds_ptr or 0), C.c_void_p(out_ptr), mem)
         self.check(rc, "bk_rollout")
+
+    def fastmcts(self, n_games, offset_ptr, iters_ptr, base_ptr, mt_ptr, log_ptr, log_len, c, out_ptr, visits_ptr,
+                 mem):
+        with self._lock:
+            rc = self._L.bk_fastmcts(self._h, n_games, C.c_void_p(offset_ptr), C.c_void_p(iters_ptr),
+                                     C.c_void_p(base_ptr), C.c_void_p(mt_ptr), C.c_void_p(log_ptr), log_len,
+                                     float(c), C.c_void_p(out_ptr), C.c_void_p(visits_ptr or None), mem)
+        self.check(rc, "bk_fastmcts")
 
     def advance(self, roots_ptr, n_roots, index_ptr, n, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
         with self._lock:

@@ -803,6 +803,165 @@ __global__ __launch_bounds__(BLOCK, 3) void k_rollout(RolloutArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256): one wave per game
+// ------------------------------------------------------------------------------------
+#define FM_N 624
+#define FM_M 397
+// bit-exact with CPython floats: no a*b+c fusion anywhere below
+#pragma clang fp contract(off)
+
+__device__ __forceinline__ uint32_t mt_y(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// new mt[kk] = mt[kk + off] ^ twist(mt[kk], mt[kk+1]) for kk in [lo, hi), 64 lanes at a
+// time; each chunk reads before it writes, and no chunk reads what a later chunk writes
+__device__ __forceinline__ void twist_range(uint32_t* mt, int lo, int hi, int off, int lane) {
+    for (int k0 = lo; k0 < hi; k0 += WAVE) {
+        const int k = k0 + lane;
+        uint32_t v = 0;
+        if (k < hi) v = mt[k + off] ^ mt_y(mt[k], mt[k + 1]);
+        __syncthreads();
+        if (k < hi) mt[k] = v;
+        __syncthreads();
+    }
+}
+
+// CPython genrand_uint32's twist (Modules/_randommodule.c), parallel in four phases
+__device__ void py_twist(uint32_t* mt, int lane) {
+    twist_range(mt, 0, FM_N - FM_M, FM_M, lane);                            // old mt[kk+397]
+    twist_range(mt, FM_N - FM_M, 2 * (FM_N - FM_M), FM_M - FM_N, lane);     // new mt[0..227)
+    twist_range(mt, 2 * (FM_N - FM_M), FM_N - 1, FM_M - FM_N, lane);        // new mt[227..396)
+    if (lane == 0) mt[FM_N - 1] = mt[FM_M - 1] ^ mt_y(mt[FM_N - 1], mt[0]);
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t py_next(uint32_t* mt, int& idx, int lane) {
+    if (idx >= FM_N) { py_twist(mt, lane); idx = 0; }
+    uint32_t y = mt[idx++];
+    y ^= y >> 11; y ^= (y << 7) & 0x9d2c5680u; y ^= (y << 15) & 0xefc60000u; y ^= y >> 18;
+    return y;
+}
+
+__device__ __forceinline__ double py_random(uint32_t* mt, int& idx, int lane) {
+    const uint32_t a = py_next(mt, idx, lane) >> 5, b = py_next(mt, idx, lane) >> 6;
+    return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
+}
+
+struct FastMctsArgs {
+    int32_t n_games;
+    const int32_t* offset;
+    const int32_t* iterations;
+    const double* base;
+    uint32_t* mt_state;
+    const double* log_table;
+    int32_t log_len;
+    double c;
+    bk_fastmcts_out* out;
+    int32_t* visits_out;  // optional: per legal index, flat by legal_offset
+    uint32_t* err;
+};
+
+// wave argmax of (value, index): larger value wins, ties -> smaller index
+__device__ __forceinline__ void wave_argmax(double& v, int& j) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double ov = __shfl_xor(v, o);
+        const int oj = __shfl_xor(j, o);
+        if (ov > v || (ov == v && oj < j)) { v = ov; j = oj; }
+    }
+}
+
+__global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
+    __shared__ uint32_t visits[BK_FASTMCTS_MAX_CHILDREN];
+    __shared__ double total[BK_FASTMCTS_MAX_CHILDREN];
+    __shared__ uint32_t mt[FM_N];
+    const int lane = threadIdx.x;
+    const int game = blockIdx.x;
+    if (game >= a.n_games) return;
+    const int n = a.offset[game + 1] - a.offset[game];
+    const int iters = a.iterations[game];
+    const double base = a.base[game];
+    uint32_t* st = a.mt_state + (size_t)game * (FM_N + 1);
+    for (int k = lane; k < FM_N; k += WAVE) mt[k] = st[k];
+    int idx = (int)st[FM_N];
+    for (int k = lane; k < n && k < BK_FASTMCTS_MAX_CHILDREN; k += WAVE) { visits[k] = 0; total[k] = 0.0; }
+    __syncthreads();
+    if (n > BK_FASTMCTS_MAX_CHILDREN || iters >= a.log_len) {
+        if (lane == 0) atomicOr(a.err, 1u);
+        return;
+    }
+    int nch = 0;
+    uint32_t root_visits = 0;
+    int it = 0;
+    for (; it < iters; ++it) {
+        int sel;
+        if (nch < n) {
+            sel = nch++;  // expand: untried_moves.pop() -> child nch <-> legal[n - 1 - nch]
+        } else {
+            const double L2 = 2.0 * a.log_table[root_visits];
+            double best = -1.0 / 0.0;
+            int bj = 0x7fffffff;
+            for (int j = lane; j < nch; j += WAVE) {
+                const double v = (double)visits[j];
+                const double u = total[j] / v + a.c * sqrt(L2 / v);
+                if (u > best) { best = u; bj = j; }
+            }
+            wave_argmax(best, bj);
+            sel = bj;
+        }
+        // NaN base: the cached legal list was empty -> reward 0.0 and no draw
+        // (fast_mcts_agent.py:255-257)
+        const double reward = (base == base) ? base + py_random(mt, idx, lane) * 0.1 : 0.0;
+        if (lane == 0) {
+            visits[sel] += 1u;
+            total[sel] += reward;
+        }
+        __syncthreads();
+        root_visits += 1u;
+    }
+    if (a.visits_out) {
+        int32_t* vo = a.visits_out + a.offset[game];
+        for (int k = lane; k < n; k += WAVE) vo[k] = (n - 1 - k < nch) ? (int32_t)visits[n - 1 - k] : 0;
+    }
+    // hand the advanced generator state back (random.setstate on the host)
+    for (int k = lane; k < FM_N; k += WAVE) st[k] = mt[k];
+    if (lane == 0) st[FM_N] = (uint32_t)idx;
+    // results
+    bk_fastmcts_out* o = a.out + game;
+    if (lane == 0) { o->iterations = it; o->n_children = nch; }
+    // best = most visited child, first on ties
+    {
+        double bv = -1.0;
+        int bj = 0x7fffffff;
+        for (int j = lane; j < nch; j += WAVE)
+            if ((double)visits[j] > bv) { bv = (double)visits[j]; bj = j; }
+        wave_argmax(bv, bj);
+        if (lane == 0) o->best_index = nch > 0 ? n - 1 - bj : 0;
+    }
+    // top moves: stable sort by visits desc (selection, marking picked children)
+    int ntop = 0;
+    for (int t = 0; t < BK_FASTMCTS_TOP && t < nch; ++t) {
+        double bv = -1.0;
+        int bj = 0x7fffffff;
+        for (int j = lane; j < nch; j += WAVE)
+            if (!(visits[j] & 0x80000000u) && (double)visits[j] > bv) { bv = (double)visits[j]; bj = j; }
+        wave_argmax(bv, bj);
+        if (lane == 0) {
+            const uint32_t v = visits[bj];
+            o->top_index[t] = n - 1 - bj;
+            o->top_visits[t] = (int32_t)v;
+            o->top_q[t] = total[bj] / (double)v;
+            visits[bj] = v | 0x80000000u;
+        }
+        __syncthreads();
+        ++ntop;
+    }
+    if (lane == 0) o->n_top = ntop;
+}
+
+// ------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------
 struct bk_handle_s {
@@ -1097,6 +1256,74 @@ int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_
     if (!out_states || !cfg || cfg->semantics != BK_SEM_ADVANCE)
         return set_err(h, BK_EINVAL, "bk_advance: needs out_states and BK_SEM_ADVANCE%s", "");
     return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, nullptr, out_states, mem);
+}
+
+int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,
+                const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
+                double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem) {
+    if (!h || n_games < 0 || !legal_offset || !iterations || !base || !mt_state || !log_table || log_len <= 0 ||
+        !out || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
+        return set_err(h, BK_EINVAL, "bk_fastmcts: invalid arguments%s", "");
+    if (n_games == 0) return BK_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    const size_t b_off = sizeof(int32_t) * (size_t)(n_games + 1), b_it = sizeof(int32_t) * (size_t)n_games,
+                 b_base = sizeof(double) * (size_t)n_games, b_mt = sizeof(uint32_t) * 625 * (size_t)n_games,
+                 b_log = sizeof(double) * (size_t)log_len, b_out = sizeof(bk_fastmcts_out) * (size_t)n_games;
+    const int32_t* d_off = legal_offset;
+    const int32_t* d_it = iterations;
+    const double* d_base = base;
+    uint32_t* d_mt = mt_state;
+    const double* d_log = log_table;
+    bk_fastmcts_out* d_out = out;
+    int32_t* d_vis = visits_out;
+    int32_t n_legal_total = 0;
+    if (mem == BK_MEM_HOST) {
+        if (legal_offset[0] != 0) return set_err(h, BK_EINVAL, "bk_fastmcts: legal_offset[0] must be 0%s", "");
+        for (int32_t i = 0; i < n_games; ++i)
+            if (legal_offset[i + 1] < legal_offset[i] || iterations[i] < 0 || iterations[i] >= log_len)
+                return set_err(h, BK_EINVAL, "bk_fastmcts: bad legal_offset/iterations%s", "");
+        n_legal_total = legal_offset[n_games];
+    }
+    if (mem == BK_MEM_HOST) {
+        // one staging buffer, 16-byte aligned sections
+        auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+        const size_t tot = al(b_off) + al(b_it) + al(b_base) + al(b_mt) + al(b_log);
+        int rc = grow(h, &h->d_in, &h->d_in_cap, tot);
+        if (rc) return rc;
+        rc = grow(h, &h->d_out, &h->d_out_cap, b_out);
+        if (rc) return rc;
+        char* p = (char*)h->d_in;
+        HIPCHK(h, hipMemcpyAsync(p, legal_offset, b_off, hipMemcpyHostToDevice, h->cur)); d_off = (const int32_t*)p; p += al(b_off);
+        HIPCHK(h, hipMemcpyAsync(p, iterations, b_it, hipMemcpyHostToDevice, h->cur)); d_it = (const int32_t*)p; p += al(b_it);
+        HIPCHK(h, hipMemcpyAsync(p, base, b_base, hipMemcpyHostToDevice, h->cur)); d_base = (const double*)p; p += al(b_base);
+        HIPCHK(h, hipMemcpyAsync(p, mt_state, b_mt, hipMemcpyHostToDevice, h->cur)); d_mt = (uint32_t*)p; p += al(b_mt);
+        HIPCHK(h, hipMemcpyAsync(p, log_table, b_log, hipMemcpyHostToDevice, h->cur)); d_log = (const double*)p;
+        d_out = (bk_fastmcts_out*)h->d_out;
+        if (visits_out) {
+            rc = grow(h, &h->d_aux, &h->d_aux_cap, sizeof(int32_t) * (size_t)n_legal_total + 4);
+            if (rc) return rc;
+            d_vis = (int32_t*)h->d_aux;
+        }
+    }
+    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
+    FastMctsArgs a{n_games, d_off, d_it, d_base, d_mt, d_log, log_len, exploration, d_out, d_vis, h->d_counter + 1};
+    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    hipLaunchKernelGGL(k_fastmcts, dim3(n_games), dim3(WAVE), 0, h->cur, a);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
+    h->timed = true;
+    if (mem == BK_MEM_HOST) {
+        uint32_t ctr[4];
+        HIPCHK(h, hipMemcpyAsync(out, d_out, b_out, hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipMemcpyAsync(mt_state, d_mt, b_mt, hipMemcpyDeviceToHost, h->cur));
+        if (visits_out && n_legal_total > 0)
+            HIPCHK(h, hipMemcpyAsync(visits_out, d_vis, sizeof(int32_t) * (size_t)n_legal_total,
+                                     hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipStreamSynchronize(h->cur));
+        if (ctr[1]) return set_err(h, BK_EINVAL, "bk_fastmcts: too many children or log table too short%s", "");
+    }
+    return BK_OK;
 }
 
 }  // extern "C"

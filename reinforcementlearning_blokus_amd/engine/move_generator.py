@@ -1,0 +1,267 @@
+"""LegalMoveGenerator on the MI355X (reference: engine/move_generator.py).
+
+get_legal_moves computes the legal SET on the GPU (bk_movegen: dense 91x20 anchor
+masks) and orders it on the host exactly as the reference does:
+
+* frontier order (default, BLOKUS_USE_FRONTIER_MOVEGEN unset/1; _get_legal_moves_frontier,
+  move_generator.py:261-559): piece asc, orientation asc, then the first (frontier cell,
+  anchor index) that produced the move -- i.e. key min over the move's cells k lying on
+  a frontier cell f of (rank of f in ``list(board.get_frontier(player))``, k);
+* naive order (BLOKUS_USE_FRONTIER_MOVEGEN=0; _get_legal_moves_naive :153-259): piece,
+  orientation, anchor row-major -- the order the dense masks already have.
+
+There is no CPU move generator behind this class: without the HIP library or a GPU
+every generation call raises NativeUnavailable.  Only single-move validation
+(is_move_legal, used by BlokusGame.make_move) runs on the host.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .bitboard import BIT_TABLE
+from .board import Board, Player, Position
+from .pieces import (ALL_PIECE_ORIENTATIONS, GID, ORIENT_CELLS, ORIENT_LIST, PieceGenerator,
+                     PieceOrientation, PiecePlacement)
+
+logger = logging.getLogger(__name__)
+
+
+def _env_flag(name: str, default: bool) -> bool:
+    raw = os.getenv(name)
+    return default if raw is None else raw.lower() in ("1", "true", "yes", "on")
+
+
+MOVEGEN_DEBUG = _env_flag("BLOKUS_MOVEGEN_DEBUG", False)
+USE_FRONTIER_MOVEGEN = _env_flag("BLOKUS_USE_FRONTIER_MOVEGEN", True)
+USE_BITBOARD_LEGALITY = _env_flag("BLOKUS_USE_BITBOARD_LEGALITY", True)   # accepted, no effect
+USE_HEURISTIC_ANCHORS = _env_flag("BLOKUS_USE_HEURISTIC_ANCHORS", False)  # accepted, no effect
+MOVEGEN_DEBUG_EQUIVALENCE = _env_flag("BLOKUS_MOVEGEN_DEBUG_EQUIVALENCE", False)
+DEBUG_BITBOARD = _env_flag("BLOKUS_DEBUG_BITBOARD", False)
+
+_PLAYERS = list(Player)
+
+# per-orientation cell offsets as padded arrays (for vectorised ordering)
+_NCELLS = np.array([len(c) for c in ORIENT_CELLS], dtype=np.int64)
+_DR = np.zeros((len(ORIENT_CELLS), 5), dtype=np.int64)
+_DC = np.zeros((len(ORIENT_CELLS), 5), dtype=np.int64)
+for _g, _cells in enumerate(ORIENT_CELLS):
+    for _k, (_r, _c) in enumerate(_cells):
+        _DR[_g, _k], _DC[_g, _k] = _r, _c
+_PID = np.array([p for p, _ in ORIENT_LIST], dtype=np.int64)
+_OID = np.array([o for _, o in ORIENT_LIST], dtype=np.int64)
+_BIG = 1 << 40
+
+
+class Move:
+    """A placement: piece id, orientation index, anchor (top-left of the bounding box)."""
+
+    def __init__(self, piece_id: int, orientation: int, anchor_row: int, anchor_col: int):
+        self.piece_id = piece_id
+        self.orientation = orientation
+        self.anchor_row = anchor_row
+        self.anchor_col = anchor_col
+
+    def get_positions(self, piece_orientations: List) -> List[Position]:
+        shape = piece_orientations[self.orientation]
+        return [Position(r, c) for r, c in PiecePlacement.get_piece_positions(shape, self.anchor_row, self.anchor_col)]
+
+    def __str__(self):
+        return (f"Move(piece_id={self.piece_id}, orientation={self.orientation}, "
+                f"anchor=({self.anchor_row}, {self.anchor_col}))")
+
+    __repr__ = __str__
+
+
+def _rows_to_naive(rows: np.ndarray):
+    """uint32[91,20] masks -> (g, r, c) arrays in naive order."""
+    bits = np.unpackbits(np.ascontiguousarray(rows, dtype="<u4").view(np.uint8).reshape(91, 20, 4),
+                         axis=2, bitorder="little")
+    g, r, c = np.nonzero(bits)
+    return g, r, c
+
+
+def order_moves(rows: np.ndarray, frontier: Optional[Sequence] = None):
+    """Order the legal moves of one board-player.
+
+    rows: uint32[91,20] GPU masks.  frontier: iteration-order list of (row, col) of
+    the player's frontier set, or None for naive order.  Returns (g, r, c) arrays.
+    """
+    g, r, c = _rows_to_naive(rows)
+    if frontier is None or len(g) == 0:
+        return g, r, c
+    rank = np.full(400, _BIG, dtype=np.int64)
+    for i, (fr, fc) in enumerate(frontier):
+        if rank[fr * 20 + fc] == _BIG:
+            rank[fr * 20 + fc] = i
+    cells = (r[:, None] + _DR[g]) * 20 + (c[:, None] + _DC[g])
+    valid = np.arange(5)[None, :] < _NCELLS[g][:, None]
+    cells = np.where(valid, np.clip(cells, 0, 399), 0)
+    key = np.where(valid, rank[cells] * 8 + np.arange(5)[None, :], _BIG * 8)
+    key = key.min(axis=1)
+    order = np.lexsort((key, g))
+    return g[order], r[order], c[order]
+
+
+class LegalMoveGenerator:
+    """Drop-in for engine.move_generator.LegalMoveGenerator, GPU-backed."""
+
+    def __init__(self, device: int = 0):
+        self.piece_generator = PieceGenerator()
+        self.all_pieces = self.piece_generator.get_all_pieces()
+        self.piece_orientations_cache = {}
+        self.piece_position_cache = {}
+        for piece in self.all_pieces:
+            shapes = self.piece_generator.get_piece_rotations_and_reflections(piece)
+            self.piece_orientations_cache[piece.id] = shapes
+            self.piece_position_cache[piece.id] = [PiecePlacement.get_piece_positions(s, 0, 0) for s in shapes]
+        self.device = device
+        self._gpu = threading.local()
+
+    # ------------------------------------------------------------------ GPU
+    def _engine(self):
+        eng = getattr(self._gpu, "engine", None)
+        if eng is None:
+            from ..gpu import BlokusGPU
+            eng = BlokusGPU(self.device)  # raises NativeUnavailable without library/GPU
+            self._gpu.engine = eng
+        return eng
+
+    def _masks(self, boards: Sequence[Board], players: Sequence[Player]):
+        from .board import pack_states
+        states = pack_states(boards)
+        pl = np.array([p.value - 1 for p in players], dtype=np.uint8)
+        return self._engine().movegen(states, pl, rows=True)
+
+    @staticmethod
+    def _to_moves(g, r, c) -> List[Move]:
+        return [Move(int(_PID[gi]), int(_OID[gi]), int(ri), int(ci)) for gi, ri, ci in zip(g, r, c)]
+
+    # ------------------------------------------------------------------ API
+    def get_legal_moves(self, board: Board, player: Player) -> List[Move]:
+        if USE_FRONTIER_MOVEGEN:
+            return self._get_legal_moves_frontier(board, player)
+        return self._get_legal_moves_naive(board, player)
+
+    def get_legal_moves_batch(self, boards: Sequence[Board], players: Sequence[Player],
+                              order: str = "frontier" if USE_FRONTIER_MOVEGEN else "naive") -> List[List[Move]]:
+        """One GPU launch for many (board, player) pairs."""
+        if not boards:
+            return []
+        _, rows = self._masks(boards, players)
+        out = []
+        for i, (b, p) in enumerate(zip(boards, players)):
+            fr = list(b.get_frontier(p)) if order == "frontier" else None
+            out.append(self._to_moves(*order_moves(rows[i], fr)))
+        return out
+
+    def _get_legal_moves_naive(self, board: Board, player: Player) -> List[Move]:
+        _, rows = self._masks([board], [player])
+        return self._to_moves(*order_moves(rows[0], None))
+
+    def _get_legal_moves_frontier(self, board: Board, player: Player) -> List[Move]:
+        _, rows = self._masks([board], [player])
+        return self._to_moves(*order_moves(rows[0], list(board.get_frontier(player))))
+
+    def get_move_count(self, board: Board, player: Player) -> int:
+        from .board import pack_states
+        cnt, _ = self._engine().movegen(pack_states([board]), np.array([player.value - 1], np.uint8), rows=False)
+        return int(cnt[0])
+
+    def has_legal_moves(self, board: Board, player: Player) -> bool:
+        return self.get_move_count(board, player) > 0
+
+    def _has_any_legal_move_frontier(self, board: Board, player: Player) -> bool:
+        return self.has_legal_moves(board, player)
+
+    def get_legal_moves_for_piece(self, board: Board, player: Player, piece_id: int) -> List[Move]:
+        if piece_id in board.player_pieces_used[player]:
+            return []
+        _, rows = self._masks([board], [player])
+        g, r, c = order_moves(rows[0], None)
+        keep = _PID[g] == piece_id
+        return self._to_moves(g[keep], r[keep], c[keep])
+
+    # ------------------------------------------------------------- host checks
+    def is_move_legal(self, board: Board, player: Player, move: Move) -> bool:
+        """Single-move validation on the host (engine/move_generator.py:912-946)."""
+        if move.piece_id in board.player_pieces_used[player]:
+            return False
+        shapes = self.piece_orientations_cache.get(move.piece_id, [])
+        if not 0 <= move.orientation < len(shapes):
+            return False
+        shape = shapes[move.orientation]
+        if not PiecePlacement.can_place_piece_at((board.SIZE, board.SIZE), shape, move.anchor_row, move.anchor_col):
+            return False
+        return board.can_place_piece(move.get_positions(shapes), player)
+
+    def is_placement_legal_bitboard_fast(self, board: Board, player: Player, piece_orientation: PieceOrientation,
+                                         anchor_row: int, anchor_col: int, is_first_move: bool = False) -> bool:
+        """Single-anchor legality from bitboards (move_generator.py:760-831)."""
+        cells = [(anchor_row + r, anchor_col + c) for r, c in piece_orientation.offsets]
+        return self.is_placement_legal_bitboard_coords(board, player, cells, is_first_move=is_first_move)
+
+    def is_placement_legal_bitboard_coords(self, board: Board, player: Player, placement_coords,
+                                           *, is_first_move: bool = False) -> bool:
+        n = board.SIZE
+        if any(not (0 <= r < n and 0 <= c < n) for r, c in placement_coords):
+            return False
+        shape = 0
+        for r, c in placement_coords:
+            shape |= BIT_TABLE[r][c]
+        if shape & board.occupied_bits:
+            return False
+        own = board.player_bits[player]
+        cs = set(placement_coords)
+        diag = orth = 0
+        for r, c in placement_coords:
+            for dr, dc in ((-1, 0), (1, 0), (0, -1), (0, 1)):
+                rr, cc = r + dr, c + dc
+                if 0 <= rr < n and 0 <= cc < n and (rr, cc) not in cs:
+                    orth |= BIT_TABLE[rr][cc]
+            for dr, dc in ((-1, -1), (-1, 1), (1, -1), (1, 1)):
+                rr, cc = r + dr, c + dc
+                if 0 <= rr < n and 0 <= cc < n and (rr, cc) not in cs:
+                    diag |= BIT_TABLE[rr][cc]
+        if orth & own:
+            return False
+        if is_first_move:
+            corner = board.player_start_corners[player]
+            return bool(shape & BIT_TABLE[corner.row][corner.col])
+        return bool(diag & own)
+
+    def get_game_state_summary(self, board: Board) -> dict:
+        return {
+            "current_player": board.current_player, "move_count": board.move_count,
+            "game_over": board.game_over,
+            "player_moves": {p.name: self.get_move_count(board, p) for p in Player},
+            "player_scores": {p.name: board.get_score(p) for p in Player},
+            "player_pieces_used": {p.name: len(board.player_pieces_used[p]) for p in Player},
+        }
+
+
+_SHARED: Optional[LegalMoveGenerator] = None
+_SHARED_LOCK = threading.Lock()
+
+
+def get_shared_generator() -> LegalMoveGenerator:
+    global _SHARED
+    with _SHARED_LOCK:
+        if _SHARED is None:
+            _SHARED = LegalMoveGenerator()
+    return _SHARED
+
+
+def move_to_int(m: Move) -> int:
+    """g * 400 + row * 20 + col (the Discrete(36400) action id)."""
+    return GID[(m.piece_id, m.orientation)] * 400 + m.anchor_row * 20 + m.anchor_col
+
+
+def int_to_move(a: int) -> Move:
+    g, rest = divmod(int(a), 400)
+    pid, o = ORIENT_LIST[g]
+    return Move(pid, o, rest // 20, rest % 20)

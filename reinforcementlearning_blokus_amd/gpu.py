@@ -142,6 +142,31 @@ class BlokusGPU:
                             out.ctypes.data, N.MEM_HOST)
         return out
 
+    # ------------------------------------------------------------------ FastMCTS
+    def fastmcts(self, n_legal, iterations, base, mt_state, log_table, exploration: float,
+                 want_visits: bool = False):
+        """Run FastMCTSAgent's bandit loop for a batch of roots (bk_fastmcts).
+
+        n_legal[i]: root legal-move count; iterations[i]; base[i]: deterministic part of
+        the rollout reward (NaN = empty cached list); mt_state: uint32[n,625] CPython
+        random states, advanced in place; log_table[k] = math.log(k).
+        Returns a FASTMCTS_OUT_DTYPE record array (and, with want_visits, the flat int32
+        visit counts per legal index)."""
+        n = len(n_legal)
+        off = np.zeros(n + 1, dtype=np.int32)
+        np.cumsum(np.asarray(n_legal, dtype=np.int32), out=off[1:])
+        it = np.ascontiguousarray(iterations, dtype=np.int32)
+        b = np.ascontiguousarray(base, dtype=np.float64)
+        assert mt_state.dtype == np.uint32 and mt_state.shape == (n, 625) and mt_state.flags.c_contiguous
+        lt = np.ascontiguousarray(log_table, dtype=np.float64)
+        out = np.zeros(n, dtype=N.FASTMCTS_OUT_DTYPE)
+        vis = np.zeros(max(int(off[-1]), 1), dtype=np.int32) if want_visits else None
+        self.handle.set_stream(None)
+        self.handle.fastmcts(n, off.ctypes.data, it.ctypes.data, b.ctypes.data, mt_state.ctypes.data,
+                             lt.ctypes.data, len(lt), exploration, out.ctypes.data,
+                             vis.ctypes.data if vis is not None else 0, N.MEM_HOST)
+        return (out, vis[: int(off[-1])]) if want_visits else out
+
 
 def empty_state() -> np.ndarray:
     """The initial position (engine/board.py:54-78): nobody has moved, RED to play."""

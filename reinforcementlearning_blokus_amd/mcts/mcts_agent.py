@@ -1,0 +1,242 @@
+"""UCT MCTS with GPU rollouts (reference: mcts/mcts_agent.py).
+
+Tree policy, expansion (``untried_moves.pop()``: last legal move first), UCB1 with
+numpy log/sqrt, best = most visited child (first on ties) and the Zobrist
+transposition cache follow mcts/mcts_agent.py:19-191, :304-437, :572-582.
+
+Rollouts (mcts/mcts_agent.py:470-554, <= max_rollout_moves plies, stop at the first
+player without a move, reward = final - initial Board.get_score of the root player)
+have two GPU backends:
+
+* ``rollout_backend="exact"`` (default when a rollout_agent with ``select_action`` is
+  given, e.g. RandomAgent): the ply loop runs on the host, every legal-move list
+  comes from the GPU in the reference's frontier order and the agent draws from its
+  own stream -- bit-identical to the reference for RandomAgent.
+* ``rollout_backend="kernel"`` (default without a rollout_agent): the whole playout
+  runs inside the persistent HIP rollout kernel (bk_rollout, BK_SEM_ROLLOUT, Philox
+  stream, naive move order): statistically the same random playout, not the same
+  random numbers.  The reference's default HeuristicAgent rollout policy is not
+  ported; without a rollout_agent this agent uses uniform random
+  rollouts.
+The learned-evaluator options of the reference are out of scope and rejected.
+"""
+from __future__ import annotations
+
+import time
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from ..engine.board import Board, Player, Position, _PLAYERS, pack_state
+from ..engine.move_generator import Move, get_shared_generator
+from ..engine.pieces import PieceGenerator
+from .zobrist import TranspositionTable, ZobristHash
+
+
+def _positions(move: Move) -> List[Position]:
+    shape = get_shared_generator().piece_orientations_cache[move.piece_id][move.orientation]
+    return [Position(move.anchor_row + int(r), move.anchor_col + int(c)) for r, c in zip(*np.nonzero(shape))]
+
+
+class MCTSNode:
+    def __init__(self, board: Board, player: Player, move: Optional[Move] = None,
+                 parent: Optional["MCTSNode"] = None):
+        self.board = board.copy()
+        self.player = player
+        self.move = move
+        self.parent = parent
+        self.children: List["MCTSNode"] = []
+        self.visits = 0
+        self.total_reward = 0.0
+        self.prior_bias = 0.0
+        self.untried_moves: List[Move] = get_shared_generator().get_legal_moves(self.board, self.player)
+
+    def is_fully_expanded(self) -> bool:
+        return not self.untried_moves
+
+    def is_terminal(self) -> bool:
+        return not self.untried_moves and not self.children
+
+    def ucb1_value(self, exploration_constant: float = 1.414, progressive_bias_weight: float = 0.0) -> float:
+        if self.visits == 0:
+            return float("inf")
+        exploit = self.total_reward / self.visits
+        explore = exploration_constant * np.sqrt(np.log(self.parent.visits) / self.visits)
+        return exploit + explore + progressive_bias_weight * (self.prior_bias / (1.0 + self.visits))
+
+    def select_child(self, exploration_constant: float = 1.414, progressive_bias_weight: float = 0.0) -> "MCTSNode":
+        return max(self.children, key=lambda ch: ch.ucb1_value(exploration_constant, progressive_bias_weight))
+
+    def expand(self) -> Optional["MCTSNode"]:
+        if not self.untried_moves:
+            return None
+        move = self.untried_moves.pop()
+        nb = self.board.copy()
+        if not nb.place_piece(_positions(move), self.player, move.piece_id, validate=False):
+            return None
+        child = MCTSNode(nb, _PLAYERS[(_PLAYERS.index(self.player) + 1) % 4], move, self)
+        self.children.append(child)
+        return child
+
+    def update(self, reward: float):
+        self.visits += 1
+        self.total_reward += reward
+
+    def get_best_move(self) -> Optional[Move]:
+        return max(self.children, key=lambda ch: ch.visits).move if self.children else None
+
+
+class MCTSAgent:
+    def __init__(self, iterations: int = 1000, time_limit: Optional[float] = None,
+                 exploration_constant: float = 1.414, rollout_agent=None, use_transposition_table: bool = True,
+                 seed: Optional[int] = None, learned_model_path: Optional[str] = None,
+                 leaf_evaluation_enabled: bool = False, progressive_bias_enabled: bool = False,
+                 progressive_bias_weight: float = 0.25, potential_shaping_enabled: bool = False,
+                 potential_shaping_gamma: float = 1.0, potential_shaping_weight: float = 1.0,
+                 potential_mode: str = "prob", max_rollout_moves: int = 50,
+                 rollout_backend: Optional[str] = None, device: int = 0):
+        if potential_mode not in {"prob", "logit"}:
+            raise ValueError("potential_mode must be either 'prob' or 'logit'.")
+        if int(max_rollout_moves) <= 0:
+            raise ValueError("max_rollout_moves must be > 0.")
+        if leaf_evaluation_enabled or progressive_bias_enabled or potential_shaping_enabled or learned_model_path:
+            raise ValueError("learned evaluation is not supported by the GPU MCTS (out of scope)")
+        self.iterations = iterations
+        self.time_limit = time_limit
+        self.exploration_constant = exploration_constant
+        self.use_transposition_table = use_transposition_table
+        self.max_rollout_moves = int(max_rollout_moves)
+        self.progressive_bias_enabled = False
+        self.progressive_bias_weight = float(progressive_bias_weight)
+        self.move_generator = get_shared_generator()
+        self.piece_generator = PieceGenerator()
+        self.zobrist_hash = ZobristHash(seed=seed)
+        self.rollout_agent = rollout_agent
+        self.rollout_backend = rollout_backend or ("exact" if rollout_agent is not None else "kernel")
+        if self.rollout_backend not in ("exact", "kernel"):
+            raise ValueError("rollout_backend must be 'exact' or 'kernel'")
+        if self.rollout_backend == "exact" and rollout_agent is None:
+            raise ValueError("rollout_backend='exact' needs a rollout_agent")
+        self.seed = 0 if seed is None else int(seed)
+        self._kernel_calls = 0
+        self.device = device
+        self._gpu = None
+        self.transposition_table = TranspositionTable() if use_transposition_table else None
+        self.stats = self._fresh_stats()
+
+    @staticmethod
+    def _fresh_stats():
+        return {"iterations_run": 0, "time_elapsed": 0.0, "transposition_hits": 0, "rollout_rewards": [],
+                "leaf_eval_calls": 0, "progressive_bias_updates": 0, "potential_shaping_terms": [],
+                "evaluator_errors": 0}
+
+    def select_action(self, board: Board, player: Player, legal_moves: List[Move]) -> Optional[Move]:
+        if not legal_moves:
+            return None
+        if len(legal_moves) == 1:
+            return legal_moves[0]
+        t0 = time.time()
+        root = MCTSNode(board, player)
+        if self.time_limit:
+            i = 0
+            while time.time() - t0 < self.time_limit:
+                self._mcts_iteration(root)
+                i += 1
+            self.stats["iterations_run"] = i
+        else:
+            for i in range(self.iterations):
+                self._mcts_iteration(root)
+                self.stats["iterations_run"] = i + 1
+        self.stats["time_elapsed"] = time.time() - t0
+        best = root.get_best_move()
+        if self.transposition_table and len(self.transposition_table.table) > 500000:
+            self.transposition_table.clear()
+        return best
+
+    def _mcts_iteration(self, root: MCTSNode):
+        node = self._selection(root)
+        if not node.is_fully_expanded() and not node.is_terminal():
+            node = node.expand()
+            if node is None:
+                return
+        self._backpropagation(node, self._simulation(node))
+
+    def _selection(self, node: MCTSNode) -> MCTSNode:
+        while not node.is_terminal():
+            if not node.is_fully_expanded():
+                return node
+            node = node.select_child(self.exploration_constant, 0.0)
+        return node
+
+    def _simulation(self, node: MCTSNode) -> float:
+        if self.transposition_table:
+            h = self.zobrist_hash.hash_board(node.board)
+            hit = self.transposition_table.get(h)
+            if hit:
+                self.stats["transposition_hits"] += 1
+                return hit["reward"]
+        reward = self._rollout(node.board, node.player)
+        if self.transposition_table:
+            self.transposition_table.put(h, {"reward": reward})
+        self.stats["rollout_rewards"].append(reward)
+        return reward
+
+    def _rollout(self, board: Board, player: Player) -> float:
+        if self.rollout_backend == "kernel":
+            return self._rollout_kernel(board, player)
+        sim = board.copy()
+        cur = player
+        start = sim.get_score(player)
+        for _ in range(self.max_rollout_moves):
+            legal = self.move_generator.get_legal_moves(sim, cur)
+            if not legal:
+                break
+            mv = self.rollout_agent.select_action(sim, cur, legal)
+            if mv is None or not sim.place_piece(_positions(mv), cur, mv.piece_id, validate=False):
+                break
+            cur = _PLAYERS[(_PLAYERS.index(cur) + 1) % 4]
+        reward = sim.get_score(player) - start
+        if sim.is_game_over():  # never set inside a rollout (reference dead code kept for parity)
+            w = sim.get_winner()
+            reward += 100 if w == player else 10 if w is None else 0
+        return reward
+
+    def _rollout_kernel(self, board: Board, player: Player) -> float:
+        from .. import _native as N
+        from ..gpu import BlokusGPU
+        if self._gpu is None:
+            self._gpu = BlokusGPU(self.device)
+        st = pack_state(board)
+        st["current_player"] = player.value - 1
+        self._kernel_calls += 1
+        res = self._gpu.rollout(st, 1, semantics=N.SEM_ROLLOUT, rng=N.RNG_PHILOX,
+                                seed=(self.seed << 20) + self._kernel_calls, max_plies=self.max_rollout_moves)
+        return float(res["reward"][0])
+
+    def _backpropagation(self, node: MCTSNode, reward: float):
+        while node is not None:
+            node.update(reward)
+            node = node.parent
+
+    def get_action_info(self) -> Dict[str, Any]:
+        info = {"name": "MCTSAgent", "type": "mcts", "description": "UCT MCTS with GPU random rollouts",
+                "parameters": {"iterations": self.iterations, "time_limit": self.time_limit,
+                               "exploration_constant": self.exploration_constant,
+                               "use_transposition_table": self.use_transposition_table,
+                               "max_rollout_moves": self.max_rollout_moves,
+                               "rollout_backend": self.rollout_backend},
+                "stats": self.stats.copy()}
+        if self.transposition_table:
+            info["transposition_stats"] = self.transposition_table.get_stats()
+        return info
+
+    def reset(self):
+        self.stats = self._fresh_stats()
+        if self.transposition_table:
+            self.transposition_table.clear()
+
+    def set_seed(self, seed: int):
+        self.zobrist_hash = ZobristHash(seed=seed)
+        self.seed = int(seed)
+        if self.rollout_agent is not None:
+            self.rollout_agent.set_seed(seed)

@@ -1,0 +1,85 @@
+"""Zobrist hashing + transposition table (reference: mcts/zobrist.py:12-220).
+
+Keys are numpy RandomState(seed).randint(0, 2**64, dtype=uint64) draws in the
+reference's order (cell x value, then turn, then player x piece), so hashes are
+bit-identical to the reference's for the same seed (pinned by tests/golden/zobrist.json).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+
+from ..engine.board import Board, Player
+
+
+class ZobristHash:
+    def __init__(self, board_size: int = 20, num_players: int = 4, seed: Optional[int] = None):
+        self.board_size = board_size
+        self.num_players = num_players
+        self.rng = np.random.RandomState(seed)
+        self._generate_hash_values()
+
+    def _generate_hash_values(self):
+        n, k = self.board_size, self.num_players
+        draw = lambda: self.rng.randint(0, 2**64, dtype=np.uint64)  # noqa: E731
+        self.position_player_hashes = np.zeros((n, n, k + 1), dtype=np.uint64)
+        for r in range(n):
+            for c in range(n):
+                for v in range(k + 1):
+                    self.position_player_hashes[r, c, v] = draw()
+        self.player_turn_hashes = np.array([draw() for _ in range(k)], dtype=np.uint64)
+        self.piece_used_hashes = np.array([[draw() for _ in range(21)] for _ in range(k)], dtype=np.uint64)
+        # flat view used for vectorised hashing: index cell * (k+1) + value
+        self._flat = self.position_player_hashes.reshape(-1)
+
+    def hash_board(self, board: Board) -> int:
+        idx = np.arange(self.board_size * self.board_size) * (self.num_players + 1) + board.grid.reshape(-1)
+        h = np.bitwise_xor.reduce(self._flat[idx])
+        h ^= self.player_turn_hashes[board.current_player.value - 1]
+        for p in Player:
+            for pid in board.player_pieces_used[p]:
+                h ^= self.piece_used_hashes[p.value - 1, pid - 1]
+        return np.uint64(h)
+
+    def hash_move(self, board: Board, move_hash: int, player: Player, piece_id: int) -> int:
+        i = board.current_player.value - 1
+        h = np.uint64(move_hash) ^ self.player_turn_hashes[i] ^ self.player_turn_hashes[(i + 1) % self.num_players]
+        return h ^ self.piece_used_hashes[player.value - 1, piece_id - 1]
+
+    def hash_position_placement(self, row: int, col: int, player: Player) -> int:
+        return self.position_player_hashes[row, col, player.value]
+
+    def get_hash_info(self):
+        return {"board_size": self.board_size, "num_players": self.num_players, "hash_bits": 64,
+                "total_positions": self.board_size * self.board_size, "total_pieces": 21}
+
+
+class TranspositionTable:
+    def __init__(self, max_size: int = 1000000):
+        self.max_size = max_size
+        self.table: Dict[int, Dict] = {}
+        self.access_count = 0
+        self.hit_count = 0
+
+    def get(self, hash_value: int) -> Optional[Dict]:
+        self.access_count += 1
+        e = self.table.get(hash_value)
+        if e is not None:
+            self.hit_count += 1
+        return e
+
+    def put(self, hash_value: int, entry: Dict):
+        if len(self.table) >= self.max_size:
+            for key in list(self.table.keys())[: self.max_size // 10]:
+                del self.table[key]
+        self.table[hash_value] = entry
+
+    def clear(self):
+        self.table.clear()
+        self.access_count = 0
+        self.hit_count = 0
+
+    def get_stats(self) -> Dict[str, float]:
+        return {"size": len(self.table), "max_size": self.max_size, "access_count": self.access_count,
+                "hit_count": self.hit_count, "hit_rate": self.hit_count / max(self.access_count, 1)}

@@ -48,3 +48,29 @@ def rows_to_moves(rows):
                 out.append(g * 400 + r * 20 + c)
                 w &= w - 1
     return out
+
+
+def engine_board(rec):
+    """The same position as a host-mirror engine.Board (place_piece in log order, so its
+    frontier sets go through the reference's exact add/discard sequence)."""
+    from reinforcementlearning_blokus_amd.engine.board import Board, Player, Position
+    b = Board()
+    for player_value, piece_id, cells in rec["log"]:
+        b.current_player = Player(player_value)
+        b.place_piece([Position(r, c) for r, c in cells], Player(player_value), piece_id, validate=False)
+    b.current_player = Player(rec["state"]["current_player"])
+    return b
+
+
+def sha_ints(ints):
+    import hashlib
+    return hashlib.sha256(",".join(str(i) for i in ints).encode()).hexdigest()
+
+
+def ints_to_rows(ints):
+    """naive-order move ints -> dense uint32[91,20] mask (bit c = column c)."""
+    rows = np.zeros((91, 20), dtype=np.uint32)
+    for a in ints:
+        g, rest = divmod(int(a), 400)
+        rows[g, rest // 20] |= np.uint32(1 << (rest % 20))
+    return rows
