@@ -26,7 +26,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MCTS random-rollout simulations/sec (20x20, 4p) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# VALU int32 peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (one 32-bit op per lane-cycle)
+# VALU int32 peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.  Measured (tools/valu_probe2.hip):
+# v_or/v_xor/v_lshrrev/v_add/v_bitop3 issue in ~2.5 cycles per wave64 with >= 2 waves per
+# SIMD (32 lanes/clk); v_lshl_or/v_lshlrev/v_bcnt/v_or3 take ~4.3-4.6 (half rate)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
@@ -146,17 +148,18 @@ def main():
         # SURVEY 8(d) algorithmic bytes: 256 B state read + 256 B write per ply, 32 B result
         bytes_per_sim = 512.0 * plies_per_sim + 32.0
         achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = valu_insts = None
         tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
         if os.path.exists(tpath):
             try:
-                traffic = json.load(open(tpath)).get("bytes_per_launch")
-            except Exception:
-                traffic = None
-        # VALU view: measured int ops per movegen x movegens per launch
-        ops_per_movegen = 20_000.0
-        movegens = n * (plies_per_sim + 4)
-        valu_tops = movegens * ops_per_movegen / (avg_ms * 1e-3) / 1e12
+                tj = json.load(open(tpath))
+                traffic, valu_insts = tj.get("bytes_per_launch"), tj.get("valu_insts_per_launch")
+            except (OSError, ValueError):
+                traffic = valu_insts = None
+        # VALU view (the real limiter): wave64 VALU instructions per launch
+        # from the committed PMC pass (SQ_INSTS_VALU, same workload) x 64 lanes over the
+        # live launch time, against the dual-issue int32 VALU peak of 32 lanes/clk/SIMD
+        valu_tops = valu_insts * 64 / (avg_ms * 1e-3) / 1e12 if valu_insts else None
         line = {
             "metric": METRIC,
             "value": value,
@@ -178,8 +181,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_rollout", "kernel_ms": avg_ms, "plies_per_sim": plies_per_sim},
             "compute_roofline": {"bound": "valu_int32", "achieved": valu_tops, "peak": VALU_PEAK_TOPS,
-                                 "unit": "Tops/s", "frac": valu_tops / VALU_PEAK_TOPS,
-                                 "ops_per_movegen": ops_per_movegen},
+                                 "unit": "Tlane-op/s", "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
+                                 "valu_insts_per_launch": valu_insts},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(roots_np, args.cpu_seconds)

@@ -13,7 +13,8 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libblokus_hip.so")
+# BK_LIB_PATH: load an alternative in-tree build (kernel tuning experiments)
+LIB_PATH = os.environ.get("BK_LIB_PATH") or os.path.join(_HERE, "_lib", "libblokus_hip.so")
 
 OK, EINVAL, EHIP, ENOMEM, EOVERFLOW = 0, -1, -2, -3, -4
 MEM_HOST, MEM_DEVICE = 0, 1

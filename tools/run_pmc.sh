@@ -1,6 +1,7 @@
 #!/bin/bash
-# PMC passes over tools/prof_target.py (GPU box only).  Each pass is a separate
-# rocprofv3 run with --kernel-trace only (no sys/runtime trace alongside --pmc).
+# PMC passes over a short bench.py run (GPU box only).  Each pass is its own rocprofv3
+# run with --kernel-trace only (no sys/runtime trace alongside --pmc).  Counter sets
+# are read one per line from stdin.  Usage: bash tools/run_pmc.sh <tag> < sets.txt
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-pmc}
 mkdir -p $OUT
 cd /tmp
@@ -9,14 +10,8 @@ i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters -d $OUT/p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/prof_target.py > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters -d $OUT/pmc$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc$i.log 2>&1
   rc=$?
   echo "pass $i ($counters) rc=$rc"
-  if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
-done <<LIST
-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
-SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_INSTS_BRANCH
-GRBM_GUI_ACTIVE GRBM_COUNT
-FETCH_SIZE
-WRITE_SIZE
-LIST
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
