@@ -1,0 +1,38 @@
+"""Game sharding across ranks (one process per GPU) and the result gather.
+
+Games are independent and every per-game seed is a pure function of (run seed, game
+index) (analytics/tournament/arena_runner.py:241-254), so rank r of W plays the games
+with index == r (mod W) and the only collective is one gather of fixed-size 32-byte
+bk_result records at the end.  On GPUs the process group is RCCL
+(backend "nccl"); the same code runs on gloo over CPU tensors in the tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+RESULT_BYTES = 32
+
+
+def shard_indices(n_total: int, rank: int, world: int) -> np.ndarray:
+    """Global game indices owned by `rank`: rank, rank + W, rank + 2W, ..."""
+    if not 0 <= rank < world:
+        raise ValueError("rank out of range")
+    return np.arange(rank, n_total, world, dtype=np.int64)
+
+
+def gather_results(local, n_total: int, rank: int, world: int, dist, device=None):
+    """All-gather every rank's result records (uint8 [n_local, 32], torch tensor) and
+    return them in global game order as a torch uint8 tensor [n_total, 32] on `device`.
+    Ranks own index == rank (mod W), so shard sizes differ by at most one: pad to the
+    largest, gather, then interleave."""
+    import torch
+    per = (n_total + world - 1) // world
+    buf = torch.zeros((per, RESULT_BYTES), dtype=torch.uint8, device=local.device)
+    buf[: local.shape[0]] = local
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out = torch.empty((n_total, RESULT_BYTES), dtype=torch.uint8, device=device or local.device)
+    for r in range(world):
+        idx = shard_indices(n_total, r, world)
+        out[torch.from_numpy(idx).to(out.device)] = parts[r][: len(idx)].to(out.device)
+    return out

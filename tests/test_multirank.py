@@ -1,0 +1,70 @@
+"""N>1 path on CPU: world_size-2 gloo ranks shard games and gather results.
+
+Each rank plays its shard (game index == rank mod 2) of a fixed set of arena playouts
+with the oracle standing in for the device (test infrastructure only), gathers the
+32-byte result records with shard.gather_results, and rank 0 checks them against one
+process playing every game: the sharded run is bit-identical to the single run.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from reinforcementlearning_blokus_amd.shard import gather_results, shard_indices
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _play(indices):
+    """Arena playouts of games `indices`: root = position (i mod 8), agent seeds from i."""
+    from oracle import pyoracle as O
+    from tests.helpers import POS, replay
+    recs = []
+    for i in indices:
+        b = replay(POS[8 + int(i) % 8])
+        res, _ = O.playout_arena(b, [int(i) * 4 + k for k in range(4)], O.ORDER_NAIVE)
+        recs.append(np.frombuffer(bytes(res), dtype=np.uint8))
+    return np.stack(recs) if recs else np.zeros((0, 32), np.uint8)
+
+
+def _worker(rank, world, port, n_total, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = _play(shard_indices(n_total, rank, world))
+        allres = gather_results(torch.from_numpy(mine), n_total, rank, world, dist)
+        if rank == 0:
+            q.put(allres.numpy().copy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total", [7, 8])
+def test_gloo_two_ranks_shard_and_gather(n_total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _play(range(n_total))
+    assert np.array_equal(got, ref)
+
+
+def test_shard_indices_partition():
+    for n in (0, 1, 5, 64, 1001):
+        for w in (1, 2, 3, 8):
+            allidx = np.sort(np.concatenate([shard_indices(n, r, w) for r in range(w)]))
+            assert np.array_equal(allidx, np.arange(n))
