@@ -191,6 +191,11 @@ struct StencilClass {
 // LDS count slots: two u16 per dword, [g/2][lane]
 __device__ __forceinline__ uint32_t cnt_off(int g, int lane) { return (uint32_t)(((g >> 1) * WAVE + lane) * 2 + (g & 1)); }
 #define CNT_WORDS_PER_WAVE (((BK_NUM_ORIENTS + 1) / 2) * WAVE)
+// rollout kernel: per-wave LDS area of 48 dwords per lane.  The per-orientation counts
+// ([g/2][lane] u16 pairs, 46 dwords) are dead once the move's orientation is picked;
+// the same bytes then hold the mover's B/C rows 0..23 as [row][lane]{B, C} pairs for
+// locate_move_lds (rows 20..23: off-board, B = ~0, C = 0).
+#define ROLL_WORDS_PER_WAVE (48 * WAVE)
 
 // Per-orientation legal-move counts of one board-player for the class's table entries
 // [i0, i1) (cnt[...] u16, indexed by global orientation id g); returns their sum.
@@ -318,6 +323,49 @@ __device__ __forceinline__ void locate_move(int gs, uint32_t kk, const uint32_t 
             if (rem < pc) {
                 // rem-th set bit from the bottom (column ascending)
                 uint32_t x = ok;
+                for (uint32_t j = 0; j < rem; ++j) x &= x - 1u;
+                found_r = r;
+                found_c = __builtin_ctz(x);
+            } else {
+                rem -= pc;
+            }
+        }
+    }
+    out_r = found_r;
+    out_c = found_c;
+}
+
+// locate_move with the mover's B/C rows in LDS (rows[R * WAVE] = {B[R], C[R]}): the
+// per-lane cell rows become per-lane LDS addresses instead of 5-way register selects.
+// Cells beyond the orientation's count repeat cell 0 (ORing a term twice is harmless);
+// anchor rows the piece cannot use reach the off-board rows 20..23 (B = ~0) and drop out.
+__device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2* rows, int& out_r, int& out_c) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    const uint2* base[5];
+    uint32_t sh[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        base[k] = rows + (cell >> 8) * WAVE;
+        sh[k] = cell & 0xFFu;
+    }
+    int found_r = -1, found_c = 0;
+    uint32_t rem = kk;
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        uint2 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = base[k][r * WAVE];
+        uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
+        uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
+        ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
+        ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
+        const uint32_t ok = ac & ~ab;
+        const uint32_t pc = __builtin_popcount(ok);
+        if (found_r < 0) {
+            if (rem < pc) {
+                uint32_t x = ok;  // rem-th set bit from the bottom (column ascending)
                 for (uint32_t j = 0; j < rem; ++j) x &= x - 1u;
                 found_r = r;
                 found_c = __builtin_ctz(x);
@@ -692,9 +740,10 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
 }
 
 __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
-    __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
+    __shared__ uint32_t lds[ROLL_WORDS_PER_WAVE * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
+    uint16_t* my = reinterpret_cast<uint16_t*>(lds + wv * ROLL_WORDS_PER_WAVE);
+    uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * ROLL_WORDS_PER_WAVE) + lane;  // + R * WAVE
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
@@ -763,8 +812,12 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         const uint32_t k = draw_index(a, g, slab, slot, total);
         uint32_t kk;
         const int gs = pick_orient(my, lane, k, kk);
+        // counts are consumed: the area now takes the mover's rows for locate
+#pragma unroll
+        for (int R = 0; R < 24; ++R)
+            rows_lds[R * WAVE] = R < 20 ? make_uint2(P.B[R], P.C[R]) : make_uint2(~0u, 0u);
         int ar, ac;
-        locate_move(gs, kk, P.B, P.C, ar, ac);
+        locate_move_lds(gs, kk, rows_lds, ar, ac);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
         const uint32_t info = kInfo[gs];
         const int n = (int)((info >> 8) & 0xFFu);
