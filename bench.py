@@ -30,6 +30,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # v_or/v_xor/v_lshrrev/v_add/v_bitop3 issue in ~2.5 cycles per wave64 with >= 2 waves per
 # SIMD (32 lanes/clk); v_lshl_or/v_lshlrev/v_bcnt/v_or3 take ~4.3-4.6 (half rate)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# Single-issue rate (one wave64 VALU op per 4 cycles per SIMD): what any stream holding
+# slow ops (v_bcnt, SGPR operands, left shifts ...) gets -- k_rollout's case
+VALU_SINGLE_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
 def parse():
@@ -182,6 +185,8 @@ def main():
                          "kernel": "k_rollout", "kernel_ms": avg_ms, "plies_per_sim": plies_per_sim},
             "compute_roofline": {"bound": "valu_int32", "achieved": valu_tops, "peak": VALU_PEAK_TOPS,
                                  "unit": "Tlane-op/s", "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
+                                 "peak_single_issue": VALU_SINGLE_TOPS,
+                                 "frac_single_issue": valu_tops / VALU_SINGLE_TOPS if valu_tops else None,
                                  "valu_insts_per_launch": valu_insts},
         }
         if not args.no_cpu_baseline and world == 1:

@@ -38,6 +38,7 @@
 
 #include <mutex>
 #include <new>
+#include <vector>
 
 #include "../../include/blokus_hip.h"
 #include "orient_table.h"
@@ -174,10 +175,16 @@ struct StencilClass {
     }
     template <typename F>
     __device__ __forceinline__ static void scan(const Planes& P, uint32_t w1, F&& f) {
+        // Shift amounts go to VGPRs: a VALU op reading an SGPR is never dual-issued on
+        // gfx950 (tools/valu_probe2.hip).  NOTE: the v_bcnt below keeps
+        // the whole stream at the single-issue rate anyway, so today this is neutral.
         uint32_t sh[5];
         sh[0] = 0;
 #pragma unroll
-        for (int k = 1; k < 5; ++k) sh[k] = (w1 >> (3 * (k - 1))) & 7u;
+        for (int k = 1; k < NT; ++k) {
+            const uint32_t v = (w1 >> (3 * (k - 1))) & 7u;
+            asm("v_mov_b32 %0, %1" : "=v"(sh[k]) : "s"(v));
+        }
         // row by row: without the barriers the scheduler interleaves all rows for ILP
         // and the live set no longer fits 3 waves per SIMD (other waves hide latency)
 #pragma unroll
@@ -188,21 +195,22 @@ struct StencilClass {
     }
 };
 
-// LDS count slots: two u16 per dword, [g/2][lane]
-__device__ __forceinline__ uint32_t cnt_off(int g, int lane) { return (uint32_t)(((g >> 1) * WAVE + lane) * 2 + (g & 1)); }
-#define CNT_WORDS_PER_WAVE (((BK_NUM_ORIENTS + 1) / 2) * WAVE)
-// rollout kernel: per-wave LDS area of 48 dwords per lane.  The per-orientation counts
-// ([g/2][lane] u16 pairs, 46 dwords) are dead once the move's orientation is picked;
-// the same bytes then hold the mover's B/C rows 0..23 as [row][lane]{B, C} pairs for
-// locate_move_lds (rows 20..23: off-board, B = ~0, C = 0).
-#define ROLL_WORDS_PER_WAVE (48 * WAVE)
+// Per-orientation counts in LDS, 10 bits each, three per dword: orientation g lives in
+// dword g / 3 at bit 10 * (g % 3), laid out [dword][lane] (31 dwords per lane).  The
+// rollout zeroes a lane's dwords before each movegen and ds_add_u32's every count in
+// (counts <= 400 < 1024, so fields never carry into each other).
+#define CNT_DWORDS ((BK_NUM_ORIENTS + 2) / 3)
+// rollout kernel: per-wave LDS area of 40 dwords per lane.  The counts (31 dwords) are
+// dead once the move's orientation is picked; the same bytes then hold the mover's
+// B/C rows 0..19 as [row][lane]{B, C} pairs for locate_move_lds.
+#define ROLL_WORDS_PER_WAVE (40 * WAVE)
 
-// Per-orientation legal-move counts of one board-player for the class's table entries
-// [i0, i1) (cnt[...] u16, indexed by global orientation id g); returns their sum.
+// Legal-move counts of one board-player for the class's table entries [i0, i1); with
+// STORE, also the per-orientation counts (cl = this lane's dword 0, stride WAVE).
 // Orientations whose piece no lane of the wave may still play are skipped with a
 // uniform branch.
-template <int H, int... T>
-__device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P, uint32_t avail, uint16_t* cl) {
+template <bool STORE, int H, int... T>
+__device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl) {
     uint32_t total = 0;
     uint32_t w0 = kClass[i0][0], w1 = kClass[i0][1];
 #pragma unroll 1
@@ -212,21 +220,26 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
         const uint32_t piece = w0 & 0xFFu;
         const int g = (int)(w0 >> 8);
         const bool av = (avail >> (piece - 1u)) & 1u;
-        uint32_t c = 0;
         if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
+            uint32_t c = 0;
             StencilClass<H, T...>::scan(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); });
             c = av ? c : 0u;
+            if constexpr (STORE) atomicAdd(cl + (g / 3) * WAVE, c << (10 * (g % 3)));
+            total += c;
         }
-        cl[(g >> 1) * (2 * WAVE) + (g & 1)] = (uint16_t)c;  // = cnt[cnt_off(g, lane)]
-        total += c;
         w0 = n0; w1 = n1;
     }
     return total;
 }
 
-__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint16_t* cnt, int lane) {
+template <bool STORE>
+__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane) {
     uint32_t t = 0;
-    uint16_t* cl = cnt + 2 * lane;  // this lane's slots; the orientation part is uniform
+    uint32_t* cl = cnt + lane;  // this lane's dwords; the orientation part is uniform
+    if constexpr (STORE) {
+#pragma unroll
+        for (int j = 0; j < CNT_DWORDS; ++j) cl[j * WAVE] = 0u;
+    }
     // opaque table offset (always 0): otherwise everything about the one-orientation
     // classes is hoisted out of the persistent loop and lives in (spilled) registers.
     // readfirstlane: an asm output counts as divergent, which would turn the table
@@ -234,7 +247,7 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     int tb0 = 0;
     asm volatile("" : "+s"(tb0));
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl);
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl);
     BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     return t;
@@ -262,25 +275,24 @@ __device__ __forceinline__ void all_rows(const Planes& P, F&& f) {
 }
 
 // orientation holding the k-th legal move (naive order: g ascending) and its rank in it
-__device__ __forceinline__ int pick_orient(const uint16_t* cnt, int lane, uint32_t k, uint32_t& kk) {
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(cnt);
-    constexpr int NW = (BK_NUM_ORIENTS + 1) / 2;
+__device__ __forceinline__ int pick_orient(const uint32_t* cnt, int lane, uint32_t k, uint32_t& kk) {
     uint32_t run = 0;
     int gs = BK_NUM_ORIENTS - 1;
     uint32_t before = 0;
     bool found = false;
 #pragma unroll 1
-    for (int h0 = 0; h0 < NW; h0 += 8) {  // 8 LDS reads in flight per batch
+    for (int h0 = 0; h0 < CNT_DWORDS; h0 += 8) {  // 8 LDS reads in flight per batch
         uint32_t v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (h0 + j < NW) ? c32[(h0 + j) * WAVE + lane] : 0u;
+        for (int j = 0; j < 8; ++j) v[j] = (h0 + j < CNT_DWORDS) ? cnt[(h0 + j) * WAVE + lane] : 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const uint32_t lo = v[j] & 0xFFFFu, hi = v[j] >> 16;
-            if (!found && k < run + lo) { gs = 2 * (h0 + j); before = run; found = true; }
-            run += lo;
-            if (!found && k < run + hi) { gs = 2 * (h0 + j) + 1; before = run; found = true; }
-            run += hi;
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+                const uint32_t c = (v[j] >> (10 * f)) & 0x3FFu;
+                if (!found && k < run + c) { gs = 3 * (h0 + j) + f; before = run; found = true; }
+                run += c;
+            }
         }
     }
     kk = k - before;
@@ -335,13 +347,15 @@ __device__ __forceinline__ void locate_move(int gs, uint32_t kk, const uint32_t 
     out_c = found_c;
 }
 
-// locate_move with the mover's B/C rows in LDS (rows[R * WAVE] = {B[R], C[R]}): the
-// per-lane cell rows become per-lane LDS addresses instead of 5-way register selects.
-// Cells beyond the orientation's count repeat cell 0 (ORing a term twice is harmless);
-// anchor rows the piece cannot use reach the off-board rows 20..23 (B = ~0) and drop out.
+// locate_move with the mover's B/C rows in LDS (rows[R * WAVE] = {B[R], C[R]}, R < 20):
+// the per-lane cell rows become per-lane LDS addresses instead of 5-way register
+// selects.  Cells beyond the orientation's count repeat cell 0 (ORing a term twice is
+// harmless).  Anchor rows past 20 - height cannot hold the piece: they are evaluated
+// at the last valid row (so every read stays in rows 0..19) and then dropped.
 __device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2* rows, int& out_r, int& out_c) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
+    const int rlim = 20 - (int)((info >> 16) & 0xFFu);
     const uint2* base[5];
     uint32_t sh[5];
 #pragma unroll
@@ -354,14 +368,15 @@ __device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2
     uint32_t rem = kk;
 #pragma unroll
     for (int r = 0; r < 20; ++r) {
+        const int rr = r < rlim ? r : rlim;
         uint2 v[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) v[k] = base[k][r * WAVE];
+        for (int k = 0; k < 5; ++k) v[k] = base[k][rr * WAVE];
         uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
         uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
         ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
         ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
-        const uint32_t ok = ac & ~ab;
+        const uint32_t ok = r <= rlim ? (ac & ~ab) : 0u;
         const uint32_t pc = __builtin_popcount(ok);
         if (found_r < 0) {
             if (rem < pc) {
@@ -459,9 +474,7 @@ __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&ow
 }
 
 __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
-    __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
-    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
+    const int lane = threadIdx.x & (WAVE - 1);
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < a.n;
     const int idx = live ? i : 0;
@@ -483,7 +496,7 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
     make_pairs(P);
     const uint32_t avail = live ? (~s->used[p] & 0x1FFFFFu) : 0u;
     if (a.out_rows == nullptr) {
-        const uint32_t total = movegen_counts(P, avail, my, lane);
+        const uint32_t total = movegen_counts<false>(P, avail, nullptr, lane);
         if (live && a.out_count) a.out_count[i] = total;
         return;
     }
@@ -508,9 +521,7 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
 }
 
 __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
-    __shared__ uint16_t cnt[CNT_WORDS_PER_WAVE * 2 * (BLOCK / WAVE)];
-    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = cnt + wv * CNT_WORDS_PER_WAVE * 2;
+    const int lane = threadIdx.x & (WAVE - 1);
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < a.n;
     const bk_state* s = a.states + (live ? i : 0);
@@ -531,7 +542,7 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
         }
         derive_rows(ow, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
         make_pairs(P);
-        const uint32_t total = movegen_counts(P, live ? (~s->used[p] & 0x1FFFFFu) : 0u, my, lane);
+        const uint32_t total = movegen_counts<false>(P, live ? (~s->used[p] & 0x1FFFFFu) : 0u, nullptr, lane);
         mask |= (uint8_t)((total > 0) << p);
     }
     if (live) a.out_mask4[i] = mask;
@@ -742,7 +753,7 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
 __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     __shared__ uint32_t lds[ROLL_WORDS_PER_WAVE * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint16_t* my = reinterpret_cast<uint16_t*>(lds + wv * ROLL_WORDS_PER_WAVE);
+    uint32_t* my = lds + wv * ROLL_WORDS_PER_WAVE;
     uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * ROLL_WORDS_PER_WAVE) + lane;  // + R * WAVE
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
@@ -797,7 +808,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         }
         make_pairs(P);
         const uint32_t avail = idle ? 0u : (~g.used.get(p) & 0x1FFFFFu);
-        const uint32_t total = movegen_counts(P, avail, my, lane);
+        const uint32_t total = movegen_counts<true>(P, avail, my, lane);
         if (idle) continue;
         if (total == 0u) {
             if (arena) {
@@ -814,8 +825,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         const int gs = pick_orient(my, lane, k, kk);
         // counts are consumed: the area now takes the mover's rows for locate
 #pragma unroll
-        for (int R = 0; R < 24; ++R)
-            rows_lds[R * WAVE] = R < 20 ? make_uint2(P.B[R], P.C[R]) : make_uint2(~0u, 0u);
+        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
         int ar, ac;
         locate_move_lds(gs, kk, rows_lds, ar, ac);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score

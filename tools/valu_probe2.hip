@@ -258,6 +258,54 @@ DEP_KERNEL(k_dep_bitop3, "v_bitop3_b32 %0, %1, %2, %0 bitop3:0xfe")
 DEP_KERNEL(k_dep_lshl_or, "v_lshl_or_b32 %0, %1, 3, %0")
 DEP_KERNEL(k_dep_bcnt, "v_bcnt_u32_b32 %0, %1, %0")
 
+// realistic stencil mixes (8 statements per iteration)
+__global__ __launch_bounds__(1024) void k_mix_lshr_s(uint32_t* out, uint32_t seed) {
+    uint32_t a0 = seed ^ threadIdx.x, a1 = a0 * 3u, a2 = a0 * 5u, a3 = a0 * 7u, a4 = a0 * 11u, a5 = a0 * 13u, a6 = a0 * 17u, a7 = a0 * 19u;
+    const uint32_t sh = seed & 7u;
+    for (int i = 0; i < N_ITERS; ++i) {
+        asm volatile("v_lshrrev_b32 %0, %8, %1\nv_lshrrev_b32 %1, %8, %2\nv_lshrrev_b32 %2, %8, %3\nv_lshrrev_b32 %3, %8, %4\n"
+                     "v_lshrrev_b32 %4, %8, %5\nv_lshrrev_b32 %5, %8, %6\nv_lshrrev_b32 %6, %8, %7\nv_lshrrev_b32 %7, %8, %0"
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(sh));
+    }
+    uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+    if (r == 0x12345678u) out[blockIdx.x] = r;
+}
+// 3 lshrrev(s) + 2 bitop3 + 1 bcnt + 2 lshrrev  (8 ops, one slow)
+__global__ __launch_bounds__(1024) void k_mix_sten(uint32_t* out, uint32_t seed) {
+    uint32_t a0 = seed ^ threadIdx.x, a1 = a0 * 3u, a2 = a0 * 5u, a3 = a0 * 7u, a4 = a0 * 11u, a5 = a0 * 13u, a6 = a0 * 17u, a7 = a0 * 19u;
+    const uint32_t sh = seed & 7u;
+    for (int i = 0; i < N_ITERS; ++i) {
+        asm volatile("v_lshrrev_b32 %0, %8, %1\nv_lshrrev_b32 %1, %8, %2\nv_bitop3_b32 %2, %3, %0, %1 bitop3:0xfe\nv_lshrrev_b32 %3, %8, %4\n"
+                     "v_lshrrev_b32 %4, %8, %5\nv_bitop3_b32 %5, %6, %3, %4 bitop3:0x54\nv_bcnt_u32_b32 %6, %5, %6\nv_lshrrev_b32 %7, %8, %0"
+                     : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7) : "s"(sh));
+    }
+    uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;
+    if (r == 0x12345678u) out[blockIdx.x] = r;
+}
+
+#define MIX_KERNEL(NAME, BODY, CONS)                                                               \
+__global__ __launch_bounds__(1024) void NAME(uint32_t* out, uint32_t seed) {                     \
+    uint32_t a0 = seed ^ threadIdx.x, a1 = a0 * 3u, a2 = a0 * 5u, a3 = a0 * 7u, a4 = a0 * 11u,   \
+             a5 = a0 * 13u, a6 = a0 * 17u, a7 = a0 * 19u;                                         \
+    uint32_t sh = seed & 7u;                                                                      \
+    uint32_t vsh = __builtin_amdgcn_readfirstlane(sh) + (threadIdx.x >> 10);                      \
+    for (int i = 0; i < N_ITERS; ++i) {                                                            \
+        asm volatile(BODY : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), \
+                     "+v"(a7) : CONS);                                                             \
+    }                                                                                              \
+    uint32_t r = a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7;                                            \
+    if (r == 0x12345678u) out[blockIdx.x] = r;                                                     \
+}
+#define R8(I) I(0,1) I(1,2) I(2,3) I(3,4) I(4,5) I(5,6) I(6,7) I(7,0)
+#define LSHR_V(d, a) "v_lshrrev_b32 %" #d ", %8, %" #a "\n"
+#define OR_S(d, a) "v_or_b32 %" #d ", %8, %" #a "\n"
+#define BITOP3_S(d, a) "v_bitop3_b32 %" #d ", %" #a ", %8, %" #d " bitop3:0xfe\n"
+#define ALIGN_V(d, a) "v_alignbit_b32 %" #d ", %" #a ", %" #d ", %8\n"
+MIX_KERNEL(k_lshr_v, R8(LSHR_V), "v"(vsh))
+MIX_KERNEL(k_or_s, R8(OR_S), "s"(sh))
+MIX_KERNEL(k_bitop3_s, R8(BITOP3_S), "s"(sh))
+MIX_KERNEL(k_lshr_inl, "v_lshrrev_b32 %0, 3, %1\nv_lshrrev_b32 %1, 3, %2\nv_lshrrev_b32 %2, 3, %3\nv_lshrrev_b32 %3, 3, %4\nv_lshrrev_b32 %4, 3, %5\nv_lshrrev_b32 %5, 3, %6\nv_lshrrev_b32 %6, 3, %7\nv_lshrrev_b32 %7, 3, %0", "v"(vsh))
+
 typedef void (*kfn)(uint32_t*, uint32_t);
 static void run(const char* name, kfn f, uint32_t* d, int num_cu) {
     hipEvent_t e0, e1;
@@ -315,5 +363,11 @@ int main() {
     run("dep v_bitop3", k_dep_bitop3, d, p.multiProcessorCount);
     run("dep v_lshl_or", k_dep_lshl_or, d, p.multiProcessorCount);
     run("dep v_bcnt", k_dep_bcnt, d, p.multiProcessorCount);
+    run("lshrrev(s)", k_mix_lshr_s, d, p.multiProcessorCount);
+    run("stencil mix 7f+1s", k_mix_sten, d, p.multiProcessorCount);
+    run("lshrrev(v)", k_lshr_v, d, p.multiProcessorCount);
+    run("lshrrev(inline)", k_lshr_inl, d, p.multiProcessorCount);
+    run("or(s)", k_or_s, d, p.multiProcessorCount);
+    run("bitop3(s)", k_bitop3_s, d, p.multiProcessorCount);
     return 0;
 }
