@@ -163,6 +163,54 @@ int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_
                bk_state* out_states, int mem);
 
 /*
+ * Reference frontier ORDER on the GPU.
+ *
+ * The reference's default generator (engine/move_generator.py:261-559) lists a
+ * (piece, orientation)'s anchors in the order its frontier SET iterates: a CPython 3.10
+ * set of (row, col) tuples whose slot layout is fixed by the exact add/discard history
+ * of engine/board.py:315-367 (update_frontier_after_move) and set.copy() (Board.copy,
+ * engine/board.py:643-660).  bk_fset is that hash table, restated bit for bit
+ * (Objects/setobject.c: LINEAR_PROBES 9, PERTURB_SHIFT 5, resize to used*4 when
+ * fill*5 >= mask*3, copy re-inserts in slot order), one per player.  Iteration order =
+ * slot order of keys >= 0.
+ */
+#define BK_FSET_SLOTS 256
+typedef struct bk_fset {
+    int16_t key[BK_PLAYERS][BK_FSET_SLOTS]; /* cell r*20+c; -1 unused; -2 dummy      */
+    uint16_t mask[BK_PLAYERS];              /* table size - 1 (7 .. 255)               */
+    uint16_t fill[BK_PLAYERS];              /* active + dummy slots                    */
+    uint16_t used[BK_PLAYERS];              /* active slots                            */
+    uint16_t reserved[BK_PLAYERS];
+} bk_fset; /* 2080 bytes */
+
+/* Host-side table maintenance for host Boards (no GPU needed):
+   Board() (engine/board.py:54-78 init_frontiers): every player's set = {start corner} */
+int bk_fset_init(bk_fset* s);
+/* place_piece's frontier update for `player` (engine/board.py:315-367).  `after` is the
+   board AFTER the piece's cells were written (the reference writes the grid first);
+   cells in place_piece order (r*20+c). */
+int bk_fset_place(bk_fset* s, const bk_state* after, int32_t player, const int32_t* cells, int32_t n);
+/* set.copy() of every player's set (Board.copy, engine/board.py:643-660) */
+int bk_fset_copy(bk_fset* dst, const bk_fset* src);
+/* iteration order of player's set into out (cap entries); returns the count or < 0 */
+int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap);
+
+/*
+ * bk_rollout / bk_advance in the reference's FRONTIER order (cfg->order ==
+ * BK_ORDER_FRONTIER): root_sets[n_roots] carry the roots' frontier tables; with
+ * BK_RNG_NUMPY_MT the playouts are the reference's default-config games move for move.
+ * BK_SEM_ARENA / BK_SEM_ROLLOUT: out[n_playouts]; out_states and out_sets NULL.
+ * BK_SEM_ROLLOUT starts from set.copy() of the root tables, as MCTSAgent._rollout plays
+ * on sim = board.copy() (mcts/mcts_agent.py:470).
+ * BK_SEM_ADVANCE: out_states[n_playouts] and out_sets[n_playouts] (out may be NULL).
+ * A table that would outgrow BK_FSET_SLOTS stops its playout with status 2.
+ */
+int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_sets, int32_t n_roots,
+                        const int32_t* root_index, int32_t n_playouts, const bk_rollout_cfg* cfg,
+                        const uint32_t* compat_seeds, bk_result* out, bk_state* out_states,
+                        bk_fset* out_sets, int mem);
+
+/*
  * FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256) for n_games independent
  * roots, one wave per game.  Game i's root children are legal[legal_offset[i] ..
  * legal_offset[i+1]) (any int payload; only the count and order matter: expansion pops

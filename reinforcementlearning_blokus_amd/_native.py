@@ -29,7 +29,13 @@ EXPORTS = (
     "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream",
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
+    "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
 )
+FSET_SLOTS = 256
+# bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
+FSET_DTYPE = np.dtype([("key", "<i2", (4, FSET_SLOTS)), ("mask", "<u2", (4,)), ("fill", "<u2", (4,)),
+                       ("used", "<u2", (4,)), ("reserved", "<u2", (4,))])
+assert FSET_DTYPE.itemsize == 2080
 FASTMCTS_TOP = 10
 FASTMCTS_MAX_CHILDREN = 2048
 
@@ -111,6 +117,12 @@ def load():
             "bk_advance": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
             "bk_fastmcts": (C.c_int, [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32, C.c_double, vp, vp, C.c_int]),
             "bk_last_kernel_ms": (C.c_int, [vp, P(C.c_float)]),
+            "bk_fset_init": (C.c_int, [vp]),
+            "bk_fset_place": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32]),
+            "bk_fset_copy": (C.c_int, [vp, vp]),
+            "bk_fset_list": (C.c_int, [vp, C.c_int32, vp, C.c_int32]),
+            "bk_rollout_frontier": (C.c_int, [vp, vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, vp,
+                                              vp, C.c_int]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -130,6 +142,40 @@ def orient_table():
             raise NativeUnavailable("bk_orient_info failed")
         out.append((pid.value, o.value, [(offs[2 * k], offs[2 * k + 1]) for k in range(n.value)]))
     return out
+
+
+def fset_new(n: int = 1) -> np.ndarray:
+    """n bk_fset records initialised as Board() does (each set = {start corner})."""
+    L = load()
+    out = np.zeros(n, dtype=FSET_DTYPE)
+    for i in range(n):
+        if L.bk_fset_init(out[i:i + 1].ctypes.data) != OK:
+            raise RuntimeError("bk_fset_init failed")
+    return out
+
+
+def fset_place(fs: np.ndarray, after_state: np.ndarray, player: int, cells) -> None:
+    """Frontier update of place_piece (engine/board.py:315-367) on record fs (1 element),
+    given the packed board after the move and the placed cells (r*20+c, in order)."""
+    L = load()
+    c = np.ascontiguousarray(cells, dtype=np.int32)
+    rc = L.bk_fset_place(fs.ctypes.data, after_state.ctypes.data, int(player), c.ctypes.data, len(c))
+    if rc != OK:
+        raise RuntimeError(f"bk_fset_place failed ({rc})")
+
+
+def fset_copy(dst: np.ndarray, src: np.ndarray) -> None:
+    if load().bk_fset_copy(dst.ctypes.data, src.ctypes.data) != OK:
+        raise RuntimeError("bk_fset_copy failed")
+
+
+def fset_list(fs: np.ndarray, player: int) -> list:
+    """Iteration order of player's frontier set (cells r*20+c)."""
+    buf = np.zeros(FSET_SLOTS, dtype=np.int32)
+    n = load().bk_fset_list(fs.ctypes.data, int(player), buf.ctypes.data, FSET_SLOTS)
+    if n < 0:
+        raise RuntimeError("bk_fset_list failed")
+    return buf[:n].tolist()
 
 
 class Handle:
@@ -206,6 +252,15 @@ class Handle:
                                      C.c_void_p(base_ptr), C.c_void_p(mt_ptr), C.c_void_p(log_ptr), log_len,
                                      float(c), C.c_void_p(out_ptr), C.c_void_p(visits_ptr or None), mem)
         self.check(rc, "bk_fastmcts")
+
+    def rollout_frontier(self, roots_ptr, sets_ptr, n_roots, index_ptr, n_playouts, cfg: BkRolloutCfg, seeds_ptr,
+                         out_ptr, states_ptr, osets_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_rollout_frontier(self._h, C.c_void_p(roots_ptr), C.c_void_p(sets_ptr), n_roots,
+                                             C.c_void_p(index_ptr or 0), n_playouts, C.byref(cfg),
+                                             C.c_void_p(seeds_ptr or 0), C.c_void_p(out_ptr or 0),
+                                             C.c_void_p(states_ptr or 0), C.c_void_p(osets_ptr or 0), mem)
+        self.check(rc, "bk_rollout_frontier")
 
     def advance(self, roots_ptr, n_roots, index_ptr, n, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
         with self._lock:

@@ -393,6 +393,70 @@ __device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2
     out_c = found_c;
 }
 
+// Frontier-order variant (BK_ORDER_FRONTIER): the kk-th anchor of orientation gs in the
+// reference's list order (engine/move_generator.py:261-559).  Pass 1 writes the legal
+// anchors of gs over the B half of each LDS row.  Pass 2 walks the mover's frontier set
+// in slot order and the orientation's cells in order; an anchor counts at its first
+// (frontier cell, cell k) hit, and its bit is cleared when it is counted.
+__device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2* rows, const int16_t* key,
+                                                     int mask, int& out_r, int& out_c) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    const int rlim = 20 - (int)((info >> 16) & 0xFFu);
+    const uint2* base[5];
+    uint32_t sh[5];
+    int cd[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        base[k] = rows + (cell >> 8) * WAVE;
+        sh[k] = cell & 0xFFu;
+        cd[k] = (int)(cell >> 8);
+    }
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        const int rr = r < rlim ? r : rlim;
+        uint2 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = base[k][rr * WAVE];
+        uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
+        uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
+        ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
+        ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
+        rows[r * WAVE].x = r <= rlim ? (ac & ~ab) : 0u;
+    }
+    int found_r = -1, found_c = 0;
+    uint32_t cnt = 0;
+    const uint4* k4 = reinterpret_cast<const uint4*>(key);
+#pragma unroll 1
+    for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 32) {  // 32 slots per batch of loads
+        uint4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) q[j] = k4[(b0 >> 3) + j];
+#pragma unroll 1
+        for (int j = 0; j < 32 && found_r < 0; ++j) {
+            const uint4 w4 = q[j >> 3];
+            const uint32_t w = ((j >> 1) & 3) == 0 ? w4.x : ((j >> 1) & 3) == 1 ? w4.y : ((j >> 1) & 3) == 2 ? w4.z : w4.w;
+            const int f = (int)(int16_t)((j & 1) ? (w >> 16) : (w & 0xFFFFu));
+            if (f < 0) continue;
+            const int fr = f / 20, fc = f - 20 * fr;
+#pragma unroll 1
+            for (int k = 0; k < n; ++k) {
+                const int ar = fr - cd[k], acl = fc - (int)sh[k];
+                if (ar < 0 || ar > 19 || acl < 0 || acl > 19) continue;
+                uint2* rp = rows + ar * WAVE;
+                const uint32_t okw = rp->x;
+                if (!((okw >> acl) & 1u)) continue;
+                if (cnt == kk) { found_r = ar; found_c = acl; break; }
+                rp->x = okw & ~(1u << acl);
+                ++cnt;
+            }
+        }
+    }
+    out_r = found_r;
+    out_c = found_c;
+}
+
 // ------------------------------------------------------------------------------------
 // random streams
 // ------------------------------------------------------------------------------------
@@ -548,6 +612,199 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
     if (live) a.out_mask4[i] = mask;
 }
 
+// ------------------------------------------------------------------------------------
+// Frontier sets: CPython 3.10 set of (row, col) tuples, restated for the reference's
+// frontier ORDER (engine/board.py:315-367 update_frontier_after_move; Objects/
+// setobject.c set_add_entry / set_discard_entry / set_table_resize / set_merge).
+// Shared by the device (tables in a per-lane global record) and the host ABI.
+// ------------------------------------------------------------------------------------
+__constant__ uint64_t kCellHash[BK_CELLS] = BK_CELL_HASH_INIT;
+static const uint64_t kCellHashHost[BK_CELLS] = BK_CELL_HASH_INIT;
+
+#define FS_PROBES 9
+#define FS_SHIFT 5
+#define FS_UNUSED ((int16_t)-1)
+#define FS_DUMMY ((int16_t)-2)
+
+struct FsetRef {  // one player's table
+    int16_t* key;
+    uint16_t* mask;
+    uint16_t* fill;
+    uint16_t* used;
+};
+
+__host__ __device__ __forceinline__ FsetRef fs_ref(bk_fset* s, int p) {
+    return FsetRef{s->key[p], &s->mask[p], &s->fill[p], &s->used[p]};
+}
+
+__host__ __device__ __forceinline__ uint64_t cell_hash(int k) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return kCellHash[k];
+#else
+    return kCellHashHost[k];
+#endif
+}
+
+// set_insert_clean: first unused slot of the probe sequence
+__host__ __device__ inline void fs_insert_clean(int16_t* key, uint32_t mask, int16_t k) {
+    const uint64_t h = cell_hash(k);
+    uint64_t perturb = h;
+    uint64_t i = h & mask;
+    for (;;) {
+        if (key[i] == FS_UNUSED) break;
+        bool hit = false;
+        if (i + FS_PROBES <= mask) {
+            for (int j = 0; j < FS_PROBES; ++j) {
+                ++i;
+                if (key[i] == FS_UNUSED) { hit = true; break; }
+            }
+        }
+        if (hit) break;
+        perturb >>= FS_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+    key[i] = k;
+}
+
+// set_table_resize(minused): fresh table, active entries re-inserted in slot order.
+// tmp holds the old keys (BK_FSET_SLOTS entries).  false: would outgrow the table.
+__host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minused) {
+    uint32_t newsize = 8;
+    while (newsize <= minused) newsize <<= 1;
+    if (newsize > BK_FSET_SLOTS) return false;
+    const uint32_t omask = *t.mask;
+    for (uint32_t i = 0; i <= omask; ++i) tmp[i] = t.key[i];
+    for (uint32_t i = 0; i < newsize; ++i) t.key[i] = FS_UNUSED;
+    *t.mask = (uint16_t)(newsize - 1);
+    *t.fill = *t.used;
+    for (uint32_t i = 0; i <= omask; ++i)
+        if (tmp[i] >= 0) fs_insert_clean(t.key, newsize - 1, tmp[i]);
+    return true;
+}
+
+// set_add_entry: an existing key is a no-op; a new key takes the LAST dummy seen on its
+// probe chain, else the unused slot that ended the search (then maybe resize)
+__host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
+    const uint64_t h = cell_hash(k);
+    const uint32_t mask = *t.mask;
+    uint64_t perturb = h;
+    uint64_t i = h & mask, e = 0;
+    int64_t freeslot = -1;
+    for (;;) {
+        e = i;
+        int probes = (i + FS_PROBES <= mask) ? FS_PROBES : 0;
+        bool unused = false;
+        for (;;) {
+            const int16_t kk = t.key[e];
+            if (kk == FS_UNUSED) { unused = true; break; }
+            if (kk == k) return true;
+            if (kk == FS_DUMMY) freeslot = (int64_t)e;
+            ++e;
+            if (probes-- == 0) break;
+        }
+        if (unused) break;
+        perturb >>= FS_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+    if (freeslot >= 0) {
+        *t.used += 1;
+        t.key[freeslot] = k;
+        return true;
+    }
+    *t.fill += 1;
+    *t.used += 1;
+    t.key[e] = k;
+    if ((uint64_t)*t.fill * 5 < (uint64_t)mask * 3) return true;
+    return fs_resize(t, tmp, *t.used > 50000 ? *t.used * 2u : *t.used * 4u);
+}
+
+// set_discard_entry: the key's slot becomes a dummy
+__host__ __device__ inline void fs_discard(FsetRef t, int16_t k) {
+    const uint64_t h = cell_hash(k);
+    const uint32_t mask = *t.mask;
+    uint64_t perturb = h;
+    uint64_t i = h & mask;
+    for (;;) {
+        uint64_t e = i;
+        int probes = (i + FS_PROBES <= mask) ? FS_PROBES : 0;
+        for (;;) {
+            const int16_t kk = t.key[e];
+            if (kk == FS_UNUSED) return;
+            if (kk == k) {
+                t.key[e] = FS_DUMMY;
+                *t.used -= 1;
+                return;
+            }
+            ++e;
+            if (probes-- == 0) break;
+        }
+        perturb >>= FS_SHIFT;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+__host__ __device__ inline void fs_clear(FsetRef t) {
+    for (int i = 0; i < BK_FSET_SLOTS; ++i) t.key[i] = FS_UNUSED;
+    *t.mask = 7;
+    *t.fill = 0;
+    *t.used = 0;
+}
+
+// update_frontier_after_move for player p, engine/board.py:315-367.  occ(r, c) / own(r, c)
+// read the board AFTER all the piece's cells were written.  false: table overflow.
+template <typename Occ, typename Own>
+__host__ __device__ inline bool fs_place(FsetRef t, int16_t* tmp, const int32_t* cells, int n, Occ occ, Own own) {
+    const int DR[4] = {-1, -1, 1, 1}, DC[4] = {-1, 1, -1, 1};  // diagonal, reference order
+    const int OR_[4] = {-1, 1, 0, 0}, OC[4] = {0, 0, -1, 1};    // orthogonal, reference order
+    for (int i = 0; i < n; ++i) {
+        const int r = cells[i] / 20, c = cells[i] % 20;
+        fs_discard(t, (int16_t)cells[i]);
+        for (int d = 0; d < 4; ++d) {
+            const int nr = r + DR[d], nc = c + DC[d];
+            if (nr < 0 || nr >= 20 || nc < 0 || nc >= 20 || occ(nr, nc)) continue;
+            bool orth = false;
+            for (int e = 0; e < 4 && !orth; ++e) {
+                const int qr = nr + OR_[e], qc = nc + OC[e];
+                if (qr >= 0 && qr < 20 && qc >= 0 && qc < 20 && own(qr, qc)) orth = true;
+            }
+            if (!orth && !fs_add(t, tmp, (int16_t)(nr * 20 + nc))) return false;
+        }
+        for (int d = 0; d < 4; ++d) {
+            const int nr = r + OR_[d], nc = c + OC[d];
+            if (nr >= 0 && nr < 20 && nc >= 0 && nc < 20) fs_discard(t, (int16_t)(nr * 20 + nc));
+        }
+    }
+    return true;
+}
+
+// set.copy() (make_new_set + set_merge into an empty set)
+__host__ __device__ inline void fs_copy(FsetRef d, const int16_t* skey, uint32_t smask, uint32_t sfill,
+                                        uint32_t sused) {
+    fs_clear(d);
+    if (sused == 0) return;
+    if (sused * 5 >= 7u * 3u) {  // (fill + other->used) * 5 >= mask * 3 on the fresh table
+        uint32_t newsize = 8;
+        while (newsize <= sused * 2) newsize <<= 1;
+        *d.mask = (uint16_t)(newsize - 1);
+    }
+    if (*d.mask == smask && sfill == sused) {
+        for (uint32_t i = 0; i <= smask; ++i) d.key[i] = skey[i];
+        *d.fill = (uint16_t)sfill;
+        *d.used = (uint16_t)sused;
+        return;
+    }
+    *d.fill = (uint16_t)sused;
+    *d.used = (uint16_t)sused;
+    for (uint32_t i = 0; i <= smask; ++i)
+        if (skey[i] >= 0) fs_insert_clean(d.key, *d.mask, skey[i]);
+}
+
+// per-lane frontier record in the rollout kernel: the tables plus resize scratch
+struct FsLane {
+    bk_fset s;
+    int16_t tmp[BK_FSET_SLOTS];
+};
+
 struct RolloutArgs {
     const bk_state* roots;
     int32_t n_roots;
@@ -561,6 +818,9 @@ struct RolloutArgs {
     uint32_t* counter;  // [0] = next playout; [1] = error word
     uint32_t max_iters; // safety valve: loop iterations any lane can need
     bk_state* out_states; // BK_SEM_ADVANCE
+    const bk_fset* root_sets;  // frontier order: roots' tables
+    bk_fset* out_sets;         // frontier order + BK_SEM_ADVANCE
+    FsLane* fslab;             // frontier order: one record per slot
 };
 
 // four per-player scalars (kept as separate SSA values: an array indexed by a
@@ -587,7 +847,7 @@ struct Game {
     uint32_t draws;
     uint32_t pcount;    // philox counter
     uint32_t move_count0;
-    bool overflow;
+    uint32_t status;    // bk_result.status bits: 1 rng stream overflow, 2 frontier table overflow
 };
 
 __device__ __forceinline__ int board_score_q(const Game& g, int q) {  // q static
@@ -624,9 +884,19 @@ __device__ __forceinline__ void store_state(const RolloutArgs& a, const Game& g,
     o->reserved[0] = o->reserved[1] = 0;
 }
 
+__device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
+    static_assert(sizeof(bk_fset) % 16 == 0, "bk_fset is copied as uint4");
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll 2
+    for (int i = 0; i < (int)(sizeof(bk_fset) / 16); ++i) d4[i] = s4[i];
+}
+
+template <bool FR>
 __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot) {
     if (a.cfg.semantics == BK_SEM_ADVANCE) {
         store_state(a, g, slab);
+        if constexpr (FR) copy_fset(a.out_sets + g.pid, &a.fslab[slot].s);
         if (a.out == nullptr) { g.pid = -1; return; }
     }
     bk_result r;
@@ -670,11 +940,12 @@ __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const
     }
     r.plies = (uint16_t)g.plies;
     r.draws = g.draws;
-    r.status = g.overflow ? 1 : 0;
+    r.status = (uint8_t)g.status;
     a.out[g.pid] = r;
     g.pid = -1;
 }
 
+template <bool FR>
 __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot, int32_t pid) {
     const int32_t ri = a.root_index ? a.root_index[pid] : (pid % a.n_roots);
     const bk_state* s = a.roots + ri;
@@ -710,7 +981,20 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
     g.root_score = board_score(g, g.cur);
     g.draws = 0;
     g.pcount = 0;
-    g.overflow = false;
+    g.status = 0;
+    if constexpr (FR) {
+        if (a.cfg.semantics == BK_SEM_ROLLOUT) {
+            // MCTSAgent._rollout plays on sim = board.copy() (mcts/mcts_agent.py:470):
+            // set.copy() re-lays the tables out
+            bk_fset* d = &a.fslab[slot].s;
+            const bk_fset* src = a.root_sets + ri;
+#pragma unroll 1
+            for (int q = 0; q < 4; ++q)
+                fs_copy(fs_ref(d, q), src->key[q], src->mask[q], src->fill[q], src->used[q]);
+        } else {
+            copy_fset(&a.fslab[slot].s, a.root_sets + ri);
+        }
+    }
     if (a.cfg.rng == BK_RNG_NUMPY_MT) {
         const int nstreams = a.cfg.seats_share_stream ? 1 : 4;
         for (int q = 0; q < nstreams; ++q) {
@@ -735,10 +1019,12 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
         uint32_t* base = slab.base + SLAB_RNG_BASE + 4 * q;
         MtCursor m;
         m.i = base[0]; m.a = base[1]; m.b = base[2]; m.c = base[3];
+        bool ov = (g.status & 1u) != 0u;
         do {
-            v = mt_cursor_next(m, g.overflow) & mask;
+            v = mt_cursor_next(m, ov) & mask;
             g.draws++;
-        } while (v > rng && !g.overflow);
+        } while (v > rng && !ov);
+        if (ov) g.status |= 1u;
         base[0] = m.i; base[1] = m.a; base[2] = m.b; base[3] = m.c;
         if (v > rng) v = 0;
     } else {
@@ -750,6 +1036,7 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
     return v;
 }
 
+template <bool FR>
 __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     __shared__ uint32_t lds[ROLL_WORDS_PER_WAVE * (BLOCK / WAVE)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
@@ -770,7 +1057,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             if (g.pid < 0) {
                 const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
                 if (next >= a.n_playouts) { done = true; break; }
-                start_game(a, g, slab, slot, next);
+                start_game<FR>(a, g, slab, slot, next);
             }
             if (arena) {
 #pragma unroll 1
@@ -779,11 +1066,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                     g.cur = (g.cur + 1) & 3;
                 }
                 if (g.out == 0xFu || (advance ? g.plies : g.turns) >= cap) {
-                    finish_game(a, g, slab, slot);
+                    finish_game<FR>(a, g, slab, slot);
                     continue;
                 }
             } else if (g.plies >= cap) {
-                finish_game(a, g, slab, slot);
+                finish_game<FR>(a, g, slab, slot);
                 continue;
             }
             break;
@@ -816,7 +1103,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 g.passes++; g.turns++; g.since_move++;
                 g.cur = (g.cur + 1) & 3;
             } else {
-                finish_game(a, g, slab, slot);  // MCTSAgent._rollout breaks
+                finish_game<FR>(a, g, slab, slot);  // MCTSAgent._rollout breaks
             }
             continue;
         }
@@ -827,7 +1114,12 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
         int ar, ac;
-        locate_move_lds(gs, kk, rows_lds, ar, ac);
+        if constexpr (FR) {
+            const bk_fset* fs = &a.fslab[slot].s;
+            locate_move_frontier(gs, kk, rows_lds, fs->key[p], fs->mask[p], ar, ac);
+        } else {
+            locate_move_lds(gs, kk, rows_lds, ar, ac);
+        }
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
         const uint32_t info = kInfo[gs];
         const int n = (int)((info >> 8) & 0xFFu);
@@ -854,18 +1146,39 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 }
             }
         }
+        if constexpr (FR) {  // the mover's frontier set (engine/board.py:548 -> :315-367)
+            int32_t cells[5];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) {
+                const uint32_t cell = kCells[gs][q < n ? q : 0];
+                cells[q] = (ar + (int)(cell >> 8)) * 20 + ac + (int)(cell & 0xFFu);
+            }
+            FsLane* fl = &a.fslab[slot];
+            const uint32_t* occ_rows = slab.base + 4 * 20;
+            const uint32_t* own_rows = slab.base + p * 20;
+            if (!fs_place(fs_ref(&fl->s, p), fl->tmp, cells, n,
+                          [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; },
+                          [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; })) {
+                g.status |= 2u;
+            }
+        }
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
         g.used.set(p, g.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
         g.first &= ~(1u << p);
         g.plies++; g.turns++; g.since_move = 0;
         g.cur = (g.cur + 1) & 3;
+        if constexpr (FR) {
+            if (g.status & 2u) finish_game<FR>(a, g, slab, slot);  // status 2: table overflow
+        }
     }
 }
 
 // Two entry points over one body so profiles separate root generation (bk_advance)
 // from the measured playouts (bk_rollout).
-__global__ __launch_bounds__(BLOCK, 3) void k_rollout(RolloutArgs a) { rollout_body(a); }
-__global__ __launch_bounds__(BLOCK, 3) void k_advance(RolloutArgs a) { rollout_body(a); }
+__global__ __launch_bounds__(BLOCK, 3) void k_rollout(RolloutArgs a) { rollout_body<false>(a); }
+__global__ __launch_bounds__(BLOCK, 3) void k_advance(RolloutArgs a) { rollout_body<false>(a); }
+// reference frontier order (compat parity mode)
+__global__ __launch_bounds__(BLOCK, 2) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
 
 // ------------------------------------------------------------------------------------
 // FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256): one wave per game
@@ -1041,6 +1354,9 @@ struct bk_handle_s {
     void* d_aux = nullptr; size_t d_aux_cap = 0;
     void* d_aux2 = nullptr; size_t d_aux2_cap = 0;
     void* d_slab = nullptr; size_t d_slab_cap = 0;
+    void* d_fin = nullptr; size_t d_fin_cap = 0;     // frontier: root tables
+    void* d_fout = nullptr; size_t d_fout_cap = 0;   // frontier: advanced tables
+    void* d_fslab = nullptr; size_t d_fslab_cap = 0; // frontier: per-slot records
     uint32_t* d_counter = nullptr;
     int num_cu = 0;
     int rollout_blocks_per_cu = 0;
@@ -1120,7 +1436,8 @@ int bk_destroy(bk_handle h) {
     if (!h) return BK_EINVAL;
     (void)hipSetDevice(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
-    void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_counter};
+    void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
+                    h->d_counter};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -1236,7 +1553,8 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
 
 static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index,
                            int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
-                           bk_result* out, bk_state* out_states, int mem) {
+                           bk_result* out, bk_state* out_states, int mem, const bk_fset* root_sets = nullptr,
+                           bk_fset* out_sets = nullptr) {
     if (!h || !roots || !cfg || n_roots <= 0 || n_playouts < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
         return set_err(h, BK_EINVAL, "bk_rollout: invalid arguments%s", "");
     if (cfg->semantics != BK_SEM_ARENA && cfg->semantics != BK_SEM_ROLLOUT && cfg->semantics != BK_SEM_ADVANCE)
@@ -1244,8 +1562,13 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     if ((cfg->semantics == BK_SEM_ADVANCE) != (out_states != nullptr))
         return set_err(h, BK_EINVAL, "bk_rollout: out_states goes with BK_SEM_ADVANCE only%s", "");
     if (!out && !out_states) return set_err(h, BK_EINVAL, "bk_rollout: no output%s", "");
-    if (cfg->order != BK_ORDER_NAIVE)
-        return set_err(h, BK_EINVAL, "bk_rollout: only BK_ORDER_NAIVE is implemented on the GPU%s", "");
+    const bool fr = cfg->order == BK_ORDER_FRONTIER;
+    if (cfg->order != BK_ORDER_NAIVE && !fr) return set_err(h, BK_EINVAL, "bk_rollout: unknown order%s", "");
+    if (fr != (root_sets != nullptr))
+        return set_err(h, BK_EINVAL, "bk_rollout: BK_ORDER_FRONTIER goes with root frontier sets "
+                                     "(bk_rollout_frontier)%s", "");
+    if (fr && (cfg->semantics == BK_SEM_ADVANCE) != (out_sets != nullptr))
+        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_sets goes with BK_SEM_ADVANCE%s", "");
     if (cfg->rng != BK_RNG_PHILOX && cfg->rng != BK_RNG_NUMPY_MT)
         return set_err(h, BK_EINVAL, "bk_rollout: unknown rng%s", "");
     if (cfg->rng == BK_RNG_NUMPY_MT && !compat_seeds)
@@ -1265,8 +1588,14 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                       &h->d_aux2_cap);
         if (rc) return rc;
     }
+    void* d_rsets = nullptr;
+    if (fr) {
+        rc = stage_in(h, root_sets, sizeof(bk_fset) * (size_t)n_roots, mem, &d_rsets, &h->d_fin, &h->d_fin_cap);
+        if (rc) return rc;
+    }
     bk_result* d_out = out;
     bk_state* d_states = out_states;
+    bk_fset* d_osets = out_sets;
     if (mem == BK_MEM_HOST) {
         const size_t rb = out ? sizeof(bk_result) * (size_t)n_playouts : 0;
         const size_t sb = out_states ? sizeof(bk_state) * (size_t)n_playouts : 0;
@@ -1274,6 +1603,11 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         if (rc) return rc;
         d_out = out ? (bk_result*)h->d_out : nullptr;
         d_states = out_states ? (bk_state*)((char*)h->d_out + rb) : nullptr;
+        if (out_sets) {
+            rc = grow(h, &h->d_fout, &h->d_fout_cap, sizeof(bk_fset) * (size_t)n_playouts);
+            if (rc) return rc;
+            d_osets = (bk_fset*)h->d_fout;
+        }
     }
     // persistent grid: every resident slot pulls playouts from the counter
     int blocks = h->num_cu * h->rollout_blocks_per_cu;
@@ -1283,15 +1617,22 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     const uint32_t nslots = (uint32_t)blocks * BLOCK;
     rc = grow(h, &h->d_slab, &h->d_slab_cap, sizeof(uint32_t) * SLAB_WORDS * (size_t)nslots);
     if (rc) return rc;
+    if (fr) {
+        rc = grow(h, &h->d_fslab, &h->d_fslab_cap, sizeof(FsLane) * (size_t)nslots);
+        if (rc) return rc;
+    }
     HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
     const uint64_t per_lane = ((uint64_t)n_playouts + nslots - 1) / nslots + 1;
     const uint64_t per_game = (cfg->semantics == BK_SEM_ROLLOUT ? (uint64_t)cfg->max_plies + 2u : 100u);
     const uint64_t iters = per_lane * per_game + 64u;
     RolloutArgs a{(const bk_state*)d_roots, n_roots, (const int32_t*)d_idx, n_playouts, *cfg,
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
-                  (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states};
+                  (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
+                  (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    if (cfg->semantics == BK_SEM_ADVANCE)
+    if (fr)
+        hipLaunchKernelGGL(k_rollout_fr, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
+    else if (cfg->semantics == BK_SEM_ADVANCE)
         hipLaunchKernelGGL(k_advance, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     else
         hipLaunchKernelGGL(k_rollout, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
@@ -1303,6 +1644,9 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
             HIPCHK(h, hipMemcpyAsync(out, d_out, sizeof(bk_result) * (size_t)n_playouts, hipMemcpyDeviceToHost, h->cur));
         if (out_states)
             HIPCHK(h, hipMemcpyAsync(out_states, d_states, sizeof(bk_state) * (size_t)n_playouts,
+                                     hipMemcpyDeviceToHost, h->cur));
+        if (out_sets)
+            HIPCHK(h, hipMemcpyAsync(out_sets, d_osets, sizeof(bk_fset) * (size_t)n_playouts,
                                      hipMemcpyDeviceToHost, h->cur));
         uint32_t ctr[4];
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
@@ -1324,6 +1668,72 @@ int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_
     if (!out_states || !cfg || cfg->semantics != BK_SEM_ADVANCE)
         return set_err(h, BK_EINVAL, "bk_advance: needs out_states and BK_SEM_ADVANCE%s", "");
     return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, nullptr, out_states, mem);
+}
+
+int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_sets, int32_t n_roots,
+                        const int32_t* root_index, int32_t n_playouts, const bk_rollout_cfg* cfg,
+                        const uint32_t* compat_seeds, bk_result* out, bk_state* out_states, bk_fset* out_sets,
+                        int mem) {
+    if (!cfg || cfg->order != BK_ORDER_FRONTIER || !root_sets)
+        return set_err(h, BK_EINVAL, "bk_rollout_frontier: needs BK_ORDER_FRONTIER and root_sets%s", "");
+    if ((cfg->semantics == BK_SEM_ADVANCE) != (out_states != nullptr))
+        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_states goes with BK_SEM_ADVANCE%s", "");
+    if (cfg->semantics != BK_SEM_ADVANCE && !out)
+        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out is NULL%s", "");
+    return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, out, out_states, mem,
+                           root_sets, out_sets);
+}
+
+// ---- host-side frontier tables (no GPU) ---------------------------------------------
+static const int32_t kCornerCell[4] = {0, 19, 399, 380};  // engine/board.py:57-61
+
+int bk_fset_init(bk_fset* s) {
+    if (!s) return BK_EINVAL;
+    memset(s, 0, sizeof *s);
+    for (int p = 0; p < 4; ++p) {
+        FsetRef t = fs_ref(s, p);
+        fs_clear(t);
+        int16_t tmp[BK_FSET_SLOTS];
+        fs_add(t, tmp, (int16_t)kCornerCell[p]);  // init_frontier_for_player :385-405
+    }
+    return BK_OK;
+}
+
+int bk_fset_place(bk_fset* s, const bk_state* after, int32_t player, const int32_t* cells, int32_t n) {
+    if (!s || !after || player < 0 || player > 3 || !cells || n < 0 || n > 5) return BK_EINVAL;
+    for (int i = 0; i < n; ++i)
+        if (cells[i] < 0 || cells[i] >= BK_CELLS) return BK_EINVAL;
+    auto bit = [&](int q, int r, int c) {
+        const int b = r * 20 + c;
+        return ((after->planes[q][b >> 6] >> (b & 63)) & 1ull) != 0ull;
+    };
+    int16_t tmp[BK_FSET_SLOTS];
+    const bool ok = fs_place(fs_ref(s, player), tmp, cells, n,
+                             [&](int r, int c) { return bit(0, r, c) || bit(1, r, c) || bit(2, r, c) || bit(3, r, c); },
+                             [&](int r, int c) { return bit(player, r, c); });
+    return ok ? BK_OK : BK_EOVERFLOW;
+}
+
+int bk_fset_copy(bk_fset* dst, const bk_fset* src) {
+    if (!dst || !src) return BK_EINVAL;
+    if (dst == src) return BK_OK;
+    for (int p = 0; p < 4; ++p) {
+        if (src->mask[p] + 1u > BK_FSET_SLOTS) return BK_EINVAL;
+        fs_copy(fs_ref(dst, p), src->key[p], src->mask[p], src->fill[p], src->used[p]);
+    }
+    return BK_OK;
+}
+
+int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {
+    if (!s || player < 0 || player > 3 || (cap > 0 && !out) || s->mask[player] + 1u > BK_FSET_SLOTS)
+        return BK_EINVAL;
+    int n = 0;
+    for (int i = 0; i <= s->mask[player]; ++i)
+        if (s->key[player][i] >= 0) {
+            if (n < cap) out[n] = s->key[player][i];
+            ++n;
+        }
+    return n;
 }
 
 int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,

@@ -120,6 +120,40 @@ class BlokusGPU:
                             seeds.ctypes.data if seeds is not None else 0, res.ctypes.data, N.MEM_HOST)
         return res
 
+    # ------------------------------------------------------------------ frontier order
+    def rollout_frontier(self, roots, root_sets, n_playouts: int, *, semantics: int = N.SEM_ARENA,
+                         rng: int = N.RNG_NUMPY_MT, seed: int = 0, max_plies: int | None = None,
+                         compat_seeds=None, root_index=None, seats_share_stream: bool = False):
+        """Playouts in the reference's FRONTIER list order (bk_rollout_frontier): with the
+        numpy-MT compat stream these are the reference's default-config games.
+        root_sets: FSET_DTYPE records (one per root).  Host numpy in/out."""
+        if max_plies is None:
+            max_plies = 2500 if semantics == N.SEM_ARENA else 50
+        cfg = N.BkRolloutCfg(semantics, N.ORDER_FRONTIER, rng, max_plies, seed & (2**64 - 1),
+                             int(seats_share_stream), 0)
+        st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
+        fs = np.ascontiguousarray(root_sets, dtype=N.FSET_DTYPE)
+        assert fs.shape[0] == st.shape[0]
+        idx = np.ascontiguousarray(root_index, dtype=np.int32) if root_index is not None else None
+        seeds = np.ascontiguousarray(compat_seeds, dtype=np.uint32).reshape(-1, 4) if compat_seeds is not None else None
+        if seeds is not None:
+            assert seeds.shape[0] >= n_playouts
+        self.handle.set_stream(None)
+        if semantics == N.SEM_ADVANCE:
+            out_st = np.zeros(n_playouts, dtype=STATE_DTYPE)
+            out_fs = np.zeros(n_playouts, dtype=N.FSET_DTYPE)
+            self.handle.rollout_frontier(st.ctypes.data, fs.ctypes.data, st.shape[0],
+                                         idx.ctypes.data if idx is not None else 0, n_playouts, cfg,
+                                         seeds.ctypes.data if seeds is not None else 0, 0, out_st.ctypes.data,
+                                         out_fs.ctypes.data, N.MEM_HOST)
+            return out_st, out_fs
+        res = np.zeros(n_playouts, dtype=RESULT_DTYPE)
+        self.handle.rollout_frontier(st.ctypes.data, fs.ctypes.data, st.shape[0],
+                                     idx.ctypes.data if idx is not None else 0, n_playouts, cfg,
+                                     seeds.ctypes.data if seeds is not None else 0, res.ctypes.data, 0, 0,
+                                     N.MEM_HOST)
+        return res
+
     # ------------------------------------------------------------------ positions
     def advance(self, roots, n: int, plies: int, *, seed: int = 0, root_index=None):
         """Play `plies` uniformly random moves (naive order, Philox stream) from each root

@@ -74,3 +74,16 @@ def ints_to_rows(ints):
         g, rest = divmod(int(a), 400)
         rows[g, rest // 20] |= np.uint32(1 << (rest % 20))
     return rows
+
+
+def fset_of(rec):
+    """The reference's frontier tables for a positions.json record (bk_fset_place replay)."""
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.engine.board import Board, Player, Position, pack_state
+    b = Board()
+    fs = N.fset_new(1)
+    for player_value, piece_id, cells in rec["log"]:
+        b.current_player = Player(player_value)
+        b.place_piece([Position(r, c) for r, c in cells], Player(player_value), piece_id, validate=False)
+        N.fset_place(fs, pack_state(b), player_value - 1, [r * 20 + c for r, c in cells])
+    return fs[0]

@@ -106,6 +106,21 @@ def render_classes(table):
     return lines
 
 
+def render_cell_hash():
+    """hash((r, c)) of this CPython (3.10: xxHash-based tuplehash over the int hashes),
+    as the 64-bit pattern: the frontier sets' slot order depends on it
+    (engine/board.py:70 player_frontiers are sets of (row, col) tuples)."""
+    import sys
+    assert sys.version_info[:2] == (3, 10), "the reference runs CPython 3.10"
+    vals = [hash((r, c)) & (2**64 - 1) for r in range(20) for c in range(20)]
+    lines = ["// CPython 3.10 hash((r, c)) for cell r*20+c (frontier set slot order)",
+             "#define BK_CELL_HASH_INIT { \\"]
+    for i in range(0, 400, 4):
+        lines.append("    " + ", ".join(f"{v:#018x}ull" for v in vals[i:i + 4]) + ", \\")
+    lines.append("}")
+    return lines
+
+
 def render(table):
     lines = [
         "// Generated by tools/gen_tables.py -- do not edit.",
@@ -151,6 +166,7 @@ def render(table):
         lines.append("    {" + ", ".join(words) + "}, \\")
     lines.append("}")
     lines += render_classes(table)
+    lines += render_cell_hash()
     return "\n".join(lines) + "\n"
 
 
