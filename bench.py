@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=20260301)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
+                    help="in-kernel move order: naive (default) or the reference's frontier order "
+                         "(CPython set tables carried per game)")
     return ap.parse_args()
 
 
@@ -90,8 +93,15 @@ def main():
     dev = torch.device("cuda", local)
     seed = args.seed + 1_000_003 * rank
     # synthetic mid-game roots, generated on the GPU (BK_SEM_ADVANCE from the empty board)
-    roots_np = gpu.advance(empty_state(), args.games, args.root_plies, seed=seed,
-                           root_index=np.zeros(args.games, dtype=np.int32))
+    if args.order == "frontier":
+        roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), args.games,
+                                                 semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=seed,
+                                                 max_plies=args.root_plies,
+                                                 root_index=np.zeros(args.games, dtype=np.int32))
+        sets = torch.from_numpy(sets_np.view(np.uint8).reshape(args.games, -1).copy()).to(dev)
+    else:
+        roots_np = gpu.advance(empty_state(), args.games, args.root_plies, seed=seed,
+                               root_index=np.zeros(args.games, dtype=np.int32))
     roots = torch.from_numpy(roots_np.view(np.uint8).reshape(args.games, 256)).to(dev)
     n = args.games * args.rollouts
     # game j's rollouts are contiguous (one wave plays 64 rollouts of the same game)
@@ -102,6 +112,10 @@ def main():
     plies_acc = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def step(k):
+        if args.order == "frontier":
+            gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k,
+                                 root_index=idx, out=out)
+            return
         gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k, root_index=idx,
                     out=out)
 
@@ -153,7 +167,7 @@ def main():
         achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
         traffic = valu_insts = None
         tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
-        if os.path.exists(tpath):
+        if os.path.exists(tpath) and args.order == "naive":  # PMC pass is of k_rollout
             try:
                 tj = json.load(open(tpath))
                 traffic, valu_insts = tj.get("bytes_per_launch"), tj.get("valu_insts_per_launch")
@@ -177,12 +191,13 @@ def main():
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": "config3: 256 concurrent games x 1024 random rollouts (arena semantics, "
-                                   "naive move order, Philox RNG) from GPU-generated 20-ply positions",
+                                   f"{args.order} move order, Philox RNG) from GPU-generated 20-ply positions",
                        "games": args.games, "rollouts_per_game": args.rollouts, "root_plies": args.root_plies,
                        "playouts_per_step": n, "parallelism": f"dp{world} (independent games per rank)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout", "kernel_ms": avg_ms, "plies_per_sim": plies_per_sim},
+                         "kernel": "k_rollout_fr" if args.order == "frontier" else "k_rollout",
+                         "kernel_ms": avg_ms, "plies_per_sim": plies_per_sim},
             "compute_roofline": {"bound": "valu_int32", "achieved": valu_tops, "peak": VALU_PEAK_TOPS,
                                  "unit": "Tlane-op/s", "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
                                  "peak_single_issue": VALU_SINGLE_TOPS,

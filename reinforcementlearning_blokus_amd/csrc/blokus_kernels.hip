@@ -204,6 +204,9 @@ struct StencilClass {
 // dead once the move's orientation is picked; the same bytes then hold the mover's
 // B/C rows 0..19 as [row][lane]{B, C} pairs for locate_move_lds.
 #define ROLL_WORDS_PER_WAVE (40 * WAVE)
+// frontier-order kernel: 64 dwords per lane; after the move is located the area also
+// stages the mover's frontier table ([slot][lane] int16, up to 128 slots)
+#define ROLL_WORDS_FR (64 * WAVE)
 
 // Legal-move counts of one board-player for the class's table entries [i0, i1); with
 // STORE, also the per-orientation counts (cl = this lane's dword 0, stride WAVE).
@@ -626,66 +629,62 @@ static const uint64_t kCellHashHost[BK_CELLS] = BK_CELL_HASH_INIT;
 #define FS_UNUSED ((int16_t)-1)
 #define FS_DUMMY ((int16_t)-2)
 
-struct FsetRef {  // one player's table
+struct FsetRef {  // one player's table: slot i at key[i * stride]
     int16_t* key;
+    int stride;
     uint16_t* mask;
     uint16_t* fill;
     uint16_t* used;
+    uint32_t cap;     // largest table this storage holds (power of 2)
+    const uint64_t* hash;  // hash((r, c)) by cell
+    __host__ __device__ __forceinline__ int16_t& at(uint64_t i) const { return key[i * (uint64_t)stride]; }
 };
 
-__host__ __device__ __forceinline__ FsetRef fs_ref(bk_fset* s, int p) {
-    return FsetRef{s->key[p], &s->mask[p], &s->fill[p], &s->used[p]};
-}
-
-__host__ __device__ __forceinline__ uint64_t cell_hash(int k) {
-#ifdef __HIP_DEVICE_COMPILE__
-    return kCellHash[k];
-#else
-    return kCellHashHost[k];
-#endif
+__host__ __device__ __forceinline__ FsetRef fs_ref(bk_fset* s, int p, const uint64_t* htab) {
+    return FsetRef{s->key[p], 1, &s->mask[p], &s->fill[p], &s->used[p], BK_FSET_SLOTS, htab};
 }
 
 // set_insert_clean: first unused slot of the probe sequence
-__host__ __device__ inline void fs_insert_clean(int16_t* key, uint32_t mask, int16_t k) {
-    const uint64_t h = cell_hash(k);
+__host__ __device__ inline void fs_insert_clean(FsetRef t, uint32_t mask, int16_t k) {
+    const uint64_t h = t.hash[k];
     uint64_t perturb = h;
     uint64_t i = h & mask;
     for (;;) {
-        if (key[i] == FS_UNUSED) break;
+        if (t.at(i) == FS_UNUSED) break;
         bool hit = false;
         if (i + FS_PROBES <= mask) {
             for (int j = 0; j < FS_PROBES; ++j) {
                 ++i;
-                if (key[i] == FS_UNUSED) { hit = true; break; }
+                if (t.at(i) == FS_UNUSED) { hit = true; break; }
             }
         }
         if (hit) break;
         perturb >>= FS_SHIFT;
         i = (i * 5 + 1 + perturb) & mask;
     }
-    key[i] = k;
+    t.at(i) = k;
 }
 
 // set_table_resize(minused): fresh table, active entries re-inserted in slot order.
-// tmp holds the old keys (BK_FSET_SLOTS entries).  false: would outgrow the table.
+// tmp (stride 1) holds the old keys.  false: the storage cannot hold the new table.
 __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minused) {
     uint32_t newsize = 8;
     while (newsize <= minused) newsize <<= 1;
-    if (newsize > BK_FSET_SLOTS) return false;
+    if (newsize > t.cap) return false;
     const uint32_t omask = *t.mask;
-    for (uint32_t i = 0; i <= omask; ++i) tmp[i] = t.key[i];
-    for (uint32_t i = 0; i < newsize; ++i) t.key[i] = FS_UNUSED;
+    for (uint32_t i = 0; i <= omask; ++i) tmp[i] = t.at(i);
+    for (uint32_t i = 0; i < newsize; ++i) t.at(i) = FS_UNUSED;
     *t.mask = (uint16_t)(newsize - 1);
     *t.fill = *t.used;
     for (uint32_t i = 0; i <= omask; ++i)
-        if (tmp[i] >= 0) fs_insert_clean(t.key, newsize - 1, tmp[i]);
+        if (tmp[i] >= 0) fs_insert_clean(t, newsize - 1, tmp[i]);
     return true;
 }
 
 // set_add_entry: an existing key is a no-op; a new key takes the LAST dummy seen on its
 // probe chain, else the unused slot that ended the search (then maybe resize)
 __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
-    const uint64_t h = cell_hash(k);
+    const uint64_t h = t.hash[k];
     const uint32_t mask = *t.mask;
     uint64_t perturb = h;
     uint64_t i = h & mask, e = 0;
@@ -695,7 +694,7 @@ __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
         int probes = (i + FS_PROBES <= mask) ? FS_PROBES : 0;
         bool unused = false;
         for (;;) {
-            const int16_t kk = t.key[e];
+            const int16_t kk = t.at(e);
             if (kk == FS_UNUSED) { unused = true; break; }
             if (kk == k) return true;
             if (kk == FS_DUMMY) freeslot = (int64_t)e;
@@ -708,19 +707,19 @@ __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
     }
     if (freeslot >= 0) {
         *t.used += 1;
-        t.key[freeslot] = k;
+        t.at(freeslot) = k;
         return true;
     }
     *t.fill += 1;
     *t.used += 1;
-    t.key[e] = k;
+    t.at(e) = k;
     if ((uint64_t)*t.fill * 5 < (uint64_t)mask * 3) return true;
     return fs_resize(t, tmp, *t.used > 50000 ? *t.used * 2u : *t.used * 4u);
 }
 
 // set_discard_entry: the key's slot becomes a dummy
 __host__ __device__ inline void fs_discard(FsetRef t, int16_t k) {
-    const uint64_t h = cell_hash(k);
+    const uint64_t h = t.hash[k];
     const uint32_t mask = *t.mask;
     uint64_t perturb = h;
     uint64_t i = h & mask;
@@ -728,10 +727,10 @@ __host__ __device__ inline void fs_discard(FsetRef t, int16_t k) {
         uint64_t e = i;
         int probes = (i + FS_PROBES <= mask) ? FS_PROBES : 0;
         for (;;) {
-            const int16_t kk = t.key[e];
+            const int16_t kk = t.at(e);
             if (kk == FS_UNUSED) return;
             if (kk == k) {
-                t.key[e] = FS_DUMMY;
+                t.at(e) = FS_DUMMY;
                 *t.used -= 1;
                 return;
             }
@@ -744,7 +743,7 @@ __host__ __device__ inline void fs_discard(FsetRef t, int16_t k) {
 }
 
 __host__ __device__ inline void fs_clear(FsetRef t) {
-    for (int i = 0; i < BK_FSET_SLOTS; ++i) t.key[i] = FS_UNUSED;
+    for (uint32_t i = 0; i < t.cap; ++i) t.at(i) = FS_UNUSED;
     *t.mask = 7;
     *t.fill = 0;
     *t.used = 0;
@@ -788,7 +787,7 @@ __host__ __device__ inline void fs_copy(FsetRef d, const int16_t* skey, uint32_t
         *d.mask = (uint16_t)(newsize - 1);
     }
     if (*d.mask == smask && sfill == sused) {
-        for (uint32_t i = 0; i <= smask; ++i) d.key[i] = skey[i];
+        for (uint32_t i = 0; i <= smask; ++i) d.at(i) = skey[i];
         *d.fill = (uint16_t)sfill;
         *d.used = (uint16_t)sused;
         return;
@@ -796,7 +795,7 @@ __host__ __device__ inline void fs_copy(FsetRef d, const int16_t* skey, uint32_t
     *d.fill = (uint16_t)sused;
     *d.used = (uint16_t)sused;
     for (uint32_t i = 0; i <= smask; ++i)
-        if (skey[i] >= 0) fs_insert_clean(d.key, *d.mask, skey[i]);
+        if (skey[i] >= 0) fs_insert_clean(d, *d.mask, skey[i]);
 }
 
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch
@@ -946,7 +945,8 @@ __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const
 }
 
 template <bool FR>
-__device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot, int32_t pid) {
+__device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot, int32_t pid,
+                                           const uint64_t* htab) {
     const int32_t ri = a.root_index ? a.root_index[pid] : (pid % a.n_roots);
     const bk_state* s = a.roots + ri;
     g.pid = pid;
@@ -990,7 +990,7 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
             const bk_fset* src = a.root_sets + ri;
 #pragma unroll 1
             for (int q = 0; q < 4; ++q)
-                fs_copy(fs_ref(d, q), src->key[q], src->mask[q], src->fill[q], src->used[q]);
+                fs_copy(fs_ref(d, q, htab), src->key[q], src->mask[q], src->fill[q], src->used[q]);
         } else {
             copy_fset(&a.fslab[slot].s, a.root_sets + ri);
         }
@@ -1038,10 +1038,17 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
 
 template <bool FR>
 __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
-    __shared__ uint32_t lds[ROLL_WORDS_PER_WAVE * (BLOCK / WAVE)];
+    constexpr int AREA = FR ? ROLL_WORDS_FR : ROLL_WORDS_PER_WAVE;
+    // FR: + the CPython cell hashes (shared by the block) for the frontier tables
+    __shared__ uint32_t lds[AREA * (BLOCK / WAVE) + (FR ? 2 * BK_CELLS : 0)];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint32_t* my = lds + wv * ROLL_WORDS_PER_WAVE;
-    uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * ROLL_WORDS_PER_WAVE) + lane;  // + R * WAVE
+    uint32_t* my = lds + wv * AREA;
+    uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * AREA) + lane;  // + R * WAVE
+    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLOCK / WAVE));
+    if constexpr (FR) {
+        for (int i = threadIdx.x; i < BK_CELLS; i += BLOCK) htab[i] = kCellHash[i];
+        __syncthreads();
+    }
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
@@ -1057,7 +1064,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             if (g.pid < 0) {
                 const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
                 if (next >= a.n_playouts) { done = true; break; }
-                start_game<FR>(a, g, slab, slot, next);
+                start_game<FR>(a, g, slab, slot, next, htab);
             }
             if (arena) {
 #pragma unroll 1
@@ -1156,11 +1163,50 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             FsLane* fl = &a.fslab[slot];
             const uint32_t* occ_rows = slab.base + 4 * 20;
             const uint32_t* own_rows = slab.base + p * 20;
-            if (!fs_place(fs_ref(&fl->s, p), fl->tmp, cells, n,
-                          [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; },
-                          [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; })) {
-                g.status |= 2u;
+            auto occ = [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; };
+            auto own = [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; };
+            bk_fset* gfs = &fl->s;
+            const uint32_t gmask = gfs->mask[p];
+            bool ok = false, staged = false;
+            if (gmask < 128u) {
+                // stage the mover's table in LDS ([slot][lane]): the probe chains of the
+                // ~45 add/discard ops then wait on LDS instead of L2
+                int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + lane;
+                const uint4* src4 = reinterpret_cast<const uint4*>(gfs->key[p]);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if ((uint32_t)(8 * i) <= gmask) {
+                        const uint4 v = src4[i];
+                        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            lk[(8 * i + 2 * j) * WAVE] = (int16_t)(w[j] & 0xFFFFu);
+                            lk[(8 * i + 2 * j + 1) * WAVE] = (int16_t)(w[j] >> 16);
+                        }
+                    }
+                }
+                uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
+                FsetRef t{lk, WAVE, &m, &f, &u, 128u, htab};
+                if (fs_place(t, fl->tmp, cells, n, occ, own)) {
+                    staged = ok = true;
+                    uint4* dst4 = reinterpret_cast<uint4*>(gfs->key[p]);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        if ((uint32_t)(8 * i) <= m) {
+                            uint32_t w[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j)
+                                w[j] = (uint16_t)lk[(8 * i + 2 * j) * WAVE] |
+                                       ((uint32_t)(uint16_t)lk[(8 * i + 2 * j + 1) * WAVE] << 16);
+                            dst4[i] = make_uint4(w[0], w[1], w[2], w[3]);
+                        }
+                    }
+                    gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+                }
             }
+            // tables of 256 slots (or a move that grows one past 128): in place in HBM
+            if (!staged) ok = fs_place(fs_ref(gfs, p, htab), fl->tmp, cells, n, occ, own);
+            if (!ok) g.status |= 2u;
         }
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
         g.used.set(p, g.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
@@ -1691,7 +1737,7 @@ int bk_fset_init(bk_fset* s) {
     if (!s) return BK_EINVAL;
     memset(s, 0, sizeof *s);
     for (int p = 0; p < 4; ++p) {
-        FsetRef t = fs_ref(s, p);
+        FsetRef t = fs_ref(s, p, kCellHashHost);
         fs_clear(t);
         int16_t tmp[BK_FSET_SLOTS];
         fs_add(t, tmp, (int16_t)kCornerCell[p]);  // init_frontier_for_player :385-405
@@ -1708,7 +1754,7 @@ int bk_fset_place(bk_fset* s, const bk_state* after, int32_t player, const int32
         return ((after->planes[q][b >> 6] >> (b & 63)) & 1ull) != 0ull;
     };
     int16_t tmp[BK_FSET_SLOTS];
-    const bool ok = fs_place(fs_ref(s, player), tmp, cells, n,
+    const bool ok = fs_place(fs_ref(s, player, kCellHashHost), tmp, cells, n,
                              [&](int r, int c) { return bit(0, r, c) || bit(1, r, c) || bit(2, r, c) || bit(3, r, c); },
                              [&](int r, int c) { return bit(player, r, c); });
     return ok ? BK_OK : BK_EOVERFLOW;
@@ -1719,7 +1765,7 @@ int bk_fset_copy(bk_fset* dst, const bk_fset* src) {
     if (dst == src) return BK_OK;
     for (int p = 0; p < 4; ++p) {
         if (src->mask[p] + 1u > BK_FSET_SLOTS) return BK_EINVAL;
-        fs_copy(fs_ref(dst, p), src->key[p], src->mask[p], src->fill[p], src->used[p]);
+        fs_copy(fs_ref(dst, p, kCellHashHost), src->key[p], src->mask[p], src->fill[p], src->used[p]);
     }
     return BK_OK;
 }

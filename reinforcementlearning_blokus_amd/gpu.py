@@ -123,7 +123,7 @@ class BlokusGPU:
     # ------------------------------------------------------------------ frontier order
     def rollout_frontier(self, roots, root_sets, n_playouts: int, *, semantics: int = N.SEM_ARENA,
                          rng: int = N.RNG_NUMPY_MT, seed: int = 0, max_plies: int | None = None,
-                         compat_seeds=None, root_index=None, seats_share_stream: bool = False):
+                         compat_seeds=None, root_index=None, seats_share_stream: bool = False, out=None):
         """Playouts in the reference's FRONTIER list order (bk_rollout_frontier): with the
         numpy-MT compat stream these are the reference's default-config games.
         root_sets: FSET_DTYPE records (one per root).  Host numpy in/out."""
@@ -131,6 +131,17 @@ class BlokusGPU:
             max_plies = 2500 if semantics == N.SEM_ARENA else 50
         cfg = N.BkRolloutCfg(semantics, N.ORDER_FRONTIER, rng, max_plies, seed & (2**64 - 1),
                              int(seats_share_stream), 0)
+        if _is_torch(roots):  # device tensors: roots uint8 [n,256], root_sets uint8 [n,2080]
+            import torch
+            assert semantics != N.SEM_ADVANCE, "device path: playout results only"
+            if out is None:
+                out = torch.empty((n_playouts, 32), dtype=torch.uint8, device=roots.device)
+            self._stream_from_torch()
+            self.handle.rollout_frontier(roots.data_ptr(), root_sets.data_ptr(), roots.shape[0],
+                                         root_index.data_ptr() if root_index is not None else 0, n_playouts, cfg,
+                                         compat_seeds.data_ptr() if compat_seeds is not None else 0,
+                                         out.data_ptr(), 0, 0, N.MEM_DEVICE)
+            return out
         st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
         fs = np.ascontiguousarray(root_sets, dtype=N.FSET_DTYPE)
         assert fs.shape[0] == st.shape[0]
