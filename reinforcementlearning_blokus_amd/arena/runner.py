@@ -1,0 +1,362 @@
+"""Arena game loop and experiment writer (reference: analytics/tournament/arena_runner.py).
+
+``run_games_gpu`` is the batched path for all-random seatings: every game is one lane of
+the frontier-order playout kernel, started from the empty board with each seat's
+RandomAgent seed (``_agent_seed``), so its record equals ``run_single_game``'s for the
+same run seed and game index.  ``run_single_game`` is the reference loop itself
+(:578-777) over the GPU-backed ``BlokusGame`` for every other seating.
+"""
+from __future__ import annotations
+
+import json
+import random
+import time
+import traceback
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ..agents.fast_mcts_agent import FastMCTSAgent
+from ..agents.gameplay_fast_mcts import GameplayFastMCTSAgent
+from ..agents.random_agent import RandomAgent
+from ..engine.board import Player
+from ..engine.game import BlokusGame
+from ..mcts.mcts_agent import MCTSAgent
+from .config import (AgentConfig, RunConfig, agent_seed, game_seed_from_run_seed, seat_assignment_for_game)
+from .stats import compute_summary
+
+# ---------------------------------------------------------------------------- agents
+
+
+class _SelectActionAdapter:
+    def __init__(self, agent: Any):
+        self.agent = agent
+
+    def choose_move(self, board, player, legal_moves, thinking_time_ms):
+        start = time.perf_counter()
+        move = self.agent.select_action(board, player, legal_moves)
+        stats: Dict[str, Any] = {"timeSpentMs": (time.perf_counter() - start) * 1000.0}
+        if isinstance(self.agent, MCTSAgent):
+            info = self.agent.get_action_info().get("stats", {})
+            if info.get("iterations_run") is not None:
+                stats["iterations_run"] = info["iterations_run"]
+            if info.get("time_elapsed") is not None:
+                stats["timeSpentMs"] = float(info["time_elapsed"]) * 1000.0
+        return move, stats
+
+
+class _FastMCTSAdapter:
+    """deterministic_time_budget: iterations = round(iterations_per_ms * budget) (:333-371)."""
+
+    def __init__(self, agent: FastMCTSAgent, *, deterministic_time_budget: bool, iterations_per_ms: float):
+        self.agent = agent
+        self.deterministic_time_budget = deterministic_time_budget
+        self.iterations_per_ms = iterations_per_ms
+
+    def choose_move(self, board, player, legal_moves, thinking_time_ms):
+        budget = int(thinking_time_ms or max(int(self.agent.time_limit * 1000), 1))
+        if self.deterministic_time_budget:
+            cap = max(1, int(round(self.iterations_per_ms * budget)))
+            orig, self.agent.iterations = self.agent.iterations, cap
+            try:
+                res = self.agent.think(board, player, legal_moves, max(10_000_000, budget))
+            finally:
+                self.agent.iterations = orig
+            stats = dict(res.get("stats") or {})
+            stats["timeBudgetMs"], stats["iterationCap"] = budget, cap
+            return res.get("move"), stats
+        res = self.agent.think(board, player, legal_moves, budget)
+        return res.get("move"), dict(res.get("stats") or {})
+
+
+class _GameplayFastMCTSAdapter:
+    def __init__(self, agent: GameplayFastMCTSAgent, *, deterministic_time_budget: bool, iterations_per_ms: float):
+        self.agent = agent
+        self.deterministic_time_budget = deterministic_time_budget
+        self.iterations_per_ms = iterations_per_ms
+
+    def choose_move(self, board, player, legal_moves, thinking_time_ms):
+        budget = int(thinking_time_ms or 1)
+        if self.deterministic_time_budget:
+            cap = max(1, int(round(self.iterations_per_ms * budget)))
+            orig, self.agent._agent.iterations = self.agent._agent.iterations, cap
+            try:
+                move, stats = self.agent.choose_move(board, player, legal_moves, max(10_000_000, budget))
+            finally:
+                self.agent._agent.iterations = orig
+            stats = dict(stats or {})
+            stats["timeBudgetMs"], stats["iterationCap"] = budget, cap
+            return move, stats
+        move, stats = self.agent.choose_move(board, player, legal_moves, budget)
+        return move, dict(stats or {})
+
+
+def build_agent(config: AgentConfig, seed: int):
+    """Agent adapter from configuration (:415-492).  ``heuristic`` seats (and MCTS with
+    the heuristic rollout policy / learned evaluation) are not ported:
+    an ``mcts`` seat here rolls out uniformly at random on the GPU."""
+    kind = config.type.lower()
+    params = dict(config.params)
+    if kind == "random":
+        return _SelectActionAdapter(RandomAgent(seed=seed))
+    if kind == "mcts":
+        deterministic = bool(params.get("deterministic_time_budget", True))
+        iterations = int(params.get("iterations", 1000))
+        time_limit = params.get("time_limit")
+        if deterministic and config.thinking_time_ms is not None:
+            iterations = max(1, int(round(float(params.get("iterations_per_ms", 10.0)) * config.thinking_time_ms)))
+            time_limit = None
+        elif time_limit is None and config.thinking_time_ms is not None:
+            time_limit = float(config.thinking_time_ms) / 1000.0
+        return _SelectActionAdapter(MCTSAgent(
+            iterations=iterations, time_limit=float(time_limit) if time_limit is not None else None,
+            exploration_constant=float(params.get("exploration_constant", 1.414)),
+            use_transposition_table=bool(params.get("use_transposition_table", True)), seed=seed,
+            learned_model_path=params.get("learned_model_path"),
+            leaf_evaluation_enabled=bool(params.get("leaf_evaluation_enabled", False)),
+            progressive_bias_enabled=bool(params.get("progressive_bias_enabled", False)),
+            potential_shaping_enabled=bool(params.get("potential_shaping_enabled", False)),
+            max_rollout_moves=int(params.get("max_rollout_moves", 50))))
+    if kind == "fast_mcts":
+        default_time = (float(config.thinking_time_ms) / 1000.0 if config.thinking_time_ms is not None
+                        else float(params.get("time_limit", 0.1)))
+        agent = FastMCTSAgent(iterations=int(params.get("iterations", 5000)), time_limit=default_time,
+                              exploration_constant=float(params.get("exploration_constant", 1.414)), seed=seed)
+        return _FastMCTSAdapter(agent, deterministic_time_budget=bool(params.get("deterministic_time_budget", True)),
+                                iterations_per_ms=float(params.get("iterations_per_ms", 20.0)))
+    if kind in {"gameplay_fast_mcts", "gameplay_mcts"}:
+        agent = GameplayFastMCTSAgent(iterations=int(params.get("iterations", 5000)),
+                                      exploration_constant=float(params.get("exploration_constant", 1.414)), seed=seed)
+        return _GameplayFastMCTSAdapter(agent,
+                                        deterministic_time_budget=bool(params.get("deterministic_time_budget", True)),
+                                        iterations_per_ms=float(params.get("iterations_per_ms", 20.0)))
+    raise ValueError(f"Unsupported agent type: {config.type}")
+
+
+# ---------------------------------------------------------------------------- records
+
+
+def _compute_ranks(scores: Mapping[str, int]) -> Dict[str, int]:
+    order = sorted(set(scores.values()), reverse=True)
+    rank = {s: i + 1 for i, s in enumerate(order)}
+    return {pid: rank[s] for pid, s in scores.items()}
+
+
+def _extract_move_telemetry(raw: Mapping[str, Any], fallback_ms: float) -> Tuple[float, Optional[float]]:
+    t = raw.get("timeSpentMs")
+    if t is None and raw.get("time_elapsed") is not None:
+        t = float(raw["time_elapsed"]) * 1000.0
+    if t is None:
+        t = fallback_ms
+    sims = None
+    for key in ("nodesEvaluated", "iterations_run", "simulations", "rollouts"):
+        if raw.get(key) is not None:
+            try:
+                sims = float(raw[key])
+                break
+            except (TypeError, ValueError):
+                continue
+    return float(t), sims
+
+
+def _finish_stats(per_agent: Dict[str, Dict[str, Any]]) -> None:
+    for e in per_agent.values():
+        moves = e["moves"]
+        e["avg_time_ms"] = e["total_time_ms"] / moves if moves > 0 else 0.0
+        if e["moves_with_simulations"] > 0:
+            e["avg_simulations_per_move"] = e["total_simulations"] / e["moves_with_simulations"]
+            ts = e["total_time_ms"] / 1000.0
+            e["simulations_per_second"] = e["total_simulations"] / ts if ts > 0 else None
+        else:
+            e["avg_simulations_per_move"] = None
+            e["simulations_per_second"] = None
+            e["total_simulations"] = None
+
+
+def _record(*, run_id, game_index, game_seed, run_config, seats, scores, winner_ids, is_tie, moves_made,
+            turn_count, passes, invalid, duration, truncated, per_agent, error) -> Dict[str, Any]:
+    scores = {str(k): int(v) for k, v in scores.items()}
+    ranks = _compute_ranks(scores)
+    return {
+        "run_id": run_id, "game_id": f"{run_id}_g{game_index:04d}", "game_index": game_index,
+        "game_seed": game_seed, "seat_assignment": dict(seats), "seat_policy": run_config.seat_policy,
+        "winner_ids": winner_ids, "winner_agents": [seats[str(p)] for p in winner_ids], "is_tie": bool(is_tie),
+        "final_scores": scores, "final_ranks": ranks, "agent_scores": {seats[p]: s for p, s in scores.items()},
+        "agent_ranks": {seats[p]: r for p, r in ranks.items()},
+        "winner_id": winner_ids[0] if len(winner_ids) == 1 else None, "moves_made": int(moves_made),
+        "turn_count": int(turn_count), "passes": int(passes), "invalid_actions": int(invalid),
+        "duration_sec": float(duration), "truncated": bool(truncated), "agent_move_stats": per_agent,
+        "snapshot_checkpoints_hit": [], "error": error,
+    }
+
+
+def run_single_game(*, run_id: str, game_index: int, game_seed: int, run_config: RunConfig,
+                    seat_assignment: Mapping[str, str], agent_configs: Mapping[str, AgentConfig]) -> Dict[str, Any]:
+    """The reference loop (:652-697): pass when stuck, validate every move, game over when
+    nobody can move, max_turns truncation."""
+    random.seed(game_seed)
+    np.random.seed(game_seed)
+    start = time.perf_counter()
+    agents = {n: build_agent(agent_configs[n], seed=agent_seed(run_config.seed, game_index, n))
+              for n in set(seat_assignment.values())}
+    per_agent = {n: {"moves": 0.0, "total_time_ms": 0.0, "total_simulations": 0.0, "moves_with_simulations": 0.0,
+                     "move_times_ms": []} for n in set(seat_assignment.values())}
+    game = BlokusGame()
+    passes = invalid = turns = 0
+    truncated, error = False, None
+    try:
+        while not game.is_game_over() and turns < run_config.max_turns:
+            cur = game.get_current_player()
+            name = seat_assignment[str(cur.value)]
+            legal = game.get_legal_moves(cur)
+            turns += 1
+            if not legal:
+                passes += 1
+                game.board._update_current_player()
+                game._check_game_over()
+                continue
+            t0 = time.perf_counter()
+            move, raw = agents[name].choose_move(game.board, cur, legal, agent_configs[name].thinking_time_ms)
+            elapsed, sims = _extract_move_telemetry(raw, (time.perf_counter() - t0) * 1000.0)
+            e = per_agent[name]
+            e["moves"] += 1
+            e["total_time_ms"] += elapsed
+            e["move_times_ms"].append(elapsed)
+            if sims is not None:
+                e["total_simulations"] += sims
+                e["moves_with_simulations"] += 1
+            if move is None or not game.make_move(move, cur):
+                invalid += move is not None
+                passes += 1
+                game.board._update_current_player()
+                game._check_game_over()
+    except Exception:  # noqa: BLE001 - recorded like the reference
+        error = traceback.format_exc()
+    if turns >= run_config.max_turns and not game.is_game_over():
+        truncated = True
+        game.board.game_over = True
+    res = game.get_game_result()
+    _finish_stats(per_agent)
+    return _record(run_id=run_id, game_index=game_index, game_seed=game_seed, run_config=run_config,
+                   seats=seat_assignment, scores=res.scores, winner_ids=[int(w) for w in res.winner_ids],
+                   is_tie=res.is_tie, moves_made=game.board.move_count, turn_count=turns, passes=passes,
+                   invalid=invalid, duration=time.perf_counter() - start, truncated=truncated,
+                   per_agent=per_agent, error=error)
+
+
+def _all_random(run_config: RunConfig) -> bool:
+    return all(a.type.lower() == "random" for a in run_config.agents)
+
+
+def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
+                  device: int = 0) -> List[Dict[str, Any]]:
+    """All-random seatings: the games ``game_indices`` in one frontier-order playout launch.
+    Per-move times are not observable inside the kernel; each game's duration is its
+    share of the launch and per-agent time is split by moves made."""
+    from .. import _native as N
+    from ..gpu import BlokusGPU, empty_state
+    if not _all_random(run_config):
+        raise ValueError("run_games_gpu plays all-random seatings; use run_single_game")
+    idx = list(game_indices)
+    n = len(idx)
+    if n == 0:
+        return []
+    seats, seeds, gseeds = [], np.zeros((n, 4), dtype=np.uint32), []
+    for i, gi in enumerate(idx):
+        gs = game_seed_from_run_seed(run_config.seed, gi)
+        st = seat_assignment_for_game(run_config.agent_names, gi, gs, run_config.seat_policy)
+        gseeds.append(gs)
+        seats.append(st)
+        seeds[i] = [agent_seed(run_config.seed, gi, st[str(p + 1)]) for p in range(4)]
+    gpu = BlokusGPU(device)
+    t0 = time.perf_counter()
+    states, _sets, res = gpu.rollout_frontier(empty_state(), N.fset_new(1), n, semantics=N.SEM_ADVANCE,
+                                              rng=N.RNG_NUMPY_MT, compat_seeds=seeds,
+                                              max_plies=run_config.max_turns,
+                                              root_index=np.zeros(n, dtype=np.int32), with_results=True)
+    dt = time.perf_counter() - t0
+    out = []
+    for i, gi in enumerate(idx):
+        r = res[i]
+        if int(r["status"]) != 0:
+            raise RuntimeError(f"game {gi}: kernel status {int(r['status'])} (stream/table overflow)")
+        scores = {p + 1: int(r["scores"][p]) for p in range(4)}
+        best = max(scores.values())
+        winners = [p for p, s in scores.items() if s == best]
+        moves = [bin(int(u)).count("1") for u in states[i]["used"]]
+        per_agent = {}
+        for p in range(4):
+            name = seats[i][str(p + 1)]
+            share = dt / n * (moves[p] / max(sum(moves), 1)) * 1000.0
+            per_agent[name] = {"moves": float(moves[p]), "total_time_ms": share,
+                               "total_simulations": 0.0, "moves_with_simulations": 0.0, "move_times_ms": []}
+        _finish_stats(per_agent)
+        turns = int(r["turns"])
+        out.append(_record(run_id=run_id, game_index=gi, game_seed=gseeds[i], run_config=run_config,
+                           seats=seats[i], scores=scores, winner_ids=winners, is_tie=len(winners) > 1,
+                           moves_made=int(states[i]["move_count"]), turn_count=turns, passes=int(r["passes"]),
+                           invalid=0, duration=dt / n, truncated=turns >= run_config.max_turns,
+                           per_agent=per_agent, error=None))
+    return out
+
+
+def _write_json(path: Path, payload: Mapping[str, Any]) -> None:
+    with path.open("w", encoding="utf-8") as fh:
+        json.dump(payload, fh, indent=2, sort_keys=True)
+        fh.write("\n")
+
+
+def run_experiment(run_config: RunConfig, *, verbose: bool = False, device: int = 0, rank: int = 0,
+                   world: int = 1, dist=None) -> Dict[str, Any]:
+    """run_config.json + games.jsonl + summary.json (:914-996).  With ``world`` > 1 each
+    rank plays games index == rank (mod world) on its GPU and rank 0 gathers the records
+    and writes the run (one gather of JSON records, games are independent)."""
+    from ..shard import shard_indices
+    mine = shard_indices(run_config.num_games, rank, world).tolist()
+    if _all_random(run_config):
+        records = run_games_gpu(run_config, mine, run_id="pending", device=device)
+    else:
+        agent_configs = {a.name: a for a in run_config.agents}
+        records = []
+        for gi in mine:
+            gs = game_seed_from_run_seed(run_config.seed, gi)
+            seats = seat_assignment_for_game(run_config.agent_names, gi, gs, run_config.seat_policy)
+            records.append(run_single_game(run_id="pending", game_index=gi, game_seed=gs, run_config=run_config,
+                                           seat_assignment=seats, agent_configs=agent_configs))
+            if verbose:
+                print(f"[{gi + 1}/{run_config.num_games}] seed={gs} winners={records[-1]['winner_agents']}")
+    if world > 1:
+        gathered: List[Any] = [None] * world
+        dist.all_gather_object(gathered, records)
+        records = [r for part in gathered for r in part]
+    records.sort(key=lambda r: r["game_index"])
+    if rank != 0:
+        return {"run_id": None, "games": len(records)}
+    root = Path(run_config.output_root)
+    root.mkdir(parents=True, exist_ok=True)
+    stamp = datetime.now().strftime("%Y%m%d_%H%M%S")
+    import hashlib
+    run_id = f"{stamp}_{hashlib.sha256(json.dumps(run_config.to_dict(), sort_keys=True).encode()).hexdigest()[:8]}"
+    run_dir = root / run_id
+    k = 1
+    while run_dir.exists():
+        run_dir = root / f"{run_id}_{k:02d}"
+        k += 1
+    run_id = run_dir.name
+    run_dir.mkdir(parents=True)
+    payload = run_config.to_dict()
+    payload.update(run_id=run_id, created_at=datetime.now().isoformat(timespec="seconds"))
+    _write_json(run_dir / "run_config.json", payload)
+    with (run_dir / "games.jsonl").open("w", encoding="utf-8") as fh:
+        for r in records:
+            r["run_id"] = run_id
+            r["game_id"] = f"{run_id}_g{r['game_index']:04d}"
+            fh.write(json.dumps(r, sort_keys=True) + "\n")
+    summary = compute_summary(records, run_id=run_id, run_seed=run_config.seed, seat_policy=run_config.seat_policy,
+                              agent_names=run_config.agent_names,
+                              thinking_time_ms_by_agent={a.name: a.thinking_time_ms for a in run_config.agents},
+                              run_config=payload)
+    _write_json(run_dir / "summary.json", summary)
+    return {"run_id": run_id, "run_dir": str(run_dir), "summary": summary}

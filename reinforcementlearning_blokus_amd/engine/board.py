@@ -8,7 +8,10 @@ engine/board.py:315-367), so CPython lays the sets out identically and
 ``list(board.get_frontier(p))`` reproduces the reference order.
 
 GPU work never reads this object directly: ``pack_state`` flattens it into the
-256-byte ``bk_state`` record of include/blokus_hip.h.
+256-byte ``bk_state`` record of include/blokus_hip.h, and ``frontier_tables`` carries
+the same frontier sets as the library's restatement of CPython's hash tables (bk_fset,
+kept in step with every place_piece / copy) for GPU playouts in the reference's
+frontier order (``pack_fsets``).
 """
 from __future__ import annotations
 
@@ -176,6 +179,8 @@ class Board:
             self.player_frontiers[p].clear()
         for p in Player:
             self.init_frontier_for_player(p)
+        from .._native import fset_new
+        self.frontier_tables = fset_new(1)
 
     def init_frontier_for_player(self, player: Player) -> None:
         corner = self.player_start_corners[player]
@@ -217,6 +222,8 @@ class Board:
         self.player_pieces_used[player].add(piece_id)
         self.player_first_move[player] = False
         self.update_frontier_after_move(player, cells)
+        from .._native import fset_place
+        fset_place(self.frontier_tables, _planes_record(self), player.value - 1, [r * 20 + c for r, c in cells])
         self.move_count += 1
         self._update_current_player()
         return True
@@ -260,6 +267,9 @@ class Board:
         b.move_count = self.move_count
         b.player_start_corners = self.player_start_corners
         b.player_frontiers = {k: v.copy() for k, v in self.player_frontiers.items()}
+        from .._native import FSET_DTYPE, fset_copy
+        b.frontier_tables = np.zeros(1, dtype=FSET_DTYPE)
+        fset_copy(b.frontier_tables, self.frontier_tables)  # set.copy() re-lays out
         b.occupied_bits = self.occupied_bits
         b.player_bits = self.player_bits.copy()
         return b
@@ -283,6 +293,24 @@ def pack_state(board: Board, out=None):
     rec["out_mask"] = 0
     rec["move_count"] = board.move_count
     return rec
+
+
+def _planes_record(board: Board) -> np.ndarray:
+    """bk_state with only the planes filled (what bk_fset_place reads)."""
+    from .._native import STATE_DTYPE
+    rec = np.zeros(1, dtype=STATE_DTYPE)
+    for i, p in enumerate(_PLAYERS):
+        rec["planes"][0, i] = np.frombuffer(int(board.player_bits[p]).to_bytes(56, "little"), dtype="<u8")
+    return rec
+
+
+def pack_fsets(boards) -> np.ndarray:
+    """The boards' frontier tables (FSET_DTYPE), for bk_rollout_frontier."""
+    from .._native import FSET_DTYPE
+    out = np.zeros(len(boards), dtype=FSET_DTYPE)
+    for i, b in enumerate(boards):
+        out[i] = b.frontier_tables[0]
+    return out
 
 
 def pack_states(boards) -> np.ndarray:

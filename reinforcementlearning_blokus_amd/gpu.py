@@ -123,7 +123,8 @@ class BlokusGPU:
     # ------------------------------------------------------------------ frontier order
     def rollout_frontier(self, roots, root_sets, n_playouts: int, *, semantics: int = N.SEM_ARENA,
                          rng: int = N.RNG_NUMPY_MT, seed: int = 0, max_plies: int | None = None,
-                         compat_seeds=None, root_index=None, seats_share_stream: bool = False, out=None):
+                         compat_seeds=None, root_index=None, seats_share_stream: bool = False, out=None,
+                         with_results: bool = False):
         """Playouts in the reference's FRONTIER list order (bk_rollout_frontier): with the
         numpy-MT compat stream these are the reference's default-config games.
         root_sets: FSET_DTYPE records (one per root).  Host numpy in/out."""
@@ -150,14 +151,16 @@ class BlokusGPU:
         if seeds is not None:
             assert seeds.shape[0] >= n_playouts
         self.handle.set_stream(None)
-        if semantics == N.SEM_ADVANCE:
+        if semantics == N.SEM_ADVANCE:  # (states, tables[, results])
             out_st = np.zeros(n_playouts, dtype=STATE_DTYPE)
             out_fs = np.zeros(n_playouts, dtype=N.FSET_DTYPE)
+            res = np.zeros(n_playouts, dtype=RESULT_DTYPE) if with_results else None
             self.handle.rollout_frontier(st.ctypes.data, fs.ctypes.data, st.shape[0],
                                          idx.ctypes.data if idx is not None else 0, n_playouts, cfg,
-                                         seeds.ctypes.data if seeds is not None else 0, 0, out_st.ctypes.data,
+                                         seeds.ctypes.data if seeds is not None else 0,
+                                         res.ctypes.data if res is not None else 0, out_st.ctypes.data,
                                          out_fs.ctypes.data, N.MEM_HOST)
-            return out_st, out_fs
+            return (out_st, out_fs, res) if with_results else (out_st, out_fs)
         res = np.zeros(n_playouts, dtype=RESULT_DTYPE)
         self.handle.rollout_frontier(st.ctypes.data, fs.ctypes.data, st.shape[0],
                                      idx.ctypes.data if idx is not None else 0, n_playouts, cfg,

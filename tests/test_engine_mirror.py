@@ -115,3 +115,17 @@ def test_fset_copy_matches_cpython_set_copy():
             s = b.get_frontier(Player(p + 1))
             assert N.fset_list(dst, p) == [r * 20 + c for r, c in s.copy()]
             assert N.fset_list(dst2, p) == [r * 20 + c for r, c in s.copy().copy()]
+
+
+@pytest.mark.parametrize("i", range(0, len(POS), 3))
+def test_board_mirror_carries_frontier_tables(i):
+    """Board.frontier_tables tracks place_piece and copy(): its iteration order equals
+    the live Python sets' (and so the reference's)."""
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.engine.board import pack_fsets
+    b = engine_board(POS[i])
+    c = b.copy().copy()
+    for p in range(4):
+        assert N.fset_list(b.frontier_tables, p) == [r * 20 + cc for r, cc in b.get_frontier(Player(p + 1))]
+        assert N.fset_list(c.frontier_tables, p) == [r * 20 + cc for r, cc in c.get_frontier(Player(p + 1))]
+    assert pack_fsets([b, c]).shape == (2,)

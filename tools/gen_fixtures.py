@@ -279,6 +279,50 @@ def gen_arena():
     return out
 
 
+ARENA_RUN = {"agents": [{"name": f"r{i}", "type": "random"} for i in range(4)], "num_games": 16,
+             "seed": 424242, "seat_policy": "randomized", "output_root": "/tmp/arena_fx2"}
+
+
+def gen_arena_game(gi):
+    _setup()
+    from analytics.tournament.arena_runner import (RunConfig, _seat_assignment_for_game, game_seed_from_run_seed,
+                                                   run_single_game)
+    cfg = RunConfig.from_dict(ARENA_RUN)
+    gs = game_seed_from_run_seed(cfg.seed, gi)
+    seats = _seat_assignment_for_game([a.name for a in cfg.agents], gi, gs, cfg.seat_policy)
+    rec, _ = run_single_game(run_id="fx2", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                             agent_configs={a.name: a for a in cfg.agents})
+    return rec
+
+
+def gen_arena_runs():
+    """16 run_single_game records (randomized seats) + the reference's compute_summary
+    over deterministic copies of them (timings replaced by fixed values)."""
+    _setup()
+    from analytics.tournament.arena_stats import compute_summary
+    with Pool(8) as pool:
+        recs = pool.map(gen_arena_game, range(ARENA_RUN["num_games"]))
+    keep = ("game_index", "game_seed", "seat_assignment", "winner_ids", "winner_agents", "winner_id", "is_tie",
+            "final_scores", "final_ranks", "agent_scores", "agent_ranks", "moves_made", "turn_count", "passes",
+            "invalid_actions", "truncated")
+    games = [{k: r[k] for k in keep} for r in recs]
+    synth = []
+    for r in recs:
+        d = dict(r)
+        d["duration_sec"] = 0.5 + 0.01 * r["game_index"]
+        d["agent_move_stats"] = {n: {"moves": st["moves"], "total_time_ms": 1.5 * st["moves"],
+                                     "total_simulations": None, "moves_with_simulations": 0.0,
+                                     "move_times_ms": [1.5] * int(st["moves"])}
+                                 for n, st in r["agent_move_stats"].items()}
+        d["error"] = None
+        synth.append(d)
+    summary = compute_summary(synth, run_id="fx2", run_seed=ARENA_RUN["seed"], seat_policy="randomized",
+                              agent_names=[a["name"] for a in ARENA_RUN["agents"]],
+                              thinking_time_ms_by_agent={a["name"]: None for a in ARENA_RUN["agents"]},
+                              run_config=ARENA_RUN)
+    return {"config": ARENA_RUN, "games": games, "summary_input": synth, "summary": summary}
+
+
 def dump(name, obj):
     path = os.path.join(OUT, name)
     with open(path, "w") as f:
@@ -339,6 +383,8 @@ def main():
         dump("zobrist.json", gen_zobrist())
     if what in ("all", "arena"):
         dump("arena_small.json", gen_arena())
+    if what in ("all", "arena_runs"):
+        dump("arena_runs.json", gen_arena_runs())
 
 
 if __name__ == "__main__":
