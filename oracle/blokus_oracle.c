@@ -767,3 +767,161 @@ int or_batch_playouts(const bk_state* roots, int n_roots, int n_playouts, uint64
     free(th); free(jobs);
     return 0;
 }
+
+/* ---------------------------------------------------------------------------------
+ * MCTSAgent (mcts/mcts_agent.py) with RandomAgent rollouts, restated node by node:
+ *   MCTSNode :19-191 (board = copy; untried = get_legal_moves at creation; expand pops
+ *   the LAST untried move, plays it on board.copy() and wraps it in a new node, which
+ *   copies again), select_action :304-341, _mcts_iteration :360-382, _selection
+ *   :384-406 (UCB1 with np.log / np.sqrt; max keeps the first best), _simulation
+ *   :408-437 (Zobrist TT lookup, hit = cached reward), _rollout :470-554 on
+ *   board.copy() (<= max_rollout_moves plies, stop at the first player without a
+ *   move, reward = final - initial get_score of the node's player), _backpropagation
+ *   :572-582.  The TT (mcts/zobrist.py:155-220) is an open-addressing table here:
+ *   empty slot = NaN value; membership semantics are the dict's.
+ * --------------------------------------------------------------------------------- */
+typedef struct {
+    or_board board;
+    int32_t player, move, parent, child0, nchild, visits;
+    double total;
+    int32_t* untried;
+    int32_t n_untried;
+} or_mnode;
+
+static int tt_find(const uint64_t* keys, const double* vals, int cap, uint64_t h, int* slot) {
+    int i = (int)(h & (uint64_t)(cap - 1));
+    while (!isnan(vals[i])) {
+        if (keys[i] == h) { *slot = i; return 1; }
+        i = (i + 1) & (cap - 1);
+    }
+    *slot = i;
+    return 0;
+}
+
+static double or_rollout_mt(const or_board* b, int player, or_mt* rng, int max_moves, int32_t* scratch) {
+    or_board* sim = (or_board*)malloc(sizeof(or_board));
+    or_board_copy(sim, b);
+    int initial = or_board_score(sim, player), made = 0, cur = player;
+    while (made < max_moves) {
+        int n = or_legal_moves(sim, cur, BK_ORDER_FRONTIER, scratch, BK_ORIENTS * 400);
+        if (n == 0) break;
+        or_place_move(sim, cur, scratch[or_np_randint(rng, n)]);
+        cur = (cur + 1) & 3;
+        ++made;
+    }
+    double r = (double)(or_board_score(sim, player) - initial);
+    free(sim);
+    return r;
+}
+
+int or_mcts(const or_board* board, int player, int iterations, double c, int max_rollout,
+            const double* log_table, int log_len, const uint64_t* ztab, or_mt* rng, int use_tt,
+            uint64_t* tt_keys, double* tt_vals, int tt_cap, int32_t* tt_count,
+            int32_t* best_move, int32_t* hits, double* rewards, uint8_t* hit_flags,
+            int32_t* child_moves, int32_t* child_visits, double* child_totals, int child_cap,
+            int32_t* n_children) {
+    int32_t* scratch = (int32_t*)malloc(sizeof(int32_t) * BK_ORIENTS * 400);
+    or_mnode* nodes = (or_mnode*)malloc(sizeof(or_mnode) * (size_t)(iterations + 1));
+    int nn = 0, rc = 0;
+    int32_t** ch = (int32_t**)calloc((size_t)(iterations + 1), sizeof(int32_t*));  /* children */
+#define NEW_NODE(B, PL, MV, PAR) do {                                                   \
+        or_mnode* nz_ = &nodes[nn];                                                      \
+        or_board_copy(&nz_->board, (B));                                                 \
+        nz_->player = (PL); nz_->move = (MV); nz_->parent = (PAR); nz_->child0 = -1;           \
+        nz_->nchild = 0; nz_->visits = 0; nz_->total = 0.0;                                  \
+        int cnt = or_legal_moves(&nz_->board, nz_->player, BK_ORDER_FRONTIER, scratch,     \
+                                 BK_ORIENTS * 400);                                    \
+        nz_->untried = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt > 0 ? cnt : 1));  \
+        memcpy(nz_->untried, scratch, sizeof(int32_t) * (size_t)cnt);                    \
+        nz_->n_untried = cnt;                                                            \
+        ch[nn] = (int32_t*)malloc(sizeof(int32_t) * (size_t)(cnt > 0 ? cnt : 1));      \
+        ++nn;                                                                          \
+    } while (0)
+    NEW_NODE(board, player, -1, -1);
+    int nhits = 0;
+    for (int it = 0; it < iterations; ++it) {
+        int u = 0;
+        /* _selection */
+        while (!(nodes[u].n_untried == 0 && nodes[u].nchild == 0)) {
+            if (nodes[u].n_untried > 0) break;
+            const or_mnode* par = &nodes[u];
+            if (par->visits >= log_len) { rc = -2; goto done; }
+            const double lg = log_table[par->visits];
+            int best = -1;
+            double bv = 0.0;
+            for (int k = 0; k < par->nchild; ++k) {
+                const or_mnode* z = &nodes[ch[u][k]];
+                double v;
+                if (z->visits == 0) {
+                    v = INFINITY;
+                } else {
+                    const double exploit = z->total / (double)z->visits;
+                    const double explore = c * sqrt(lg / (double)z->visits);
+                    const double bias = 0.0 * (0.0 / (1.0 + (double)z->visits));
+                    v = exploit + explore;
+                    v = v + bias;
+                }
+                if (best < 0 || v > bv) { best = ch[u][k]; bv = v; }
+            }
+            u = best;
+        }
+        /* expansion */
+        if (nodes[u].n_untried > 0) {
+            or_mnode* z = &nodes[u];
+            const int mv = z->untried[--z->n_untried];
+            or_board* nb = (or_board*)malloc(sizeof(or_board));
+            or_board_copy(nb, &z->board);
+            or_place_move(nb, z->player, mv);
+            const int child = nn;
+            NEW_NODE(nb, (z->player + 1) & 3, mv, u);
+            free(nb);
+            ch[u][nodes[u].nchild++] = child;
+            u = child;
+        }
+        /* simulation */
+        double reward = 0.0;
+        int hit = 0, slot = 0;
+        uint64_t h = 0;
+        if (use_tt) {
+            h = or_zobrist_hash(&nodes[u].board, ztab);
+            hit = tt_find(tt_keys, tt_vals, tt_cap, h, &slot);
+        }
+        if (hit) {
+            reward = tt_vals[slot];
+            ++nhits;
+        } else {
+            reward = or_rollout_mt(&nodes[u].board, nodes[u].player, rng, max_rollout, scratch);
+            if (use_tt) {
+                if (*tt_count + 1 >= tt_cap) { rc = -3; goto done; }
+                tt_keys[slot] = h;
+                tt_vals[slot] = reward;
+                ++*tt_count;
+            }
+        }
+        rewards[it] = reward;
+        hit_flags[it] = (uint8_t)hit;
+        /* backpropagation */
+        for (int v = u; v >= 0; v = nodes[v].parent) {
+            nodes[v].visits += 1;
+            nodes[v].total += reward;
+        }
+    }
+    {
+        int best = -1, bv = -1;
+        for (int k = 0; k < nodes[0].nchild; ++k) {
+            const or_mnode* z = &nodes[ch[0][k]];
+            if (k < child_cap) {
+                child_moves[k] = z->move; child_visits[k] = z->visits; child_totals[k] = z->total;
+            }
+            if (z->visits > bv) { bv = z->visits; best = z->move; }
+        }
+        *n_children = nodes[0].nchild;
+        *best_move = best;
+        *hits = nhits;
+    }
+done:
+    for (int i = 0; i < nn; ++i) { free(nodes[i].untried); free(ch[i]); }
+    free(ch); free(nodes); free(scratch);
+    return rc;
+#undef NEW_NODE
+}

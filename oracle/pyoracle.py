@@ -97,6 +97,10 @@ def lib():
             "or_zobrist_hash": (C.c_uint64, [P(Board), P(C.c_uint64)]),
             "or_batch_playouts": (C.c_int, [P(State), C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
                                             C.c_int, P(Result)]),
+            "or_mcts": (C.c_int, [P(Board), C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int,
+                                  C.c_void_p, P(MT), C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                  P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_void_p,
+                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, P(C.c_int32)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -227,3 +231,66 @@ def batch_playouts(states, n_playouts, seed, semantics=SEM_ARENA, max_plies=2500
     out = (Result * n_playouts)()
     lib().or_batch_playouts(states, len(states), n_playouts, seed, semantics, max_plies, threads, out)
     return out
+
+
+def zobrist_table(seed):
+    t = np.zeros(2088, np.uint64)
+    lib().or_zobrist_table(seed, t.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return t
+
+
+def numpy_mt(seed):
+    m = MT()
+    lib().or_mt_seed_numpy(C.byref(m), seed)
+    return m
+
+
+class TT:
+    """Transposition table as open addressing (empty slot = NaN value)."""
+
+    def __init__(self, cap=1 << 12):
+        self.keys = np.zeros(cap, np.uint64)
+        self.vals = np.full(cap, np.nan)
+        self.count = 0
+
+
+def mcts(b, player, iterations, exploration, max_rollout, ztab, rng, tt=None, child_cap=4096):
+    """or_mcts: one MCTSAgent search (mcts/mcts_agent.py:304-582) with RandomAgent
+    rollouts drawing from `rng` (an MT, advanced in place).  tt: a TT or None."""
+    log_table = np.zeros(iterations + 2)
+    log_table[1:] = np.log(np.arange(1, iterations + 2))
+    use_tt = tt is not None
+    if use_tt:
+        while (tt.count + iterations + 1) * 2 > len(tt.keys):  # grow: re-insert live keys
+            live = ~np.isnan(tt.vals)
+            k, v = tt.keys[live], tt.vals[live]
+            cap = len(tt.keys) * 2
+            tt.keys = np.zeros(cap, np.uint64)
+            tt.vals = np.full(cap, np.nan)
+            for kk, vv in zip(k.tolist(), v.tolist()):
+                i = kk & (cap - 1)
+                while not np.isnan(tt.vals[i]):
+                    i = (i + 1) & (cap - 1)
+                tt.keys[i], tt.vals[i] = kk, vv
+        keys, vals, cap = tt.keys, tt.vals, len(tt.keys)
+    else:
+        keys, vals, cap = np.zeros(1, np.uint64), np.full(1, np.nan), 1
+    cnt = C.c_int32(tt.count if use_tt else 0)
+    best, hits, nch = C.c_int32(), C.c_int32(), C.c_int32()
+    rewards = np.zeros(iterations)
+    flags = np.zeros(iterations, np.uint8)
+    cm = np.zeros(child_cap, np.int32)
+    cv = np.zeros(child_cap, np.int32)
+    ct = np.zeros(child_cap)
+    rc = lib().or_mcts(C.byref(b), player, iterations, exploration, max_rollout, log_table.ctypes.data,
+                       len(log_table), ztab.ctypes.data, C.byref(rng), int(use_tt), keys.ctypes.data,
+                       vals.ctypes.data, cap, C.byref(cnt), C.byref(best), C.byref(hits),
+                       rewards.ctypes.data, flags.ctypes.data, cm.ctypes.data, cv.ctypes.data,
+                       ct.ctypes.data, child_cap, C.byref(nch))
+    if rc != 0:
+        raise RuntimeError(f"or_mcts failed: {rc}")
+    if use_tt:
+        tt.count = cnt.value
+    n = min(nch.value, child_cap)
+    return {"move": best.value, "hits": hits.value, "rewards": rewards, "hit_flags": flags,
+            "children": list(zip(cm[:n].tolist(), cv[:n].tolist(), ct[:n].tolist()))}

@@ -166,3 +166,41 @@ def test_arena_full_games_match_run_single_game():
         assert [p + 1 for p in range(4) if res.winner_mask >> p & 1] == rec["winner_ids"]
         assert b.move_count == rec["moves_made"] and res.passes == rec["passes"]
         assert res.turns == rec["turn_count"]
+
+
+MCTS = load_golden("mcts.json")
+
+
+@pytest.mark.parametrize("case", range(len(MCTS)))
+def test_mcts_search_matches_reference(case):
+    """or_mcts vs MCTSAgent(rollout_agent=RandomAgent(seed)) searches: best move, every
+    root child's (move, visits, total_reward), TT hits, rollout rewards in order, TT
+    size and the rollout stream's final MT19937 state, over two consecutive calls."""
+    c = MCTS[case]
+    b = replay(POS[c["position"]])
+    ztab = O.zobrist_table(c["zobrist_seed"])
+    rng = O.numpy_mt(c["rollout_seed"])
+    tt = O.TT() if c["use_tt"] else None
+    hits, rewards = 0, []
+    for call in c["calls"]:
+        player = call["player"] - 1
+        assert b.cur == player
+        legal = O.legal_moves(b, player)
+        assert len(legal) == call["n_legal"]
+        if call["searched"]:
+            res = O.mcts(b, player, c["iterations"], 1.414, c["max_rollout_moves"], ztab, rng, tt)
+            assert res["move"] == call["move"]
+            assert [list(x) for x in res["children"]] == call["root_children"]
+            hits += res["hits"]
+            rewards += [r for r, f in zip(res["rewards"].tolist(), res["hit_flags"].tolist()) if not f]
+            assert hits == call["transposition_hits"]
+            assert rewards == call["rollout_rewards"]
+            assert (tt.count if tt else None) == call["tt_size"]
+        else:
+            assert call["move"] == (legal[0] if legal else None)
+        assert rng.mti == call["rng_pos"]
+        assert _sha(list(rng.mt)) == call["rng_sha"]
+        if call["move"] is None:
+            break
+        O.place_move(b, player, call["move"])
+        assert b.cur == (player + 1) % 4

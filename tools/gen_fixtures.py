@@ -28,6 +28,10 @@ What is recorded (all reference behaviour, nothing re-implemented here):
 * ``fastmcts.json``    -- FastMCTSAgent.think results (agents/fast_mcts_agent.py:112)
 * ``zobrist.json``     -- ZobristHash.hash_board values (mcts/zobrist.py:70)
 * ``arena_small.json`` -- run_single_game records for 4 random agents
+* ``mcts.json``        -- MCTSAgent (UCT + Zobrist transposition table) searches with
+                          RandomAgent rollouts (mcts/mcts_agent.py:304-582): two
+                          consecutive select_action calls per agent, the root children
+                          (move, visits, total_reward), stats and rollout-RNG state
 """
 from __future__ import annotations
 
@@ -323,6 +327,73 @@ def gen_arena_runs():
     return {"config": ARENA_RUN, "games": games, "summary_input": synth, "summary": summary}
 
 
+# (position index, iterations, max_rollout_moves, use_tt, rollout seed, zobrist seed)
+MCTS_CASES = [
+    (8, 24, 50, True, 11, 3), (12, 40, 50, True, 12, 4), (16, 24, 50, False, 13, 5),
+    (20, 60, 8, True, 14, 6), (24, 120, 4, True, 15, 7), (30, 200, 2, True, 16, 8),
+    (36, 48, 50, True, 17, 9), (47, 150, 3, True, 18, 10), (50, 60, 50, True, 19, 11),
+    (49, 100, 50, True, 20, 12), (53, 300, 1, True, 21, 13), (40, 64, 6, False, 22, 14),
+    (46, 80, 50, True, 23, 15), (18, 450, 2, True, 24, 16), (19, 400, 3, True, 25, 17),
+]
+
+
+def gen_mcts_case(case):
+    """MCTSAgent.select_action (mcts/mcts_agent.py:304-341) restated around the
+    agent's own methods so the root node can be recorded: root = MCTSNode(board,
+    player); _run_mcts_with_iterations(root); best = root.get_best_move(); the TT
+    clear rule of :338-339.  Call 1 searches the position, call 2 the position
+    after call 1's move (same agent: TT and rollout stream carry over)."""
+    pos, iters, max_roll, use_tt, rseed, zseed = case
+    _setup()
+    from agents.random_agent import RandomAgent
+    from engine.board import Player
+    from engine.move_generator import get_shared_generator
+    from mcts.mcts_agent import MCTSAgent, MCTSNode
+    from tests.utils_game_states import generate_random_valid_state
+    gid_of = _gid_map()
+    board, cur = generate_random_valid_state(*POSITION_SPECS[pos])
+    agent = MCTSAgent(iterations=iters, rollout_agent=RandomAgent(seed=rseed), seed=zseed,
+                      use_transposition_table=use_tt, max_rollout_moves=max_roll)
+    gen = get_shared_generator()
+    calls = []
+    for call in range(2):
+        legal = gen.get_legal_moves(board, cur)
+        rec = {"player": cur.value, "n_legal": len(legal)}
+        if len(legal) <= 1:
+            rec["move"] = move_int(gid_of, legal[0]) if legal else None
+            rec["searched"] = False
+        else:
+            root = MCTSNode(board, cur)
+            agent._run_mcts_with_iterations(root)
+            best = root.get_best_move()
+            if agent.transposition_table and len(agent.transposition_table.table) > 500000:
+                agent.transposition_table.clear()
+            rec.update({
+                "searched": True,
+                "move": move_int(gid_of, best),
+                "root_children": [[move_int(gid_of, ch.move), ch.visits, float(ch.total_reward)]
+                                  for ch in root.children],
+                "root_visits": root.visits,
+                "root_untried": len(root.untried_moves),
+                "iterations_run": agent.stats["iterations_run"],
+                "transposition_hits": agent.stats["transposition_hits"],
+                "rollout_rewards": [float(r) for r in agent.stats["rollout_rewards"]],
+                "tt_size": len(agent.transposition_table.table) if agent.transposition_table else None,
+            })
+            best = rec["move"]
+        st = agent.rollout_agent.rng.get_state()
+        rec["rng_pos"] = int(st[2])
+        rec["rng_sha"] = _sha(int(x) for x in st[1])
+        calls.append(rec)
+        if rec["move"] is None:
+            break
+        mv = next(m for m in legal if move_int(gid_of, m) == rec["move"])
+        board.place_piece(agent._get_move_positions(mv), cur, mv.piece_id, validate=False)
+        cur = list(Player)[(list(Player).index(cur) + 1) % 4]
+    return {"position": pos, "iterations": iters, "max_rollout_moves": max_roll, "use_tt": use_tt,
+            "rollout_seed": rseed, "zobrist_seed": zseed, "calls": calls}
+
+
 def dump(name, obj):
     path = os.path.join(OUT, name)
     with open(path, "w") as f:
@@ -385,6 +456,9 @@ def main():
         dump("arena_small.json", gen_arena())
     if what in ("all", "arena_runs"):
         dump("arena_runs.json", gen_arena_runs())
+    if what in ("all", "mcts"):
+        with Pool(8) as pool:
+            dump("mcts.json", pool.map(gen_mcts_case, MCTS_CASES))
 
 
 if __name__ == "__main__":
