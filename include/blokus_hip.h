@@ -242,6 +242,75 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
                 const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
                 double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem);
 
+/*
+ * bk_mcts -- MCTSAgent.select_action searches (mcts/mcts_agent.py:304-582, MCTSNode
+ * :19-191) with RandomAgent rollouts (agents/random_agent.py:49) and the Zobrist
+ * transposition table (mcts/zobrist.py:12-220), one search per game, all on the GPU.
+ * Bit-exact with the reference for the same inputs: frontier-order legal lists
+ * (root_sets = the Board's frontier tables, see bk_fset_*), untried.pop() expansion,
+ * UCB1 in IEEE double with np.log values from log_table (log_table[v] = np.log(v)),
+ * first-best ties, the rollout agent's numpy MT19937 stream (mt_state[625] per game:
+ * key[624] then pos; in/out), TT hits reusing the cached reward.
+ *
+ * Inputs per game: roots[g] / root_sets[g] (the position), players[g] (the searching
+ * player, MCTSNode.player), root_hash[g] (ZobristHash.hash_board of the position),
+ * zobrist_index[g] (which 2088-entry key table of `zobrist` the agent uses: 20*20*5 cell
+ * keys, 4 turn keys, 4*21 piece keys, mcts/zobrist.py:41-68).
+ * TT per game: tt_keys/tt_vals[g * cfg.tt_cap ...] open addressing (linear probing,
+ * slot = key & (tt_cap - 1), empty slot = NaN value), tt_count[g] entries; in/out so the
+ * table persists across an agent's searches like the reference's dict.
+ * nodes[g * cfg.node_cap ...]: the tree (node 0 = root; children of a node are a block
+ * reserved at its first expansion, in expansion order); left on return for inspection.
+ * rewards / hit_flags (optional, [g * cfg.iterations + i]): per iteration the simulated
+ * reward and 1 if it came from the TT (stats["rollout_rewards"] = the non-hit ones).
+ * out[g].status != 0 means the search stopped early (see BK_MCTS_E*): enlarge the pool /
+ * TT and retry from the saved inputs.
+ */
+#define BK_MCTS_NODE_EVALUATED 1u
+typedef struct bk_mcts_node {
+    double total;       /* total_reward                                               */
+    uint32_t visits;
+    int32_t child0;     /* first slot of the child block, -1 = none                   */
+    uint16_t move;      /* g * 400 + anchor cell of the move leading here (root 0xFFFF) */
+    uint16_t n_exp;     /* len(children)                                              */
+    uint16_t n_legal;   /* len(legal moves) once evaluated                            */
+    uint16_t flags;     /* BK_MCTS_NODE_EVALUATED                                     */
+} bk_mcts_node;         /* 24 bytes */
+
+typedef struct bk_mcts_cfg {
+    int32_t iterations;        /* MCTSAgent.iterations (also the rewards row stride)   */
+    int32_t max_rollout_moves; /* MCTSAgent.max_rollout_moves (> 0)                    */
+    double exploration;        /* exploration_constant                                 */
+    int32_t use_tt;            /* use_transposition_table                              */
+    int32_t node_cap;          /* node slots per game                                  */
+    int32_t tt_cap;            /* TT slots per game, power of two (>= 2 when use_tt)   */
+    int32_t time_limit_us;     /* > 0: stop at the first iteration boundary past it    */
+} bk_mcts_cfg;
+
+#define BK_MCTS_EPOOL 1u   /* node pool full                    */
+#define BK_MCTS_EFSET 2u   /* frontier table overflow           */
+#define BK_MCTS_ETT 4u     /* TT full                           */
+#define BK_MCTS_EPATH 8u   /* tree deeper than BK_MCTS_MAX_DEPTH */
+#define BK_MCTS_ELOG 16u   /* log_table too short               */
+#define BK_MCTS_EINTERNAL 32u /* consistency check failed        */
+#define BK_MCTS_MAX_DEPTH 63
+typedef struct bk_mcts_out {
+    int32_t best_move;       /* g*400+cell of the most visited root child (first on ties), -1 */
+    int32_t iterations_run;
+    int32_t tt_hits;         /* simulations answered by the TT                           */
+    int32_t rollouts;        /* simulations that ran a rollout                           */
+    int32_t nodes_used;
+    int32_t root_children;
+    uint32_t status;         /* BK_MCTS_E* bits                                          */
+    int32_t reserved;
+} bk_mcts_out;
+
+int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const uint8_t* players,
+            const uint64_t* root_hash, int32_t n_games, const bk_mcts_cfg* cfg, const uint64_t* zobrist,
+            int32_t n_zobrist, const int32_t* zobrist_index, uint32_t* mt_state, uint64_t* tt_keys,
+            double* tt_vals, int32_t* tt_count, const double* log_table, int32_t log_len,
+            bk_mcts_node* nodes, double* rewards, uint8_t* hit_flags, bk_mcts_out* out, int mem);
+
 /* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
    stream, measured with HIP events around that launch. */
 int bk_last_kernel_ms(bk_handle h, float* ms);

@@ -30,6 +30,7 @@ EXPORTS = (
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
+    "bk_mcts",
 )
 FSET_SLOTS = 256
 # bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
@@ -73,6 +74,25 @@ FASTMCTS_OUT_DTYPE = np.dtype([("best_index", "<i4"), ("iterations", "<i4"), ("n
                                ("top_q", "<f8", (10,))])
 assert FASTMCTS_OUT_DTYPE.itemsize == 176
 assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRolloutCfg) == 32
+
+
+class BkMctsCfg(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("max_rollout_moves", C.c_int32), ("exploration", C.c_double),
+                ("use_tt", C.c_int32), ("node_cap", C.c_int32), ("tt_cap", C.c_int32),
+                ("time_limit_us", C.c_int32)]
+
+
+assert C.sizeof(BkMctsCfg) == 32
+MCTS_NODE_DTYPE = np.dtype([("total", "<f8"), ("visits", "<u4"), ("child0", "<i4"), ("move", "<u2"),
+                            ("n_exp", "<u2"), ("n_legal", "<u2"), ("flags", "<u2")])
+assert MCTS_NODE_DTYPE.itemsize == 24
+MCTS_OUT_DTYPE = np.dtype([("best_move", "<i4"), ("iterations_run", "<i4"), ("tt_hits", "<i4"),
+                           ("rollouts", "<i4"), ("nodes_used", "<i4"), ("root_children", "<i4"),
+                           ("status", "<u4"), ("reserved", "<i4")])
+assert MCTS_OUT_DTYPE.itemsize == 32
+MCTS_ZOBRIST_WORDS = 2088
+MCTS_MAX_DEPTH = 63
+MCTS_EPOOL, MCTS_EFSET, MCTS_ETT, MCTS_EPATH, MCTS_ELOG, MCTS_EINTERNAL = 1, 2, 4, 8, 16, 32
 
 # numpy views of the same records
 
@@ -123,6 +143,8 @@ def load():
             "bk_fset_list": (C.c_int, [vp, C.c_int32, vp, C.c_int32]),
             "bk_rollout_frontier": (C.c_int, [vp, vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, vp,
                                               vp, C.c_int]),
+            "bk_mcts": (C.c_int, [vp, vp, vp, vp, vp, C.c_int32, P(BkMctsCfg), vp, C.c_int32, vp, vp, vp, vp,
+                                  vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -261,6 +283,16 @@ class Handle:
                                              C.c_void_p(seeds_ptr or 0), C.c_void_p(out_ptr or 0),
                                              C.c_void_p(states_ptr or 0), C.c_void_p(osets_ptr or 0), mem)
         self.check(rc, "bk_rollout_frontier")
+
+    def mcts(self, roots_ptr, sets_ptr, players_ptr, hash_ptr, n_games, cfg: BkMctsCfg, zob_ptr, n_zob, zidx_ptr,
+             mt_ptr, ttk_ptr, ttv_ptr, ttc_ptr, log_ptr, log_len, nodes_ptr, rewards_ptr, flags_ptr, out_ptr, mem):
+        v = lambda x: C.c_void_p(x or 0)  # noqa: E731
+        with self._lock:
+            rc = self._L.bk_mcts(self._h, v(roots_ptr), v(sets_ptr), v(players_ptr), v(hash_ptr), n_games,
+                                 C.byref(cfg), v(zob_ptr), n_zob, v(zidx_ptr), v(mt_ptr), v(ttk_ptr), v(ttv_ptr),
+                                 v(ttc_ptr), v(log_ptr), log_len, v(nodes_ptr), v(rewards_ptr), v(flags_ptr),
+                                 v(out_ptr), mem)
+        self.check(rc, "bk_mcts")
 
     def advance(self, roots_ptr, n_roots, index_ptr, n, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
         with self._lock:

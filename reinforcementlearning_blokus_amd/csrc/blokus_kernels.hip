@@ -776,26 +776,29 @@ __host__ __device__ inline bool fs_place(FsetRef t, int16_t* tmp, const int32_t*
     return true;
 }
 
-// set.copy() (make_new_set + set_merge into an empty set)
-__host__ __device__ inline void fs_copy(FsetRef d, const int16_t* skey, uint32_t smask, uint32_t sfill,
+// set.copy() (make_new_set + set_merge into an empty set).  false: the copy's table
+// would not fit the storage (d left empty)
+__host__ __device__ inline bool fs_copy(FsetRef d, const int16_t* skey, uint32_t smask, uint32_t sfill,
                                         uint32_t sused) {
     fs_clear(d);
-    if (sused == 0) return;
+    if (sused == 0) return true;
     if (sused * 5 >= 7u * 3u) {  // (fill + other->used) * 5 >= mask * 3 on the fresh table
         uint32_t newsize = 8;
         while (newsize <= sused * 2) newsize <<= 1;
+        if (newsize > d.cap) return false;
         *d.mask = (uint16_t)(newsize - 1);
     }
     if (*d.mask == smask && sfill == sused) {
         for (uint32_t i = 0; i <= smask; ++i) d.at(i) = skey[i];
         *d.fill = (uint16_t)sfill;
         *d.used = (uint16_t)sused;
-        return;
+        return true;
     }
     *d.fill = (uint16_t)sused;
     *d.used = (uint16_t)sused;
     for (uint32_t i = 0; i <= smask; ++i)
         if (skey[i] >= 0) fs_insert_clean(d, *d.mask, skey[i]);
+    return true;
 }
 
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch
@@ -990,7 +993,8 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
             const bk_fset* src = a.root_sets + ri;
 #pragma unroll 1
             for (int q = 0; q < 4; ++q)
-                fs_copy(fs_ref(d, q, htab), src->key[q], src->mask[q], src->fill[q], src->used[q]);
+                if (!fs_copy(fs_ref(d, q, htab), src->key[q], src->mask[q], src->fill[q], src->used[q]))
+                    g.status |= 2u;
         } else {
             copy_fset(&a.fslab[slot].s, a.root_sets + ri);
         }
@@ -1386,6 +1390,493 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// MCTSAgent searches (mcts/mcts_agent.py:19-582) with RandomAgent rollouts: one lane =
+// one game's whole search.  The UCT tree lives in a per-game node pool in HBM, the
+// Zobrist TT is a per-game open-addressing table in HBM, the rollout stream is the
+// agent's numpy MT19937.  A node stores no board: the selected leaf's board is replayed
+// from the root along the tree path with the reference's copy/place/copy sequence
+// (frontier-set layouts, hence list orders, depend on it).  Every kernel step runs ONE
+// movegen for each busy lane -- the expansion of its selected leaf or one rollout ply --
+// and the divergent tree work (selection, replay, TT, backpropagation) in between.
+// ------------------------------------------------------------------------------------
+#define MC_SELECT 0
+#define MC_EXPAND 1
+#define MC_ROLLOUT 2
+#define MC_PATH (BK_MCTS_MAX_DEPTH + 1)
+#define MC_ZOB 2088
+
+struct McLane {          // per-lane scratch record in HBM
+    FsLane A;            // node.board tables of the node being worked on
+    FsLane B;            // copy target; the rollout's sim board
+    bk_fset root;        // root.board (= board.copy(), made once per search)
+    int32_t path[MC_PATH];
+};
+static_assert(sizeof(FsLane) % 16 == 0 && sizeof(bk_fset) % 16 == 0, "McLane tables are read as uint4");
+
+struct MctsArgs {
+    const bk_state* roots;
+    const bk_fset* root_sets;
+    const uint8_t* players;
+    const uint64_t* root_hash;
+    int32_t n_games;
+    bk_mcts_cfg cfg;
+    const uint64_t* zobrist;
+    const int32_t* zidx;
+    uint32_t* mt;
+    uint64_t* tt_keys;
+    double* tt_vals;
+    int32_t* tt_count;
+    const double* log_table;
+    int32_t log_len;
+    bk_mcts_node* nodes;
+    double* rewards;
+    uint8_t* hit_flags;
+    bk_mcts_out* out;
+    uint32_t* slab;
+    McLane* lanes;
+    uint32_t* counter;  // [0] next game, [1] step guard tripped
+    uint64_t max_steps;
+    uint64_t limit_ticks;  // cfg.time_limit_us in wall-clock (s_memrealtime) ticks
+};
+
+struct Mc {
+    int32_t game;       // -1 = none
+    int32_t it;         // iterations done
+    int32_t mode;
+    int32_t depth;      // path[depth] = node being expanded / simulated
+    int32_t node;
+    int32_t nodes_used, tt_cnt, hits, rollouts;
+    int32_t root_player, root_cp;
+    int32_t cur, player, plies, score0;
+    uint32_t status, mt_pos, first, tt_slot;
+    bool tt_miss;
+    Quad used, cells;
+    uint64_t hash, t0;
+};
+
+__device__ __forceinline__ uint32_t mc_temper(uint32_t y) {
+    y ^= y >> 11; y ^= (y << 7) & 0x9d2c5680u; y ^= (y << 15) & 0xefc60000u; y ^= y >> 18;
+    return y;
+}
+
+// numpy mt19937_gen in place, 16 words per batch of loads (a batch only reads words an
+// earlier batch wrote, or old words no batch has written yet)
+__device__ void mc_twist(uint32_t* st) {
+#pragma unroll 1
+    for (int i0 = 0; i0 < FM_N; i0 += 16) {
+        uint32_t x[16], y[16], z[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = i0 + j;
+            x[j] = st[i];
+            y[j] = st[i == FM_N - 1 ? 0 : i + 1];
+            z[j] = st[i < FM_N - FM_M ? i + FM_M : i - (FM_N - FM_M)];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) st[i0 + j] = z[j] ^ mt_y(x[j], y[j]);
+    }
+}
+
+// RandomState.randint(0, n): masked rejection over 32-bit outputs; n == 1 draws nothing
+__device__ __forceinline__ uint32_t mc_randint(uint32_t* st, uint32_t& pos, uint32_t n) {
+    const uint32_t rng = n - 1u;
+    if (rng == 0u) return 0u;
+    const uint32_t mask = mask_for(rng);
+    uint32_t v;
+    do {
+        if (pos >= FM_N) { mc_twist(st); pos = 0; }
+        v = mc_temper(st[pos++]) & mask;
+    } while (v > rng);
+    return v;
+}
+
+__device__ __forceinline__ int mc_score(const Mc& m, int p) {  // Board.get_score, engine/board.py:562
+    return (int)m.cells.get(p) + ((m.used.get(p) == 0x1FFFFFu) ? 15 : 0);
+}
+
+__device__ __forceinline__ bool mc_copy_tables(bk_fset* d, const bk_fset* s, const uint64_t* htab) {
+    bool ok = true;
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) ok &= fs_copy(fs_ref(d, q, htab), s->key[q], s->mask[q], s->fill[q], s->used[q]);
+    return ok;
+}
+
+// Board.place_piece(validate=False) of orientation gs at (ar, ac) for player p: rows,
+// used / cells / first, and the player's frontier table in T (engine/board.py:515-555)
+__device__ bool mc_place(Mc& m, const Slab& slab, int p, int gs, int ar, int ac, FsLane* T, const uint64_t* htab) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    int32_t cells[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const uint32_t cell = kCells[gs][q < n ? q : 0];
+        const int r = ar + (int)(cell >> 8), c = ac + (int)(cell & 0xFFu);
+        cells[q] = r * 20 + c;
+        if (q < n) {
+            slab.at(p, r) |= 1u << c;
+            slab.at(4, r) |= 1u << c;
+        }
+    }
+    const uint32_t* occ_rows = slab.base + 4 * 20;
+    const uint32_t* own_rows = slab.base + p * 20;
+    auto occ = [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; };
+    auto own = [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; };
+    const bool ok = fs_place(fs_ref(&T->s, p, htab), T->tmp, cells, n, occ, own);
+    m.cells.set(p, m.cells.get(p) + (uint32_t)n);
+    m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
+    m.first &= ~(1u << p);
+    return ok;
+}
+
+// Zobrist update for that placement (mcts/zobrist.py:70-99 terms that change)
+__device__ __forceinline__ uint64_t mc_hash_step(const uint64_t* Z, uint64_t h, int p, int cp, int gs, int ar, int ac) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    h ^= Z[2000 + cp] ^ Z[2000 + ((cp + 1) & 3)];
+    for (int q = 0; q < n; ++q) {
+        const uint32_t cell = kCells[gs][q];
+        const int ci = (ar + (int)(cell >> 8)) * 20 + ac + (int)(cell & 0xFFu);
+        h ^= Z[ci * 5] ^ Z[ci * 5 + p + 1];
+    }
+    return h ^ Z[2004 + p * 21 + (int)(info & 0xFFu) - 1];
+}
+
+__device__ __forceinline__ void mc_move_split(uint32_t mv, int& gs, int& ar, int& ac) {
+    gs = (int)(mv / 400u);
+    const int cell = (int)(mv % 400u);
+    ar = cell / 20;
+    ac = cell - 20 * ar;
+}
+
+// root.board into the lane: rows from the state, tables = the search's root copy
+__device__ void mc_load_root(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L) {
+    const bk_state* s = a.roots + m.game;
+    uint32_t occ[20];
+#pragma unroll
+    for (int R = 0; R < 20; ++R) occ[R] = 0;
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p) {
+        uint32_t cells = 0;
+        uint64_t w[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) w[k] = s->planes[p][k];
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            const uint32_t row = plane_row(w, R);
+            slab.at(p, R) = row;
+            occ[R] |= row;
+            cells += __builtin_popcount(row);
+        }
+        m.cells.set(p, cells);
+        m.used.set(p, s->used[p] & 0x1FFFFFu);
+    }
+#pragma unroll
+    for (int R = 0; R < 20; ++R) slab.at(4, R) = occ[R];
+    m.first = s->first_move & 0xFu;
+    copy_fset(&L->A.s, &L->root);
+}
+
+__device__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab) {
+    m.game = g;
+    m.it = 0;
+    m.mode = MC_SELECT;
+    m.nodes_used = 1;
+    m.tt_cnt = a.cfg.use_tt ? a.tt_count[g] : 0;
+    m.hits = m.rollouts = 0;
+    m.root_player = a.players[g] & 3;
+    m.root_cp = a.roots[g].current_player & 3;
+    m.status = 0;
+    m.mt_pos = a.mt[(size_t)g * (FM_N + 1) + FM_N];
+    m.t0 = wall_clock64();
+    bk_mcts_node* root = a.nodes + (size_t)g * a.cfg.node_cap;
+    root->total = 0.0; root->visits = 0; root->child0 = -1;
+    root->move = 0xFFFFu; root->n_exp = 0; root->n_legal = 0; root->flags = 0;
+    if (!mc_copy_tables(&L->root, a.root_sets + g, htab)) m.status |= BK_MCTS_EFSET;  // MCTSNode: board.copy()
+}
+
+__device__ void mc_finish_game(const MctsArgs& a, Mc& m) {
+    const int32_t g = m.game;
+    const bk_mcts_node* pool = a.nodes + (size_t)g * a.cfg.node_cap;
+    const bk_mcts_node root = pool[0];
+    int32_t best = -1;
+    uint32_t bv = 0;
+    for (int k = 0; k < (int)root.n_exp; ++k) {  // get_best_move: max visits, first on ties
+        const bk_mcts_node c = pool[root.child0 + k];
+        if (best < 0 || c.visits > bv) { bv = c.visits; best = c.move; }
+    }
+    bk_mcts_out o;
+    o.best_move = best;
+    o.iterations_run = m.it;
+    o.tt_hits = m.hits;
+    o.rollouts = m.rollouts;
+    o.nodes_used = m.nodes_used;
+    o.root_children = root.n_exp;
+    o.status = m.status;
+    o.reserved = 0;
+    a.out[g] = o;
+    a.mt[(size_t)g * (FM_N + 1) + FM_N] = m.mt_pos;
+    if (a.cfg.use_tt) a.tt_count[g] = m.tt_cnt;
+    m.game = -1;
+}
+
+// TT probe for m.hash: hit -> reward; miss -> remembers the free slot for the insert
+__device__ __forceinline__ bool mc_tt_lookup(const MctsArgs& a, Mc& m, double& reward) {
+    const uint64_t mask = (uint64_t)a.cfg.tt_cap - 1u;
+    const uint64_t* keys = a.tt_keys + (size_t)m.game * a.cfg.tt_cap;
+    const double* vals = a.tt_vals + (size_t)m.game * a.cfg.tt_cap;
+    uint64_t i = m.hash & mask;
+    for (;;) {
+        const double v = vals[i];
+        if (v != v) break;
+        if (keys[i] == m.hash) { reward = v; return true; }
+        i = (i + 1) & mask;
+    }
+    m.tt_slot = (uint32_t)i;
+    return false;
+}
+
+// simulation result: TT insert on a miss, stats, backpropagation (mcts_agent.py:408-437,
+// :572-582), next iteration
+__device__ void mc_complete(const MctsArgs& a, Mc& m, McLane* L, double reward, bool hit) {
+    if (hit) {
+        m.hits++;
+    } else {
+        m.rollouts++;
+        if (a.cfg.use_tt) {
+            if ((uint32_t)m.tt_cnt + 2u > (uint32_t)a.cfg.tt_cap) {
+                m.status |= BK_MCTS_ETT;
+            } else {
+                a.tt_keys[(size_t)m.game * a.cfg.tt_cap + m.tt_slot] = m.hash;
+                a.tt_vals[(size_t)m.game * a.cfg.tt_cap + m.tt_slot] = reward;
+                m.tt_cnt++;
+            }
+        }
+    }
+    if (a.rewards) {
+        a.rewards[(size_t)m.game * a.cfg.iterations + m.it] = reward;
+        a.hit_flags[(size_t)m.game * a.cfg.iterations + m.it] = hit ? 1u : 0u;
+    }
+    bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+    for (int d = 0; d <= m.depth; ++d) {
+        bk_mcts_node* v = pool + L->path[d];
+        v->visits += 1u;
+        v->total += reward;
+    }
+    m.it++;
+    m.mode = MC_SELECT;
+}
+
+// simulate the node in m.node / m.hash whose player has no legal move: the rollout
+// breaks at once (reward 0.0, no draw)
+__device__ void mc_sim_terminal(const MctsArgs& a, Mc& m, McLane* L) {
+    double reward = 0.0;
+    bool hit = false;
+    if (a.cfg.use_tt) hit = mc_tt_lookup(a, m, reward);
+    if (!hit) reward = 0.0;
+    mc_complete(a, m, L, reward, hit);
+}
+
+// selection (mcts_agent.py:384-406, UCB1 :68-111) from the root; leaves m.node at the
+// node to expand or simulate, m.depth / path / m.hash for it.  Returns true when that
+// node is evaluated terminal (no untried move, no child).
+__device__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, const uint64_t* Z) {
+    const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+    int u = 0, depth = 0;
+    uint64_t h = a.root_hash[m.game];
+    L->path[0] = 0;
+    for (;;) {
+        const bk_mcts_node nd = pool[u];
+        if (!(nd.flags & BK_MCTS_NODE_EVALUATED) || nd.n_legal > nd.n_exp) break;  // expand it
+        if (nd.n_exp == 0) { m.node = u; m.depth = depth; m.hash = h; return true; }
+        if ((int32_t)nd.visits >= a.log_len) { m.status |= BK_MCTS_ELOG; break; }
+        if (depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; break; }
+        const double lg = a.log_table[nd.visits];
+        int best = nd.child0;
+        double bv = 0.0;
+        for (int k = 0; k < (int)nd.n_exp; ++k) {
+            const bk_mcts_node c = pool[nd.child0 + k];
+            double v;
+            if (c.visits == 0u) {
+                v = __builtin_inf();
+            } else {
+                const double vis = (double)c.visits;
+                const double exploit = c.total / vis;
+                const double explore = a.cfg.exploration * __builtin_sqrt(lg / vis);
+                v = exploit + explore;
+            }
+            if (k == 0 || v > bv) { bv = v; best = nd.child0 + k; }
+        }
+        int gs, ar, ac;
+        mc_move_split(pool[best].move, gs, ar, ac);
+        h = mc_hash_step(Z, h, (m.root_player + depth) & 3, (m.root_cp + depth) & 3, gs, ar, ac);
+        u = best;
+        L->path[++depth] = u;
+    }
+    m.node = u;
+    m.depth = depth;
+    m.hash = h;
+    return false;
+}
+
+// node.board of path[depth] into the lane (slab rows + table A): root, then per edge
+// new_board = board.copy(); place; MCTSNode(new_board) copies again (mcts_agent.py:113-145)
+__device__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L, const uint64_t* htab) {
+    mc_load_root(a, m, slab, L);
+    const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+    for (int d = 1; d <= m.depth; ++d) {
+        int gs, ar, ac;
+        mc_move_split(pool[L->path[d]].move, gs, ar, ac);
+        bool ok = mc_copy_tables(&L->B.s, &L->A.s, htab);
+        ok &= mc_place(m, slab, (m.root_player + d - 1) & 3, gs, ar, ac, &L->B, htab);
+        ok &= mc_copy_tables(&L->A.s, &L->B.s, htab);
+        if (!ok) m.status |= BK_MCTS_EFSET;
+    }
+}
+
+__global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
+    __shared__ uint32_t lds[ROLL_WORDS_PER_WAVE * (BLOCK / WAVE) + 2 * BK_CELLS];
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    uint32_t* my = lds + wv * ROLL_WORDS_PER_WAVE;
+    uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
+    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + ROLL_WORDS_PER_WAVE * (BLOCK / WAVE));
+    for (int i = threadIdx.x; i < BK_CELLS; i += BLOCK) htab[i] = kCellHash[i];
+    __syncthreads();
+    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
+    McLane* L = a.lanes + slot;
+    Mc m;
+    m.game = -1;
+    m.mode = MC_SELECT;
+    bool done = false;
+    for (uint64_t step = 0;; ++step) {
+        // ---- tree work until this lane needs a movegen (divergent)
+        while (!done && m.mode == MC_SELECT) {
+            if (m.game < 0) {
+                const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
+                if (next >= a.n_games) { done = true; break; }
+                mc_start_game(a, m, L, next, htab);
+            }
+            const bool timed_out = a.cfg.time_limit_us > 0 &&
+                                   wall_clock64() - m.t0 >= a.limit_ticks;
+            if (m.it >= a.cfg.iterations || timed_out || m.status) { mc_finish_game(a, m); continue; }
+            const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
+            if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
+            if (m.status) continue;
+            mc_replay(a, m, slab, L, htab);
+            m.mode = MC_EXPAND;
+        }
+        if (__ballot(!done) == 0ull) break;
+        if (step > a.max_steps) {  // safety valve: never spin forever
+            if (lane == 0) atomicOr(&a.counter[1], 1u);
+            break;
+        }
+        // ---- one movegen per busy lane (uniform work)
+        const bool idle = done;
+        const int p = idle ? 0 : (m.mode == MC_EXPAND ? ((m.root_player + m.depth) & 3) : m.cur);
+        Planes P;
+        {
+            uint32_t own[20], occ[20];
+#pragma unroll
+            for (int R = 0; R < 20; ++R) {
+                own[R] = idle ? 0u : slab.at(p, R);
+                occ[R] = idle ? 0u : slab.at(4, R);
+            }
+            derive_rows(own, occ, (m.first >> p) & 1u, p, P.B, P.C);
+        }
+        make_pairs(P);
+        const uint32_t avail = idle ? 0u : (~m.used.get(p) & 0x1FFFFFu);
+        const uint32_t total = movegen_counts<true>(P, avail, my, lane);
+        if (idle) continue;
+        bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+        uint32_t k;
+        if (m.mode == MC_EXPAND) {
+            bk_mcts_node* nd = pool + m.node;
+            uint32_t n_legal = nd->n_legal, n_exp = nd->n_exp;
+            int32_t child0 = nd->child0;
+            if (!(nd->flags & BK_MCTS_NODE_EVALUATED)) {  // MCTSNode._initialize_untried_moves
+                n_legal = total;
+                if (total > 0u) {
+                    if ((uint64_t)m.nodes_used + total > (uint64_t)a.cfg.node_cap) {
+                        m.status |= BK_MCTS_EPOOL;
+                        m.mode = MC_SELECT;
+                        continue;
+                    }
+                    child0 = m.nodes_used;
+                    m.nodes_used += (int32_t)total;
+                }
+                nd->n_legal = (uint16_t)n_legal;
+                nd->child0 = child0;
+                nd->flags = BK_MCTS_NODE_EVALUATED;
+            }
+            if (n_legal != total) {  // an evaluated node's list cannot change
+                m.status |= BK_MCTS_EINTERNAL;
+                m.mode = MC_SELECT;
+                continue;
+            }
+            if (n_legal == n_exp) {  // no legal move: terminal leaf
+                mc_sim_terminal(a, m, L);
+                continue;
+            }
+            k = n_legal - n_exp - 1u;  // untried_moves.pop(): the last list entry
+        } else {
+            if (total == 0u) {  // _rollout: no legal move -> break
+                mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
+                continue;
+            }
+            k = mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
+        }
+        uint32_t kk;
+        const int gs = pick_orient(my, lane, k, kk);
+#pragma unroll
+        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+        FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
+        int ar, ac;
+        locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+        if (ar < 0) {  // the table does not list the move: counts and tables disagree
+            m.status |= BK_MCTS_EINTERNAL;
+            m.mode = MC_SELECT;
+            continue;
+        }
+        if (m.mode == MC_EXPAND) {  // MCTSNode.expand (mcts_agent.py:113-145)
+            bk_mcts_node* nd = pool + m.node;
+            const uint32_t c = (uint32_t)nd->child0 + nd->n_exp;
+            nd->n_exp = (uint16_t)(nd->n_exp + 1u);
+            bk_mcts_node ch;
+            ch.total = 0.0; ch.visits = 0; ch.child0 = -1;
+            ch.move = (uint16_t)(gs * 400 + ar * 20 + ac);
+            ch.n_exp = 0; ch.n_legal = 0; ch.flags = 0;
+            pool[c] = ch;
+            if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
+            bool ok = mc_copy_tables(&L->B.s, &L->A.s, htab);
+            ok &= mc_place(m, slab, p, gs, ar, ac, &L->B, htab);
+            ok &= mc_copy_tables(&L->A.s, &L->B.s, htab);
+            if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
+            m.hash = mc_hash_step(Z, m.hash, p, (m.root_cp + m.depth) & 3, gs, ar, ac);
+            L->path[++m.depth] = (int32_t)c;
+            m.node = (int32_t)c;
+            double reward = 0.0;
+            if (a.cfg.use_tt && mc_tt_lookup(a, m, reward)) {
+                mc_complete(a, m, L, reward, true);
+                continue;
+            }
+            // _rollout (mcts_agent.py:470-554) on sim = node.board.copy()
+            if (!mc_copy_tables(&L->B.s, &L->A.s, htab)) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            m.player = m.cur = (m.root_player + m.depth) & 3;
+            m.score0 = mc_score(m, m.player);
+            m.plies = 0;
+            m.mode = MC_ROLLOUT;
+        } else {
+            if (!mc_place(m, slab, p, gs, ar, ac, &L->B, htab)) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            m.plies++;
+            m.cur = (m.cur + 1) & 3;
+            if (m.plies >= a.cfg.max_rollout_moves)
+                mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------
 struct bk_handle_s {
@@ -1403,6 +1894,8 @@ struct bk_handle_s {
     void* d_fin = nullptr; size_t d_fin_cap = 0;     // frontier: root tables
     void* d_fout = nullptr; size_t d_fout_cap = 0;   // frontier: advanced tables
     void* d_fslab = nullptr; size_t d_fslab_cap = 0; // frontier: per-slot records
+    void* d_mc = nullptr; size_t d_mc_cap = 0;       // bk_mcts: staged inputs/outputs
+    void* d_mclane = nullptr; size_t d_mclane_cap = 0; // bk_mcts: per-slot records
     uint32_t* d_counter = nullptr;
     int num_cu = 0;
     int rollout_blocks_per_cu = 0;
@@ -1483,7 +1976,7 @@ int bk_destroy(bk_handle h) {
     (void)hipSetDevice(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_counter};
+                    h->d_mc, h->d_mclane, h->d_counter};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -1765,7 +2258,8 @@ int bk_fset_copy(bk_fset* dst, const bk_fset* src) {
     if (dst == src) return BK_OK;
     for (int p = 0; p < 4; ++p) {
         if (src->mask[p] + 1u > BK_FSET_SLOTS) return BK_EINVAL;
-        fs_copy(fs_ref(dst, p, kCellHashHost), src->key[p], src->mask[p], src->fill[p], src->used[p]);
+        if (!fs_copy(fs_ref(dst, p, kCellHashHost), src->key[p], src->mask[p], src->fill[p], src->used[p]))
+            return BK_EINVAL;
     }
     return BK_OK;
 }
@@ -1847,6 +2341,114 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
         HIPCHK(h, hipStreamSynchronize(h->cur));
         if (ctr[1]) return set_err(h, BK_EINVAL, "bk_fastmcts: too many children or log table too short%s", "");
     }
+    return BK_OK;
+}
+
+int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const uint8_t* players,
+            const uint64_t* root_hash, int32_t n_games, const bk_mcts_cfg* cfg, const uint64_t* zobrist,
+            int32_t n_zobrist, const int32_t* zobrist_index, uint32_t* mt_state, uint64_t* tt_keys,
+            double* tt_vals, int32_t* tt_count, const double* log_table, int32_t log_len,
+            bk_mcts_node* nodes, double* rewards, uint8_t* hit_flags, bk_mcts_out* out, int mem) {
+    if (!h || !cfg || n_games < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
+        return set_err(h, BK_EINVAL, "bk_mcts: invalid arguments%s", "");
+    if (n_games == 0) return BK_OK;
+    if (!roots || !root_sets || !players || !root_hash || !zobrist || n_zobrist < 1 || !zobrist_index ||
+        !mt_state || !log_table || log_len < 1 || !out || (rewards == nullptr) != (hit_flags == nullptr))
+        return set_err(h, BK_EINVAL, "bk_mcts: missing buffer%s", "");
+    if (cfg->iterations < 0 || cfg->max_rollout_moves <= 0 || cfg->node_cap < 1 || cfg->time_limit_us < 0)
+        return set_err(h, BK_EINVAL, "bk_mcts: bad cfg (iterations/max_rollout_moves/node_cap)%s", "");
+    if (cfg->use_tt && (!tt_keys || !tt_vals || !tt_count || cfg->tt_cap < 2 || (cfg->tt_cap & (cfg->tt_cap - 1))))
+        return set_err(h, BK_EINVAL, "bk_mcts: use_tt needs tt buffers and a power-of-two tt_cap%s", "");
+    if (mem == BK_MEM_HOST) {
+        for (int32_t g = 0; g < n_games; ++g) {
+            if (players[g] > 3 || zobrist_index[g] < 0 || zobrist_index[g] >= n_zobrist || mt_state[(size_t)g * 625 + 624] > 624)
+                return set_err(h, BK_EINVAL, "bk_mcts: bad player / zobrist_index / mt pos%s", "");
+            for (int q = 0; q < 4; ++q)
+                if (root_sets[g].mask[q] + 1u > BK_FSET_SLOTS)
+                    return set_err(h, BK_EINVAL, "bk_mcts: root frontier table too large%s", "");
+            if (cfg->use_tt && (tt_count[g] < 0 || tt_count[g] >= cfg->tt_cap))
+                return set_err(h, BK_EINVAL, "bk_mcts: bad tt_count%s", "");
+        }
+    }
+    HIPCHK(h, hipSetDevice(h->device));
+    const size_t n = (size_t)n_games, ttc = cfg->use_tt ? (size_t)cfg->tt_cap : 0;
+    const size_t it = (size_t)cfg->iterations;
+    struct Sec { const void* host; size_t bytes; int dir; void* dev; };  // dir: 1 in, 2 out, 3 in+out
+    Sec sec[] = {
+        {roots, sizeof(bk_state) * n, 1, nullptr},
+        {root_sets, sizeof(bk_fset) * n, 1, nullptr},
+        {players, n, 1, nullptr},
+        {root_hash, sizeof(uint64_t) * n, 1, nullptr},
+        {zobrist, sizeof(uint64_t) * MC_ZOB * (size_t)n_zobrist, 1, nullptr},
+        {zobrist_index, sizeof(int32_t) * n, 1, nullptr},
+        {mt_state, sizeof(uint32_t) * 625 * n, 3, nullptr},
+        {tt_keys, sizeof(uint64_t) * ttc * n, 3, nullptr},
+        {tt_vals, sizeof(double) * ttc * n, 3, nullptr},
+        {tt_count, cfg->use_tt ? sizeof(int32_t) * n : 0, 3, nullptr},
+        {log_table, sizeof(double) * (size_t)log_len, 1, nullptr},
+        {nodes, sizeof(bk_mcts_node) * (size_t)cfg->node_cap * n, 2, nullptr},
+        {rewards, sizeof(double) * it * n, 2, nullptr},
+        {hit_flags, it * n, 2, nullptr},
+        {out, sizeof(bk_mcts_out) * n, 2, nullptr},
+    };
+    const int NSEC = (int)(sizeof sec / sizeof sec[0]);
+    const int NODES = 11;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    size_t tot = 0;
+    for (int i = 0; i < NSEC; ++i) {
+        const bool staged = mem == BK_MEM_HOST || (i == NODES && nodes == nullptr);
+        if (staged && sec[i].bytes && (sec[i].host || i == NODES)) tot += al(sec[i].bytes);
+    }
+    int rc = grow(h, &h->d_mc, &h->d_mc_cap, tot + 256);
+    if (rc) return rc;
+    char* p = (char*)h->d_mc;
+    for (int i = 0; i < NSEC; ++i) {
+        const bool staged = mem == BK_MEM_HOST || (i == NODES && nodes == nullptr);
+        if (!staged) { sec[i].dev = const_cast<void*>(sec[i].host); continue; }
+        if (!sec[i].bytes || (!sec[i].host && i != NODES)) { sec[i].dev = nullptr; continue; }
+        sec[i].dev = p;
+        if ((sec[i].dir & 1) && sec[i].host)
+            HIPCHK(h, hipMemcpyAsync(p, sec[i].host, sec[i].bytes, hipMemcpyHostToDevice, h->cur));
+        p += al(sec[i].bytes);
+    }
+    // persistent grid: every resident slot pulls whole searches from the counter
+    int blocks = h->num_cu * 2;
+    const int need = (n_games + BLOCK - 1) / BLOCK;
+    if (blocks > need) blocks = need;
+    if (blocks < 1) blocks = 1;
+    const uint32_t nslots = (uint32_t)blocks * BLOCK;
+    rc = grow(h, &h->d_slab, &h->d_slab_cap, sizeof(uint32_t) * SLAB_WORDS * (size_t)nslots);
+    if (rc) return rc;
+    rc = grow(h, &h->d_mclane, &h->d_mclane_cap, sizeof(McLane) * (size_t)nslots);
+    if (rc) return rc;
+    int khz = 0;
+    HIPCHK(h, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
+    if (khz <= 0) khz = 100000;
+    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
+    const uint64_t per_lane = ((uint64_t)n_games + nslots - 1) / nslots + 1;
+    const uint64_t steps = per_lane * ((uint64_t)cfg->iterations + 1) * ((uint64_t)cfg->max_rollout_moves + 2) + 64;
+    MctsArgs a{(const bk_state*)sec[0].dev, (const bk_fset*)sec[1].dev, (const uint8_t*)sec[2].dev,
+               (const uint64_t*)sec[3].dev, n_games, *cfg, (const uint64_t*)sec[4].dev,
+               (const int32_t*)sec[5].dev, (uint32_t*)sec[6].dev, (uint64_t*)sec[7].dev, (double*)sec[8].dev,
+               (int32_t*)sec[9].dev, (const double*)sec[10].dev, log_len, (bk_mcts_node*)sec[11].dev,
+               (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
+               (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
+               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u};
+    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
+    h->timed = true;
+    uint32_t ctr[4];
+    if (mem == BK_MEM_HOST) {
+        for (int i = 0; i < NSEC; ++i)
+            if ((sec[i].dir & 2) && sec[i].host && sec[i].bytes)
+                HIPCHK(h, hipMemcpyAsync(const_cast<void*>(sec[i].host), sec[i].dev, sec[i].bytes,
+                                         hipMemcpyDeviceToHost, h->cur));
+    }
+    HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
+    if (ctr[1]) return set_err(h, BK_EOVERFLOW, "bk_mcts: step guard tripped%s", "");
     return BK_OK;
 }
 

@@ -215,6 +215,132 @@ class BlokusGPU:
                              vis.ctypes.data if vis is not None else 0, N.MEM_HOST)
         return (out, vis[: int(off[-1])]) if want_visits else out
 
+    # ------------------------------------------------------------------ MCTSAgent
+    def mcts(self, roots, root_sets, players, root_hash, *, iterations: int, zobrist, mt_state,
+             zobrist_index=None, tt: "MctsTT" = None, max_rollout_moves: int = 50, exploration: float = 1.414,
+             log_table=None, node_cap: int = 0, time_limit_us: int = 0, want_rewards: bool = True,
+             want_nodes: bool = False):
+        """MCTSAgent.select_action searches for a batch of positions, whole on the GPU
+        (bk_mcts; mcts/mcts_agent.py:304-582 with RandomAgent rollouts).
+
+        roots / root_sets / players / root_hash: per game (STATE_DTYPE, FSET_DTYPE, the
+        searching player 0..3, ZobristHash.hash_board).  zobrist: uint64[n_tables, 2088]
+        key tables (cells x 5, turn x 4, player x piece), zobrist_index[g] picks one.
+        mt_state: uint32[n, 625] numpy MT19937 states (key then pos), advanced in place.
+        tt: an MctsTT (one table per game, kept across calls) or None (no TT).
+        Returns dict(out=MCTS_OUT_DTYPE[n], rewards, hit_flags, nodes).  A search that
+        outgrows its node pool is re-run from the saved inputs with a larger pool."""
+        n = len(roots)
+        roots = np.ascontiguousarray(roots, dtype=STATE_DTYPE)
+        root_sets = np.ascontiguousarray(root_sets, dtype=N.FSET_DTYPE)
+        pl = np.ascontiguousarray(players, dtype=np.uint8)
+        rh = np.ascontiguousarray(np.asarray(root_hash, dtype=np.uint64))
+        zob = np.ascontiguousarray(np.asarray(zobrist, dtype=np.uint64).reshape(-1, N.MCTS_ZOBRIST_WORDS))
+        zi = np.zeros(n, np.int32) if zobrist_index is None else np.ascontiguousarray(zobrist_index, dtype=np.int32)
+        assert mt_state.dtype == np.uint32 and mt_state.shape == (n, 625) and mt_state.flags.c_contiguous
+        assert len(root_sets) == n and len(pl) == n and len(rh) == n and len(zi) == n
+        if log_table is None:
+            log_table = mcts_log_table(iterations)
+        lt = np.ascontiguousarray(log_table, dtype=np.float64)
+        if tt is not None:
+            tt.reserve(iterations + 1)
+            assert tt.keys.shape[0] == n
+        cap = int(node_cap) or 1 + (iterations + 1) * 256
+        mt0 = mt_state.copy()
+        tt0 = tt.snapshot() if tt is not None else None
+        while True:
+            cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(tt is not None), cap,
+                              tt.cap if tt is not None else 0, int(time_limit_us))
+            out = np.zeros(n, dtype=N.MCTS_OUT_DTYPE)
+            rewards = np.zeros((n, max(iterations, 1))) if want_rewards else None
+            flags = np.zeros((n, max(iterations, 1)), np.uint8) if want_rewards else None
+            nodes = np.zeros((n, cap), dtype=N.MCTS_NODE_DTYPE) if want_nodes else None
+            ptr = lambda x: x.ctypes.data if x is not None else 0  # noqa: E731
+            self.handle.set_stream(None)
+            self.handle.mcts(roots.ctypes.data, root_sets.ctypes.data, pl.ctypes.data, rh.ctypes.data, n, cfg,
+                             zob.ctypes.data, len(zob), zi.ctypes.data, mt_state.ctypes.data,
+                             ptr(tt.keys) if tt is not None else 0, ptr(tt.vals) if tt is not None else 0,
+                             ptr(tt.count) if tt is not None else 0, lt.ctypes.data, len(lt), ptr(nodes),
+                             ptr(rewards), ptr(flags), out.ctypes.data, N.MEM_HOST)
+            st = out["status"]
+            if (st & N.MCTS_EPOOL).any() and not (st & ~np.uint32(N.MCTS_EPOOL)).any():
+                mt_state[:] = mt0  # roll back and retry with a bigger pool
+                if tt is not None:
+                    tt.restore(tt0)
+                cap = cap * 2 + 1
+                continue
+            if st.any():
+                raise RuntimeError(f"bk_mcts: search stopped early, status bits {sorted(set(st[st != 0].tolist()))}")
+            return {"out": out, "rewards": rewards, "hit_flags": flags, "nodes": nodes, "node_cap": cap}
+
+
+def mcts_log_table(iterations: int) -> np.ndarray:
+    """log_table[v] = np.log(v): the exact doubles numpy's log gives UCB1
+    (mcts_agent.py:86); index 0 is unused."""
+    t = np.zeros(iterations + 2)
+    t[1:] = np.log(np.arange(1, iterations + 2, dtype=np.float64))
+    return t
+
+
+class MctsTT:
+    """Per-game Zobrist transposition tables for bk_mcts (mcts/zobrist.py:155-220 as
+    open addressing: slot = key & (cap - 1), linear probing, NaN value = empty)."""
+
+    def __init__(self, n_games: int, cap: int = 1 << 12):
+        assert cap >= 2 and cap & (cap - 1) == 0
+        self.keys = np.zeros((n_games, cap), np.uint64)
+        self.vals = np.full((n_games, cap), np.nan)
+        self.count = np.zeros(n_games, np.int32)
+
+    @property
+    def cap(self) -> int:
+        return self.keys.shape[1]
+
+    def snapshot(self):
+        return self.keys.copy(), self.vals.copy(), self.count.copy()
+
+    def restore(self, snap):
+        self.keys, self.vals, self.count = (x.copy() for x in snap)
+
+    def clear(self, g=None):
+        sl = slice(None) if g is None else g
+        self.keys[sl] = 0
+        self.vals[sl] = np.nan
+        self.count[sl] = 0
+
+    def items(self, g: int):
+        live = ~np.isnan(self.vals[g])
+        return self.keys[g][live], self.vals[g][live]
+
+    def reserve(self, extra: int):
+        """Grow (rehash) so every table stays at most half full after `extra` inserts."""
+        need = int(self.count.max(initial=0)) + int(extra) + 1
+        cap = self.cap
+        while need * 2 > cap:
+            cap *= 2
+        if cap == self.cap:
+            return
+        n = self.keys.shape[0]
+        keys = np.zeros((n, cap), np.uint64)
+        vals = np.full((n, cap), np.nan)
+        for g in range(n):
+            k, v = self.items(g)
+            slot = (k & np.uint64(cap - 1)).astype(np.int64)
+            todo = np.arange(len(k))
+            while len(todo):  # place one key per free slot per round, others probe on
+                cand = slot[todo]
+                free = np.isnan(vals[g, cand])
+                _, first = np.unique(cand, return_index=True)
+                win = np.zeros(len(todo), bool)
+                win[first] = True
+                win &= free
+                keys[g, cand[win]] = k[todo[win]]
+                vals[g, cand[win]] = v[todo[win]]
+                rest = todo[~win]
+                slot[rest] = (slot[rest] + 1) % cap
+                todo = rest
+        self.keys, self.vals = keys, vals
+
 
 def empty_state() -> np.ndarray:
     """The initial position (engine/board.py:54-78): nobody has moved, RED to play."""

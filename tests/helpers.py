@@ -87,3 +87,24 @@ def fset_of(rec):
         b.place_piece([Position(r, c) for r, c in cells], Player(player_value), piece_id, validate=False)
         N.fset_place(fs, pack_state(b), player_value - 1, [r * 20 + c for r, c in cells])
     return fs[0]
+
+
+def oracle_fset(b):
+    """An oracle board's CPython frontier tables as one bk_fset record (same slot
+    encoding: -1 unused, -2 dummy, else r*20+c)."""
+    fs = np.zeros(1, dtype=N.FSET_DTYPE)[0]
+    for p in range(4):
+        s = b.fr[p]
+        assert s.mask + 1 <= N.FSET_SLOTS
+        fs["key"][p, :] = -1
+        fs["key"][p, : s.mask + 1] = np.ctypeslib.as_array(s.key)[: s.mask + 1]
+        fs["mask"][p], fs["fill"][p], fs["used"][p] = s.mask, s.fill, s.used
+    return fs
+
+
+def mt_array(m):
+    """An oracle MT (numpy RandomState stream) as bk_mcts's uint32[625] (key, pos)."""
+    a = np.zeros(625, np.uint32)
+    a[:624] = np.ctypeslib.as_array(m.mt)
+    a[624] = m.mti
+    return a
