@@ -312,6 +312,15 @@ class MctsTT:
         live = ~np.isnan(self.vals[g])
         return self.keys[g][live], self.vals[g][live]
 
+    def load(self, g: int, keys, vals):
+        """Replace table g's contents with the given (key, reward) entries."""
+        keys = np.asarray(keys, np.uint64)
+        while 2 * (len(keys) + 1) > self.cap:
+            self.reserve(self.cap)
+        self.clear(g)
+        _insert(self.keys[g], self.vals[g], keys, np.asarray(vals, np.float64))
+        self.count[g] = len(keys)
+
     def reserve(self, extra: int):
         """Grow (rehash) so every table stays at most half full after `extra` inserts."""
         need = int(self.count.max(initial=0)) + int(extra) + 1
@@ -324,22 +333,28 @@ class MctsTT:
         keys = np.zeros((n, cap), np.uint64)
         vals = np.full((n, cap), np.nan)
         for g in range(n):
-            k, v = self.items(g)
-            slot = (k & np.uint64(cap - 1)).astype(np.int64)
-            todo = np.arange(len(k))
-            while len(todo):  # place one key per free slot per round, others probe on
-                cand = slot[todo]
-                free = np.isnan(vals[g, cand])
-                _, first = np.unique(cand, return_index=True)
-                win = np.zeros(len(todo), bool)
-                win[first] = True
-                win &= free
-                keys[g, cand[win]] = k[todo[win]]
-                vals[g, cand[win]] = v[todo[win]]
-                rest = todo[~win]
-                slot[rest] = (slot[rest] + 1) % cap
-                todo = rest
+            _insert(keys[g], vals[g], *self.items(g))
         self.keys, self.vals = keys, vals
+
+
+def _insert(tkeys: np.ndarray, tvals: np.ndarray, k: np.ndarray, v: np.ndarray) -> None:
+    """Linear-probing inserts of distinct keys into one table row (NaN = empty slot):
+    each round places one key per free slot, the others probe on."""
+    cap = len(tkeys)
+    slot = (k & np.uint64(cap - 1)).astype(np.int64)
+    todo = np.arange(len(k))
+    while len(todo):
+        cand = slot[todo]
+        free = np.isnan(tvals[cand])
+        _, first = np.unique(cand, return_index=True)
+        win = np.zeros(len(todo), bool)
+        win[first] = True
+        win &= free
+        tkeys[cand[win]] = k[todo[win]]
+        tvals[cand[win]] = v[todo[win]]
+        rest = todo[~win]
+        slot[rest] = (slot[rest] + 1) % cap
+        todo = rest
 
 
 def empty_state() -> np.ndarray:

@@ -6,12 +6,18 @@ transposition cache follow mcts/mcts_agent.py:19-191, :304-437, :572-582.
 
 Rollouts (mcts/mcts_agent.py:470-554, <= max_rollout_moves plies, stop at the first
 player without a move, reward = final - initial Board.get_score of the root player)
-have two GPU backends:
+have three GPU backends:
 
-* ``rollout_backend="exact"`` (default when a rollout_agent with ``select_action`` is
-  given, e.g. RandomAgent): the ply loop runs on the host, every legal-move list
-  comes from the GPU in the reference's frontier order and the agent draws from its
-  own stream -- bit-identical to the reference for RandomAgent.
+* ``rollout_backend="search"`` (default when the rollout_agent is a RandomAgent): the
+  WHOLE search -- selection, expansion, TT lookups, RandomAgent rollouts,
+  backpropagation -- runs in one bk_mcts launch (k_mcts), bit-identical to the
+  reference: frontier-order legal lists, the agent's numpy MT19937 stream (read from
+  and written back to ``rollout_agent.rng``), the Zobrist TT kept in device-layout
+  tables across calls.  ``search_batch`` runs many agents' searches in one launch.
+* ``rollout_backend="exact"`` (a rollout_agent with ``select_action``): the tree and
+  the ply loop run on the host, every legal-move list comes from the GPU in the
+  reference's frontier order and the agent draws from its own stream -- bit-identical
+  to the reference for RandomAgent, usable with any agent.
 * ``rollout_backend="kernel"`` (default without a rollout_agent): the whole playout
   runs inside the persistent HIP rollout kernel (bk_rollout, BK_SEM_ROLLOUT, Philox
   stream, naive move order): statistically the same random playout, not the same
@@ -28,7 +34,7 @@ from typing import Any, Dict, List, Optional
 import numpy as np
 
 from ..engine.board import Board, Player, Position, _PLAYERS, pack_state
-from ..engine.move_generator import Move, get_shared_generator
+from ..engine.move_generator import Move, get_shared_generator, int_to_move
 from ..engine.pieces import PieceGenerator
 from .zobrist import TranspositionTable, ZobristHash
 
@@ -112,16 +118,24 @@ class MCTSAgent:
         self.piece_generator = PieceGenerator()
         self.zobrist_hash = ZobristHash(seed=seed)
         self.rollout_agent = rollout_agent
-        self.rollout_backend = rollout_backend or ("exact" if rollout_agent is not None else "kernel")
-        if self.rollout_backend not in ("exact", "kernel"):
-            raise ValueError("rollout_backend must be 'exact' or 'kernel'")
+        from ..agents.random_agent import RandomAgent
+        if rollout_backend is None:
+            rollout_backend = ("search" if isinstance(rollout_agent, RandomAgent) else
+                               "exact" if rollout_agent is not None else "kernel")
+        self.rollout_backend = rollout_backend
+        if self.rollout_backend not in ("search", "exact", "kernel"):
+            raise ValueError("rollout_backend must be 'search', 'exact' or 'kernel'")
         if self.rollout_backend == "exact" and rollout_agent is None:
             raise ValueError("rollout_backend='exact' needs a rollout_agent")
+        if self.rollout_backend == "search" and not isinstance(rollout_agent, RandomAgent):
+            raise ValueError("rollout_backend='search' needs a RandomAgent rollout_agent (its numpy stream "
+                             "is replayed on the GPU)")
         self.seed = 0 if seed is None else int(seed)
         self._kernel_calls = 0
         self.device = device
         self._gpu = None
         self.transposition_table = TranspositionTable() if use_transposition_table else None
+        self._gpu_tt = None  # "search" backend: the TT as a device-layout open-addressing table
         self.stats = self._fresh_stats()
 
     @staticmethod
@@ -135,6 +149,8 @@ class MCTSAgent:
             return None
         if len(legal_moves) == 1:
             return legal_moves[0]
+        if self.rollout_backend == "search":
+            return MCTSAgent.search_batch([self], [board], [player], [legal_moves])[0]
         t0 = time.time()
         root = MCTSNode(board, player)
         if self.time_limit:
@@ -152,6 +168,94 @@ class MCTSAgent:
         if self.transposition_table and len(self.transposition_table.table) > 500000:
             self.transposition_table.clear()
         return best
+
+    @staticmethod
+    def search_batch(agents: List["MCTSAgent"], boards: List[Board], players: List[Player],
+                     legal_moves: Optional[List[List[Move]]] = None) -> List[Optional[Move]]:
+        """select_action for several "search"-backend agents in ONE bk_mcts launch (one
+        search per agent; an agent appears at most once).  Each result equals the
+        agent's own select_action on that position: the search reads and advances the
+        agent's rollout stream and TT, and updates its stats, exactly as the
+        reference's select_action (mcts/mcts_agent.py:304-341) does.  Positions with
+        < 2 legal moves are answered without a search (:313-318); ``legal_moves[i]`` is
+        the caller's legal list for position i (generated here when omitted)."""
+        from .. import _native as N
+        from ..gpu import BlokusGPU, MctsTT
+        from .zobrist import flat_keys, hash_states
+        assert len(agents) == len(boards) == len(players)
+        assert len({id(a) for a in agents}) == len(agents), "one search per agent per launch"
+        out: List[Optional[Move]] = [None] * len(agents)
+        todo = []
+        gen = get_shared_generator()
+        for i, (a, b, p) in enumerate(zip(agents, boards, players)):
+            if a.rollout_backend != "search":
+                raise ValueError("search_batch needs rollout_backend='search' agents")
+            legal = legal_moves[i] if legal_moves is not None else gen.get_legal_moves(b, p)
+            if len(legal) <= 1:
+                out[i] = legal[0] if legal else None
+            else:
+                todo.append(i)
+        if not todo:
+            return out
+        groups = {}  # agents sharing (iterations, rollout cap, c, TT on/off) share a launch
+        for i in todo:
+            a = agents[i]
+            if a.time_limit:
+                raise ValueError("rollout_backend='search' runs a fixed iteration count (time_limit unsupported)")
+            key = (int(a.iterations), a.max_rollout_moves, float(a.exploration_constant), a.use_transposition_table)
+            groups.setdefault(key, []).append(i)
+        for (iters, max_roll, c, use_tt), idx in groups.items():
+            ags = [agents[i] for i in idx]
+            gpu = ags[0]._gpu = ags[0]._gpu or BlokusGPU(ags[0].device)
+            roots = np.concatenate([pack_state(boards[i]) for i in idx])
+            sets = np.concatenate([boards[i].frontier_tables for i in idx])
+            pl = np.array([players[i].value - 1 for i in idx], np.uint8)
+            tabs, zidx = [], []
+            for a in ags:
+                tabs.append(flat_keys(a.zobrist_hash))
+                zidx.append(len(tabs) - 1)
+            zob = np.stack(tabs)
+            rh = np.array([hash_states(roots[j:j + 1], zob[j])[0] for j in range(len(idx))], np.uint64)
+            mt = np.zeros((len(idx), 625), np.uint32)
+            rng_states = [a.rollout_agent.rng.get_state() for a in ags]
+            for j, st in enumerate(rng_states):
+                mt[j, :624] = st[1]
+                mt[j, 624] = st[2]
+            tt = None
+            if use_tt:
+                tt = MctsTT(len(idx), cap=max([a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12]))
+                for j, a in enumerate(ags):
+                    if a._gpu_tt is not None and a._gpu_tt.count[0]:
+                        tt.load(j, *a._gpu_tt.items(0))
+            t0 = time.time()
+            r = gpu.mcts(roots, sets, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
+                         mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c)
+            dt = time.time() - t0
+            for j, (i, a) in enumerate(zip(idx, ags)):
+                o = r["out"][j]
+                st = rng_states[j]
+                a.rollout_agent.rng.set_state((st[0], mt[j, :624].copy(), int(mt[j, 624]), st[3], st[4]))
+                hits = r["hit_flags"][j, :int(o["iterations_run"])]
+                rew = r["rewards"][j, :int(o["iterations_run"])]
+                a.stats["iterations_run"] = int(o["iterations_run"])
+                a.stats["time_elapsed"] = dt
+                a.stats["transposition_hits"] += int(o["tt_hits"])
+                a.stats["rollout_rewards"].extend(float(x) for x in rew[hits == 0])
+                if use_tt:
+                    a._gpu_tt = MctsTT(1, cap=tt.cap)
+                    a._gpu_tt.load(0, *tt.items(j))
+                    t = a.transposition_table
+                    t.access_count += int(o["tt_hits"]) + int(o["rollouts"])
+                    t.hit_count += int(o["tt_hits"])
+                    t.gpu_size = int(a._gpu_tt.count[0])
+                    if t.gpu_size > 500000:  # mcts_agent.py:338-339
+                        t.clear()
+                        a._gpu_tt = None
+                out[i] = int_to_move(int(o["best_move"])) if o["best_move"] >= 0 else None
+        return out
+
+    def _get_move_positions(self, move: Move) -> List[Position]:
+        return _positions(move)
 
     def _mcts_iteration(self, root: MCTSNode):
         node = self._selection(root)
@@ -234,6 +338,7 @@ class MCTSAgent:
         self.stats = self._fresh_stats()
         if self.transposition_table:
             self.transposition_table.clear()
+        self._gpu_tt = None
 
     def set_seed(self, seed: int):
         self.zobrist_hash = ZobristHash(seed=seed)

@@ -61,6 +61,7 @@ class TranspositionTable:
         self.table: Dict[int, Dict] = {}
         self.access_count = 0
         self.hit_count = 0
+        self.gpu_size = 0  # entries held in the GPU search backend's device-layout table
 
     def get(self, hash_value: int) -> Optional[Dict]:
         self.access_count += 1
@@ -77,9 +78,39 @@ class TranspositionTable:
 
     def clear(self):
         self.table.clear()
+        self.gpu_size = 0
         self.access_count = 0
         self.hit_count = 0
 
     def get_stats(self) -> Dict[str, float]:
-        return {"size": len(self.table), "max_size": self.max_size, "access_count": self.access_count,
+        return {"size": len(self.table) + self.gpu_size, "max_size": self.max_size, "access_count": self.access_count,
                 "hit_count": self.hit_count, "hit_rate": self.hit_count / max(self.access_count, 1)}
+
+
+def flat_keys(z: ZobristHash) -> np.ndarray:
+    """The 2088-word key table bk_mcts reads: cells x 5 values (row-major, value
+    0 = empty, p = player p), 4 turn keys, 4 x 21 piece keys (mcts/zobrist.py:41-68)."""
+    return np.concatenate([z.position_player_hashes.reshape(-1), z.player_turn_hashes,
+                           z.piece_used_hashes.reshape(-1)]).astype(np.uint64)
+
+
+def hash_states(states: np.ndarray, keys: np.ndarray) -> np.ndarray:
+    """ZobristHash.hash_board (mcts/zobrist.py:70-99) of packed bk_state records,
+    vectorised: XOR of the 400 cell keys, the side-to-move key and the used-piece keys."""
+    states = np.atleast_1d(states)
+    keys = np.asarray(keys, dtype=np.uint64).reshape(-1)
+    n = len(states)
+    cells = np.arange(400)
+    word, bit = cells // 64, (cells % 64).astype(np.uint64)
+    grid = np.zeros((n, 400), np.int64)
+    for p in range(4):
+        occ = (states["planes"][:, p, word] >> bit) & np.uint64(1)
+        grid += occ.astype(np.int64) * (p + 1)
+    h = np.bitwise_xor.reduce(keys[cells * 5 + grid], axis=1)
+    h ^= keys[2000 + states["current_player"].astype(np.int64)]
+    for p in range(4):
+        used = states["used"][:, p].astype(np.int64)
+        for pid in range(21):
+            on = (used >> pid) & 1 == 1
+            h[on] ^= keys[2004 + p * 21 + pid]
+    return h.astype(np.uint64)

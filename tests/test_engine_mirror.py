@@ -129,3 +129,40 @@ def test_board_mirror_carries_frontier_tables(i):
         assert N.fset_list(b.frontier_tables, p) == [r * 20 + cc for r, cc in b.get_frontier(Player(p + 1))]
         assert N.fset_list(c.frontier_tables, p) == [r * 20 + cc for r, cc in c.get_frontier(Player(p + 1))]
     assert pack_fsets([b, c]).shape == (2,)
+
+
+def test_hash_states_matches_reference_zobrist():
+    """mcts.zobrist.hash_states (vectorised ZobristHash.hash_board over packed states,
+    the bk_mcts root hash) against the reference's hashes (tests/golden/zobrist.json)
+    and the host ZobristHash on the same boards."""
+    from tests.conftest import load_golden
+    from reinforcementlearning_blokus_amd.mcts.zobrist import ZobristHash, flat_keys, hash_states
+    for rec in load_golden("zobrist.json"):
+        z = ZobristHash(seed=rec["seed"])
+        keys = flat_keys(z)
+        assert [str(x) for x in keys[:10]] == rec["table_head"]
+        assert [str(x) for x in keys[2000:2004]] == rec["turn"]
+        boards = [engine_board(p) for p in POS[:12]]
+        st = np.concatenate([pack_state(b) for b in boards])
+        got = hash_states(st, keys)
+        assert [str(x) for x in got] == rec["hashes"]
+        assert [int(z.hash_board(b)) for b in boards] == [int(x) for x in got]
+
+
+def test_mcts_tt_load_and_reserve_keep_entries():
+    from reinforcementlearning_blokus_amd.gpu import MctsTT
+    rng = np.random.RandomState(3)
+    keys = np.unique(rng.randint(0, 2**63, size=300, dtype=np.int64).astype(np.uint64))
+    vals = rng.randint(-20, 40, size=len(keys)).astype(np.float64)
+    tt = MctsTT(2, cap=8)
+    tt.load(1, keys, vals)
+    assert tt.cap >= 2 * (len(keys) + 1) and int(tt.count[1]) == len(keys) and int(tt.count[0]) == 0
+    tt.reserve(5000)
+    k, v = tt.items(1)
+    assert dict(zip(k.tolist(), v.tolist())) == dict(zip(keys.tolist(), vals.tolist()))
+    for key, val in zip(keys.tolist(), vals.tolist()):  # every key reachable by linear probing
+        s = key & (tt.cap - 1)
+        while tt.keys[1, s] != key:
+            assert not np.isnan(tt.vals[1, s])
+            s = (s + 1) % tt.cap
+        assert tt.vals[1, s] == val

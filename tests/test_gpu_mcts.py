@@ -129,3 +129,74 @@ def test_pool_overflow_retries_to_the_same_answer(gpu):
                      max_rollout_moves=8)
         res.append((r["out"]["best_move"].tolist(), r["rewards"].tolist(), mt.tolist(), tt.count.tolist()))
     assert res[0] == res[1]
+
+
+def _agent_for(c):
+    from reinforcementlearning_blokus_amd.agents.random_agent import RandomAgent
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
+    a = MCTSAgent(iterations=c["iterations"], rollout_agent=RandomAgent(seed=c["rollout_seed"]),
+                  seed=c["zobrist_seed"], use_transposition_table=c["use_tt"],
+                  max_rollout_moves=c["max_rollout_moves"])
+    assert a.rollout_backend == "search"
+    return a
+
+
+@pytest.mark.parametrize("case", range(len(MCTS)))
+def test_agent_select_action_matches_reference(case):
+    """MCTSAgent.select_action through the drop-in API (host mirror Board + Player,
+    RandomAgent rollout agent, rollout_backend="search" = one bk_mcts launch): the
+    reference's chosen moves, cumulative stats (TT hits, rollout rewards, TT size) and
+    rollout RNG state over two consecutive calls (tests/golden/mcts.json)."""
+    from reinforcementlearning_blokus_amd.engine.board import Player
+    from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator, move_to_int
+    from tests.helpers import engine_board
+    c = MCTS[case]
+    board = engine_board(POS[c["position"]])
+    agent = _agent_for(c)
+    gen = get_shared_generator()
+    for call in c["calls"]:
+        cur = Player(call["player"])
+        legal = gen.get_legal_moves(board, cur)
+        assert len(legal) == call["n_legal"]
+        mv = agent.select_action(board, cur, legal)
+        assert (move_to_int(mv) if mv is not None else None) == call["move"]
+        if call["searched"]:
+            assert agent.stats["iterations_run"] == c["iterations"]
+            assert agent.stats["transposition_hits"] == call["transposition_hits"]
+            assert agent.stats["rollout_rewards"] == call["rollout_rewards"]
+            if c["use_tt"]:
+                assert agent.transposition_table.get_stats()["size"] == call["tt_size"]
+        st = agent.rollout_agent.rng.get_state()
+        assert int(st[2]) == call["rng_pos"] and sha_ints(int(x) for x in st[1]) == call["rng_sha"]
+        if mv is None:
+            break
+        board.place_piece(agent._get_move_positions(mv), cur, mv.piece_id, validate=False)
+
+
+def test_agent_search_batch_equals_sequential():
+    """search_batch (several agents' searches in one launch) == each agent's own
+    select_action, including the RNG streams and TT contents left behind."""
+    from reinforcementlearning_blokus_amd.engine.board import Player
+    from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator, move_to_int
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
+    from tests.helpers import engine_board
+    cases = [c for c in MCTS if c["calls"][0]["searched"]][:8]
+    gen = get_shared_generator()
+
+    def setup():
+        boards = [engine_board(POS[c["position"]]) for c in cases]
+        return [_agent_for(c) for c in cases], boards, [Player(c["calls"][0]["player"]) for c in cases]
+
+    a1, b1, p1 = setup()
+    seq = [a.select_action(b, p, gen.get_legal_moves(b, p)) for a, b, p in zip(a1, b1, p1)]
+    a2, b2, p2 = setup()
+    bat = MCTSAgent.search_batch(a2, b2, p2)
+    assert [move_to_int(m) for m in seq] == [move_to_int(m) for m in bat]
+    for x, y in zip(a1, a2):
+        sx, sy = x.rollout_agent.rng.get_state(), y.rollout_agent.rng.get_state()
+        assert sx[2] == sy[2] and np.array_equal(sx[1], sy[1])
+        assert x.stats["rollout_rewards"] == y.stats["rollout_rewards"]
+        if x._gpu_tt is not None:
+            kx, vx = x._gpu_tt.items(0)
+            ky, vy = y._gpu_tt.items(0)
+            assert dict(zip(kx.tolist(), vx.tolist())) == dict(zip(ky.tolist(), vy.tolist()))
