@@ -315,6 +315,11 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
    stream, measured with HIP events around that launch. */
 int bk_last_kernel_ms(bk_handle h, float* ms);
 
+/* Diagnostics (no reference counterpart): per-section shader-clock cycles summed over
+   waves since the last reset, from a library built with -DBK_SECTION_PROF
+   (tools/sections.py).  The product build returns BK_EINVAL and zeros. */
+int bk_debug_sections(bk_handle h, uint64_t* out, int32_t n, int32_t reset);
+
 #ifdef __cplusplus
 }
 #endif

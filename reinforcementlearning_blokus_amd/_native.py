@@ -30,7 +30,7 @@ EXPORTS = (
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
-    "bk_mcts",
+    "bk_mcts", "bk_debug_sections",
 )
 FSET_SLOTS = 256
 # bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
@@ -145,6 +145,7 @@ def load():
                                               vp, C.c_int]),
             "bk_mcts": (C.c_int, [vp, vp, vp, vp, vp, C.c_int32, P(BkMctsCfg), vp, C.c_int32, vp, vp, vp, vp,
                                   vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int]),
+            "bk_debug_sections": (C.c_int, [vp, vp, C.c_int32, C.c_int32]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)

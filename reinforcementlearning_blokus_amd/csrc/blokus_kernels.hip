@@ -44,6 +44,22 @@
 #include "orient_table.h"
 
 #define BK_TABLES_VERSION 1
+
+// Section timers (diagnostic build only, -DBK_SECTION_PROF): per-wave shader-clock
+// cycles spent in each section of a kernel's loop, summed over waves into
+// g_sections[] (read with bk_debug_sections).  Compiled out of the product build.
+#define BK_NSECT 16
+#ifdef BK_SECTION_PROF
+__device__ unsigned long long g_sections[BK_NSECT];
+#define SECT_DECL uint64_t sect_acc[BK_NSECT] = {0}; uint64_t sect_t = clock64();
+#define SECT(i) do { const uint64_t now_ = clock64(); sect_acc[i] += now_ - sect_t; sect_t = now_; } while (0)
+#define SECT_FLUSH do { if ((threadIdx.x & (WAVE - 1)) == 0) for (int i_ = 0; i_ < BK_NSECT; ++i_) \
+        if (sect_acc[i_]) atomicAdd(&g_sections[i_], (unsigned long long)sect_acc[i_]); } while (0)
+#else
+#define SECT_DECL
+#define SECT(i) do {} while (0)
+#define SECT_FLUSH do {} while (0)
+#endif
 #define WAVE 64
 #define BLOCK 256
 #define ROWMASK 0x000FFFFFu  // columns 0..19
@@ -426,38 +442,56 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
         uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
         ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
         ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
-        rows[r * WAVE].x = r <= rlim ? (ac & ~ab) : 0u;
+        // the anchors go to the C half: row r's C word is not read again (later rows
+        // read rows >= r + 1), and the B half stays intact for frontier_addable
+        rows[r * WAVE].y = r <= rlim ? (ac & ~ab) : 0u;
     }
+    // Pass 2 reads the table 16 slots per pair of uint4 loads into registers, all
+    // indices static (a dynamically indexed key array would live in scratch memory)
     int found_r = -1, found_c = 0;
     uint32_t cnt = 0;
     const uint4* k4 = reinterpret_cast<const uint4*>(key);
 #pragma unroll 1
-    for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 32) {  // 32 slots per batch of loads
-        uint4 q[4];
+    for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 16) {
+        const uint4 qa = k4[b0 >> 3], qb = k4[(b0 >> 3) + 1];
+        const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[j] = k4[(b0 >> 3) + j];
-#pragma unroll 1
-        for (int j = 0; j < 32 && found_r < 0; ++j) {
-            const uint4 w4 = q[j >> 3];
-            const uint32_t w = ((j >> 1) & 3) == 0 ? w4.x : ((j >> 1) & 3) == 1 ? w4.y : ((j >> 1) & 3) == 2 ? w4.z : w4.w;
-            const int f = (int)(int16_t)((j & 1) ? (w >> 16) : (w & 0xFFFFu));
-            if (f < 0) continue;
+        for (int j = 0; j < 16; ++j) {
+            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            if (found_r >= 0 || f < 0 || b0 + j > mask) continue;
             const int fr = f / 20, fc = f - 20 * fr;
-#pragma unroll 1
-            for (int k = 0; k < n; ++k) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                if (k >= n || found_r >= 0) continue;
                 const int ar = fr - cd[k], acl = fc - (int)sh[k];
                 if (ar < 0 || ar > 19 || acl < 0 || acl > 19) continue;
                 uint2* rp = rows + ar * WAVE;
-                const uint32_t okw = rp->x;
+                const uint32_t okw = rp->y;
                 if (!((okw >> acl) & 1u)) continue;
-                if (cnt == kk) { found_r = ar; found_c = acl; break; }
-                rp->x = okw & ~(1u << acl);
+                if (cnt == kk) { found_r = ar; found_c = acl; continue; }
+                rp->y = okw & ~(1u << acl);
                 ++cnt;
             }
         }
     }
     out_r = found_r;
     out_c = found_c;
+}
+
+// After locate_move_frontier (B half of the LDS rows = the mover's blocked rows BEFORE
+// the move): the cells update_frontier_after_move may add for the placed piece, i.e.
+// empty and not orthogonally adjacent to the mover on the board AFTER the move
+// (engine/board.py:340-352), for rows ar - 1 .. ar + 5 (A[i] = row ar - 1 + i).
+// m[d] = the piece's cells in row ar + d.
+__device__ __forceinline__ void frontier_addable(const uint2* rows, int ar, const uint32_t (&m)[5], uint32_t (&A)[7]) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const int R = ar - 1 + i;
+        const uint32_t pr = (i >= 1 && i <= 5) ? m[i - 1] : 0u;
+        const uint32_t up = (i >= 2) ? m[i - 2] : 0u, dn = (i <= 4) ? m[i] : 0u;
+        const uint32_t b = (R >= 0 && R <= 19) ? rows[(R < 0 ? 0 : R > 19 ? 19 : R) * WAVE].x : ~0u;
+        A[i] = ~(b | pr | (pr << 1) | (pr >> 1) | up | dn) & ROWMASK;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -681,9 +715,13 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
     return true;
 }
 
-// set_add_entry: an existing key is a no-op; a new key takes the LAST dummy seen on its
-// probe chain, else the unused slot that ended the search (then maybe resize)
-__host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
+// One probe routine for both set operations, so kernels carry a single copy of the
+// probe loop (set_lookkey / set_add_entry / set_discard_entry, Objects/setobject.c):
+// * add: an existing key is a no-op; a new key takes the LAST dummy seen on its probe
+//   chain, else the unused slot that ended the search (then maybe resize);
+// * discard: the key's slot becomes a dummy (absent key: no-op).
+// false: the table outgrew its storage (add only).
+__host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
     const uint64_t h = t.hash[k];
     const uint32_t mask = *t.mask;
     uint64_t perturb = h;
@@ -696,7 +734,13 @@ __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
         for (;;) {
             const int16_t kk = t.at(e);
             if (kk == FS_UNUSED) { unused = true; break; }
-            if (kk == k) return true;
+            if (kk == k) {
+                if (!add) {
+                    t.at(e) = FS_DUMMY;
+                    *t.used -= 1;
+                }
+                return true;
+            }
             if (kk == FS_DUMMY) freeslot = (int64_t)e;
             ++e;
             if (probes-- == 0) break;
@@ -705,6 +749,7 @@ __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
         perturb >>= FS_SHIFT;
         i = (i * 5 + 1 + perturb) & mask;
     }
+    if (!add) return true;
     if (freeslot >= 0) {
         *t.used += 1;
         t.at(freeslot) = k;
@@ -717,30 +762,8 @@ __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) {
     return fs_resize(t, tmp, *t.used > 50000 ? *t.used * 2u : *t.used * 4u);
 }
 
-// set_discard_entry: the key's slot becomes a dummy
-__host__ __device__ inline void fs_discard(FsetRef t, int16_t k) {
-    const uint64_t h = t.hash[k];
-    const uint32_t mask = *t.mask;
-    uint64_t perturb = h;
-    uint64_t i = h & mask;
-    for (;;) {
-        uint64_t e = i;
-        int probes = (i + FS_PROBES <= mask) ? FS_PROBES : 0;
-        for (;;) {
-            const int16_t kk = t.at(e);
-            if (kk == FS_UNUSED) return;
-            if (kk == k) {
-                t.at(e) = FS_DUMMY;
-                *t.used -= 1;
-                return;
-            }
-            ++e;
-            if (probes-- == 0) break;
-        }
-        perturb >>= FS_SHIFT;
-        i = (i * 5 + 1 + perturb) & mask;
-    }
-}
+__host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) { return fs_op(t, tmp, k, true); }
+__host__ __device__ inline void fs_discard(FsetRef t, int16_t k) { fs_op(t, nullptr, k, false); }
 
 __host__ __device__ inline void fs_clear(FsetRef t) {
     for (uint32_t i = 0; i < t.cap; ++i) t.at(i) = FS_UNUSED;
@@ -751,29 +774,44 @@ __host__ __device__ inline void fs_clear(FsetRef t) {
 
 // update_frontier_after_move for player p, engine/board.py:315-367.  occ(r, c) / own(r, c)
 // read the board AFTER all the piece's cells were written.  false: table overflow.
-template <typename Occ, typename Own>
-__host__ __device__ inline bool fs_place(FsetRef t, int16_t* tmp, const int32_t* cells, int n, Occ occ, Own own) {
-    const int DR[4] = {-1, -1, 1, 1}, DC[4] = {-1, 1, -1, 1};  // diagonal, reference order
-    const int OR_[4] = {-1, 1, 0, 0}, OC[4] = {0, 0, -1, 1};    // orthogonal, reference order
-    for (int i = 0; i < n; ++i) {
+// addable(nr, nc): the in-bounds diagonal neighbour is empty and not orthogonally
+// adjacent to the mover (both on the board after the move).  The op sequence (discard
+// the cell, add its diagonals, discard its orthogonals, cell by cell) is the reference's.
+template <typename Add>
+__host__ __device__ inline bool fs_place_pred(FsetRef t, int16_t* tmp, const int32_t* cells, int n, Add addable) {
+    // fully unrolled (static cell / op indices): measured faster on gfx950 than a
+    // compact runtime op loop, whose divergent-loop bookkeeping costs more than the
+    // larger code (the I-cache miss rate stays ~0.1 %, profiles/r01_pmc_frontier)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        if (i >= n) break;
         const int r = cells[i] / 20, c = cells[i] % 20;
-        fs_discard(t, (int16_t)cells[i]);
-        for (int d = 0; d < 4; ++d) {
-            const int nr = r + DR[d], nc = c + DC[d];
-            if (nr < 0 || nr >= 20 || nc < 0 || nc >= 20 || occ(nr, nc)) continue;
-            bool orth = false;
-            for (int e = 0; e < 4 && !orth; ++e) {
-                const int qr = nr + OR_[e], qc = nc + OC[e];
-                if (qr >= 0 && qr < 20 && qc >= 0 && qc < 20 && own(qr, qc)) orth = true;
-            }
-            if (!orth && !fs_add(t, tmp, (int16_t)(nr * 20 + nc))) return false;
-        }
-        for (int d = 0; d < 4; ++d) {
-            const int nr = r + OR_[d], nc = c + OC[d];
-            if (nr >= 0 && nr < 20 && nc >= 0 && nc < 20) fs_discard(t, (int16_t)(nr * 20 + nc));
+#pragma unroll
+        for (int o = 0; o < 9; ++o) {
+            // o = 0: the cell; 1..4: diagonals (-1,-1) (-1,1) (1,-1) (1,1), added when
+            // addable; 5..8: orthogonals (-1,0) (1,0) (0,-1) (0,1), discarded
+            const bool add = o >= 1 && o <= 4;
+            const int nr = r + (o == 1 || o == 2 || o == 5 ? -1 : o == 3 || o == 4 || o == 6 ? 1 : 0);
+            const int nc = c + (o == 1 || o == 3 || o == 7 ? -1 : o == 2 || o == 4 || o == 8 ? 1 : 0);
+            if (nr < 0 || nr >= 20 || nc < 0 || nc >= 20) continue;
+            if (add && !addable(nr, nc)) continue;
+            if (!fs_op(t, tmp, (int16_t)(nr * 20 + nc), add)) return false;
         }
     }
     return true;
+}
+
+template <typename Occ, typename Own>
+__host__ __device__ inline bool fs_place(FsetRef t, int16_t* tmp, const int32_t* cells, int n, Occ occ, Own own) {
+    auto addable = [&](int nr, int nc) {
+        if (occ(nr, nc)) return false;
+        if (nr > 0 && own(nr - 1, nc)) return false;
+        if (nr < 19 && own(nr + 1, nc)) return false;
+        if (nc > 0 && own(nr, nc - 1)) return false;
+        if (nc < 19 && own(nr, nc + 1)) return false;
+        return true;
+    };
+    return fs_place_pred(t, tmp, cells, n, addable);
 }
 
 // set.copy() (make_new_set + set_merge into an empty set).  false: the copy's table
@@ -806,6 +844,69 @@ struct FsLane {
     bk_fset s;
     int16_t tmp[BK_FSET_SLOTS];
 };
+
+// the 7 addable rows of frontier_addable as opaque register values: a select chain over
+// array elements gets folded into a dynamically indexed (scratch) load otherwise
+struct AddRows {
+    uint32_t a0, a1, a2, a3, a4, a5, a6;
+    __device__ __forceinline__ explicit AddRows(const uint32_t (&A)[7])
+        : a0(A[0]), a1(A[1]), a2(A[2]), a3(A[3]), a4(A[4]), a5(A[5]), a6(A[6]) {
+        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6));
+    }
+    // bit (nr, nc), nr in ar-1 .. ar+5 (row index i = nr - ar + 1)
+    __device__ __forceinline__ bool at(int ar, int nr, int nc) const {
+        const int i = nr - ar + 1;
+        const uint32_t row = i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : i == 3 ? a3 : i == 4 ? a4 : i == 5 ? a5 : a6;
+        return ((row >> nc) & 1u) != 0u;
+    }
+};
+
+// update_frontier_after_move (engine/board.py:315-367) of player p's table in fl for a
+// piece at cells[0..n) whose top row is ar, addability from A.  A table of <= 128
+// slots is staged in LDS (lk: [slot][lane] int16, stride WAVE) so the probe chains of
+// the ~45 add/discard ops wait on LDS, not L2/HBM; a 256-slot table (or a move that
+// grows one past 128) is updated in place.  false: table overflow.
+__device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
+                                               const int32_t (&cells)[5], int n, int ar, const uint32_t (&A)[7]) {
+    const AddRows rows7(A);
+    auto addable = [&](int nr, int nc) { return rows7.at(ar, nr, nc); };
+    bk_fset* gfs = &fl->s;
+    const uint32_t gmask = gfs->mask[p];
+    if (gmask < 128u) {
+        const uint4* src4 = reinterpret_cast<const uint4*>(gfs->key[p]);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if ((uint32_t)(8 * i) <= gmask) {
+                const uint4 v = src4[i];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    lk[(8 * i + 2 * j) * WAVE] = (int16_t)(w[j] & 0xFFFFu);
+                    lk[(8 * i + 2 * j + 1) * WAVE] = (int16_t)(w[j] >> 16);
+                }
+            }
+        }
+        uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
+        FsetRef t{lk, WAVE, &m, &f, &u, 128u, htab};
+        if (fs_place_pred(t, fl->tmp, cells, n, addable)) {
+            uint4* dst4 = reinterpret_cast<uint4*>(gfs->key[p]);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if ((uint32_t)(8 * i) <= m) {
+                    uint32_t w[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        w[j] = (uint16_t)lk[(8 * i + 2 * j) * WAVE] |
+                               ((uint32_t)(uint16_t)lk[(8 * i + 2 * j + 1) * WAVE] << 16);
+                    dst4[i] = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+            }
+            gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+            return true;
+        }
+    }
+    return fs_place_pred(fs_ref(gfs, p, htab), fl->tmp, cells, n, addable);
+}
 
 struct RolloutArgs {
     const bk_state* roots;
@@ -1062,7 +1163,9 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     Game g;
     g.pid = -1;
     bool done = false;
+    SECT_DECL
     for (uint32_t iter = 0;; ++iter) {
+        SECT(0);
         // ---- make sure this lane has a game whose current player may still move
         for (int guard = 0; guard < 3 && !done; ++guard) {
             if (g.pid < 0) {
@@ -1091,6 +1194,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             if (lane == 0) atomicOr(&a.counter[1], 1u);
             break;
         }
+        SECT(1);
         // ---- derive + movegen for every active lane (uniform work)
         const bool idle = done || g.pid < 0;
         const int p = idle ? 0 : g.cur;
@@ -1107,6 +1211,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         make_pairs(P);
         const uint32_t avail = idle ? 0u : (~g.used.get(p) & 0x1FFFFFu);
         const uint32_t total = movegen_counts<true>(P, avail, my, lane);
+        SECT(2);
         if (idle) continue;
         if (total == 0u) {
             if (arena) {
@@ -1124,6 +1229,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         // counts are consumed: the area now takes the mover's rows for locate
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+        SECT(3);
         int ar, ac;
         if constexpr (FR) {
             const bk_fset* fs = &a.fslab[slot].s;
@@ -1131,18 +1237,20 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         } else {
             locate_move_lds(gs, kk, rows_lds, ar, ac);
         }
+        SECT(4);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
         const uint32_t info = kInfo[gs];
         const int n = (int)((info >> 8) & 0xFFu);
-        {   // per piece row d: one mask; all row loads issued before any store
-            uint32_t m[5] = {0u, 0u, 0u, 0u, 0u};
+        // per piece row d: one mask; all row loads issued before any store
+        uint32_t m[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int q = 0; q < 5; ++q) {
-                const uint32_t cell = kCells[gs][q];
-                const uint32_t bit = q < n ? (1u << (ac + (int)(cell & 0xFFu))) : 0u;
+        for (int q = 0; q < 5; ++q) {
+            const uint32_t cell = kCells[gs][q];
+            const uint32_t bit = q < n ? (1u << (ac + (int)(cell & 0xFFu))) : 0u;
 #pragma unroll
-                for (int d = 0; d < 5; ++d) m[d] |= ((cell >> 8) == (uint32_t)d) ? bit : 0u;
-            }
+            for (int d = 0; d < 5; ++d) m[d] |= ((cell >> 8) == (uint32_t)d) ? bit : 0u;
+        }
+        {
             uint32_t ow[5], oc[5];
 #pragma unroll
             for (int d = 0; d < 5; ++d) {
@@ -1157,6 +1265,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 }
             }
         }
+        SECT(5);
         if constexpr (FR) {  // the mover's frontier set (engine/board.py:548 -> :315-367)
             int32_t cells[5];
 #pragma unroll
@@ -1164,54 +1273,12 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 const uint32_t cell = kCells[gs][q < n ? q : 0];
                 cells[q] = (ar + (int)(cell >> 8)) * 20 + ac + (int)(cell & 0xFFu);
             }
-            FsLane* fl = &a.fslab[slot];
-            const uint32_t* occ_rows = slab.base + 4 * 20;
-            const uint32_t* own_rows = slab.base + p * 20;
-            auto occ = [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; };
-            auto own = [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; };
-            bk_fset* gfs = &fl->s;
-            const uint32_t gmask = gfs->mask[p];
-            bool ok = false, staged = false;
-            if (gmask < 128u) {
-                // stage the mover's table in LDS ([slot][lane]): the probe chains of the
-                // ~45 add/discard ops then wait on LDS instead of L2
-                int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + lane;
-                const uint4* src4 = reinterpret_cast<const uint4*>(gfs->key[p]);
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    if ((uint32_t)(8 * i) <= gmask) {
-                        const uint4 v = src4[i];
-                        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            lk[(8 * i + 2 * j) * WAVE] = (int16_t)(w[j] & 0xFFFFu);
-                            lk[(8 * i + 2 * j + 1) * WAVE] = (int16_t)(w[j] >> 16);
-                        }
-                    }
-                }
-                uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
-                FsetRef t{lk, WAVE, &m, &f, &u, 128u, htab};
-                if (fs_place(t, fl->tmp, cells, n, occ, own)) {
-                    staged = ok = true;
-                    uint4* dst4 = reinterpret_cast<uint4*>(gfs->key[p]);
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        if ((uint32_t)(8 * i) <= m) {
-                            uint32_t w[4];
-#pragma unroll
-                            for (int j = 0; j < 4; ++j)
-                                w[j] = (uint16_t)lk[(8 * i + 2 * j) * WAVE] |
-                                       ((uint32_t)(uint16_t)lk[(8 * i + 2 * j + 1) * WAVE] << 16);
-                            dst4[i] = make_uint4(w[0], w[1], w[2], w[3]);
-                        }
-                    }
-                    gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
-                }
-            }
-            // tables of 256 slots (or a move that grows one past 128): in place in HBM
-            if (!staged) ok = fs_place(fs_ref(gfs, p, htab), fl->tmp, cells, n, occ, own);
-            if (!ok) g.status |= 2u;
+            uint32_t A[7];
+            frontier_addable(rows_lds, ar, m, A);  // before the table staging reuses the area
+            int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + lane;
+            if (!place_frontier(&a.fslab[slot], p, lk, htab, cells, n, ar, A)) g.status |= 2u;
         }
+        SECT(6);
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
         g.used.set(p, g.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
         g.first &= ~(1u << p);
@@ -1221,6 +1288,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             if (g.status & 2u) finish_game<FR>(a, g, slab, slot);  // status 2: table overflow
         }
     }
+    SECT_FLUSH;
 }
 
 // Two entry points over one body so profiles separate root generation (bk_advance)
@@ -1503,7 +1571,7 @@ __device__ __forceinline__ bool mc_copy_tables(bk_fset* d, const bk_fset* s, con
 
 // Board.place_piece(validate=False) of orientation gs at (ar, ac) for player p: rows,
 // used / cells / first, and the player's frontier table in T (engine/board.py:515-555)
-__device__ bool mc_place(Mc& m, const Slab& slab, int p, int gs, int ar, int ac, FsLane* T, const uint64_t* htab) {
+__device__ __forceinline__ bool mc_place(Mc& m, const Slab& slab, int p, int gs, int ar, int ac, FsLane* T, const uint64_t* htab) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
     int32_t cells[5];
@@ -1522,6 +1590,45 @@ __device__ bool mc_place(Mc& m, const Slab& slab, int p, int gs, int ar, int ac,
     auto occ = [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; };
     auto own = [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; };
     const bool ok = fs_place(fs_ref(&T->s, p, htab), T->tmp, cells, n, occ, own);
+    m.cells.set(p, m.cells.get(p) + (uint32_t)n);
+    m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
+    m.first &= ~(1u << p);
+    return ok;
+}
+
+// The placed piece's row masks (pm[d] = cells in row ar + d) and cell indices.
+__device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&pm)[5], int32_t (&cells)[5]) {
+    const int n = (int)((kInfo[gs] >> 8) & 0xFFu);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) pm[d] = 0u;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const uint32_t cell = kCells[gs][q < n ? q : 0];
+        const int dr = (int)(cell >> 8), c = ac + (int)(cell & 0xFFu);
+        cells[q] = (ar + dr) * 20 + c;
+        const uint32_t bit = q < n ? (1u << c) : 0u;
+#pragma unroll
+        for (int d = 0; d < 5; ++d) pm[d] |= (dr == d) ? bit : 0u;
+    }
+}
+
+// mc_place with the frontier update on the LDS-staged table (place_frontier).  pm /
+// cells from piece_cells, A from frontier_addable -- computed by EVERY lane of the wave
+// before any lane stages a table: the staged tables of some lanes overlay the LDS rows
+// of others.
+__device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
+                                                const uint64_t* htab, const uint32_t (&pm)[5],
+                                                const int32_t (&cells)[5], const uint32_t (&A)[7], int16_t* lk) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+        if (pm[d]) {
+            slab.at(p, ar + d) |= pm[d];
+            slab.at(4, ar + d) |= pm[d];
+        }
+    }
+    const bool ok = place_frontier(T, p, lk, htab, cells, n, ar, A);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
     m.first &= ~(1u << p);
@@ -1549,7 +1656,7 @@ __device__ __forceinline__ void mc_move_split(uint32_t mv, int& gs, int& ar, int
 }
 
 // root.board into the lane: rows from the state, tables = the search's root copy
-__device__ void mc_load_root(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L) {
+__device__ __forceinline__ void mc_load_root(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L) {
     const bk_state* s = a.roots + m.game;
     uint32_t occ[20];
 #pragma unroll
@@ -1576,7 +1683,7 @@ __device__ void mc_load_root(const MctsArgs& a, Mc& m, const Slab& slab, McLane*
     copy_fset(&L->A.s, &L->root);
 }
 
-__device__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab) {
+__device__ __forceinline__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab) {
     m.game = g;
     m.it = 0;
     m.mode = MC_SELECT;
@@ -1594,7 +1701,7 @@ __device__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, co
     if (!mc_copy_tables(&L->root, a.root_sets + g, htab)) m.status |= BK_MCTS_EFSET;  // MCTSNode: board.copy()
 }
 
-__device__ void mc_finish_game(const MctsArgs& a, Mc& m) {
+__device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m) {
     const int32_t g = m.game;
     const bk_mcts_node* pool = a.nodes + (size_t)g * a.cfg.node_cap;
     const bk_mcts_node root = pool[0];
@@ -1637,7 +1744,7 @@ __device__ __forceinline__ bool mc_tt_lookup(const MctsArgs& a, Mc& m, double& r
 
 // simulation result: TT insert on a miss, stats, backpropagation (mcts_agent.py:408-437,
 // :572-582), next iteration
-__device__ void mc_complete(const MctsArgs& a, Mc& m, McLane* L, double reward, bool hit) {
+__device__ __forceinline__ void mc_complete(const MctsArgs& a, Mc& m, McLane* L, double reward, bool hit) {
     if (hit) {
         m.hits++;
     } else {
@@ -1668,7 +1775,7 @@ __device__ void mc_complete(const MctsArgs& a, Mc& m, McLane* L, double reward, 
 
 // simulate the node in m.node / m.hash whose player has no legal move: the rollout
 // breaks at once (reward 0.0, no draw)
-__device__ void mc_sim_terminal(const MctsArgs& a, Mc& m, McLane* L) {
+__device__ __forceinline__ void mc_sim_terminal(const MctsArgs& a, Mc& m, McLane* L) {
     double reward = 0.0;
     bool hit = false;
     if (a.cfg.use_tt) hit = mc_tt_lookup(a, m, reward);
@@ -1679,7 +1786,7 @@ __device__ void mc_sim_terminal(const MctsArgs& a, Mc& m, McLane* L) {
 // selection (mcts_agent.py:384-406, UCB1 :68-111) from the root; leaves m.node at the
 // node to expand or simulate, m.depth / path / m.hash for it.  Returns true when that
 // node is evaluated terminal (no untried move, no child).
-__device__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, const uint64_t* Z) {
+__device__ __forceinline__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, const uint64_t* Z) {
     const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
     int u = 0, depth = 0;
     uint64_t h = a.root_hash[m.game];
@@ -1720,7 +1827,7 @@ __device__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, const uint64_t* Z
 
 // node.board of path[depth] into the lane (slab rows + table A): root, then per edge
 // new_board = board.copy(); place; MCTSNode(new_board) copies again (mcts_agent.py:113-145)
-__device__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L, const uint64_t* htab) {
+__device__ __forceinline__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L, const uint64_t* htab) {
     mc_load_root(a, m, slab, L);
     const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
     for (int d = 1; d <= m.depth; ++d) {
@@ -1734,11 +1841,13 @@ __device__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L,
 }
 
 __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
-    __shared__ uint32_t lds[ROLL_WORDS_PER_WAVE * (BLOCK / WAVE) + 2 * BK_CELLS];
+    // per wave: counts / B,C rows / the staged frontier table share ROLL_WORDS_FR
+    __shared__ uint32_t lds[ROLL_WORDS_FR * (BLOCK / WAVE) + 2 * BK_CELLS];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint32_t* my = lds + wv * ROLL_WORDS_PER_WAVE;
+    uint32_t* my = lds + wv * ROLL_WORDS_FR;
     uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
-    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + ROLL_WORDS_PER_WAVE * (BLOCK / WAVE));
+    int16_t* lk = reinterpret_cast<int16_t*>(my) + lane;
+    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + ROLL_WORDS_FR * (BLOCK / WAVE));
     for (int i = threadIdx.x; i < BK_CELLS; i += BLOCK) htab[i] = kCellHash[i];
     __syncthreads();
     const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
@@ -1748,7 +1857,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
     m.game = -1;
     m.mode = MC_SELECT;
     bool done = false;
+    SECT_DECL
     for (uint64_t step = 0;; ++step) {
+        SECT(13);
         // ---- tree work until this lane needs a movegen (divergent)
         while (!done && m.mode == MC_SELECT) {
             if (m.game < 0) {
@@ -1770,6 +1881,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
             if (lane == 0) atomicOr(&a.counter[1], 1u);
             break;
         }
+        SECT(8);
         // ---- one movegen per busy lane (uniform work)
         const bool idle = done;
         const int p = idle ? 0 : (m.mode == MC_EXPAND ? ((m.root_player + m.depth) & 3) : m.cur);
@@ -1786,6 +1898,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
         make_pairs(P);
         const uint32_t avail = idle ? 0u : (~m.used.get(p) & 0x1FFFFFu);
         const uint32_t total = movegen_counts<true>(P, avail, my, lane);
+        SECT(9);
         if (idle) continue;
         bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
         uint32_t k;
@@ -1831,15 +1944,26 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
         FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
         int ar, ac;
+        SECT(10);
         locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+        SECT(11);
         if (ar < 0) {  // the table does not list the move: counts and tables disagree
             m.status |= BK_MCTS_EINTERNAL;
             m.mode = MC_SELECT;
             continue;
         }
-        if (m.mode == MC_EXPAND) {  // MCTSNode.expand (mcts_agent.py:113-145)
+        uint32_t pm[5], A[7];
+        int32_t cells[5];
+        piece_cells(gs, ar, ac, pm, cells);
+        frontier_addable(rows_lds, ar, pm, A);  // all lanes, before any table staging
+        // MCTSNode.expand (mcts_agent.py:113-145) places on new_board = board.copy() (B),
+        // a rollout ply on sim (B): one place call site for both
+        const bool expand = m.mode == MC_EXPAND;
+        uint32_t c = 0;
+        bool ok = true;
+        if (expand) {
             bk_mcts_node* nd = pool + m.node;
-            const uint32_t c = (uint32_t)nd->child0 + nd->n_exp;
+            c = (uint32_t)nd->child0 + nd->n_exp;
             nd->n_exp = (uint16_t)(nd->n_exp + 1u);
             bk_mcts_node ch;
             ch.total = 0.0; ch.visits = 0; ch.child0 = -1;
@@ -1847,9 +1971,11 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
             ch.n_exp = 0; ch.n_legal = 0; ch.flags = 0;
             pool[c] = ch;
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
-            bool ok = mc_copy_tables(&L->B.s, &L->A.s, htab);
-            ok &= mc_place(m, slab, p, gs, ar, ac, &L->B, htab);
-            ok &= mc_copy_tables(&L->A.s, &L->B.s, htab);
+            ok = mc_copy_tables(&L->B.s, &L->A.s, htab);
+        }
+        ok &= mc_place_staged(m, slab, p, gs, ar, &L->B, htab, pm, cells, A, lk);
+        if (expand) {
+            ok &= mc_copy_tables(&L->A.s, &L->B.s, htab);  // MCTSNode(new_board): board.copy()
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             m.hash = mc_hash_step(Z, m.hash, p, (m.root_cp + m.depth) & 3, gs, ar, ac);
@@ -1866,14 +1992,17 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
             m.score0 = mc_score(m, m.player);
             m.plies = 0;
             m.mode = MC_ROLLOUT;
+            SECT(12);
         } else {
-            if (!mc_place(m, slab, p, gs, ar, ac, &L->B, htab)) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             m.plies++;
             m.cur = (m.cur + 1) & 3;
             if (m.plies >= a.cfg.max_rollout_moves)
                 mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
+            SECT(14);
         }
     }
+    SECT_FLUSH;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2001,6 +2130,26 @@ int bk_last_error(bk_handle h, char* buf, size_t len) {
     if (!h || !buf || len == 0) return BK_EINVAL;
     snprintf(buf, len, "%s", h->err);
     return BK_OK;
+}
+
+int bk_debug_sections(bk_handle h, uint64_t* out, int32_t n, int32_t reset) {
+    if (!h || !out || n < 1) return BK_EINVAL;
+#ifdef BK_SECTION_PROF
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
+    unsigned long long v[BK_NSECT];
+    HIPCHK(h, hipMemcpyFromSymbol(v, HIP_SYMBOL(g_sections), sizeof v));
+    for (int i = 0; i < n; ++i) out[i] = i < BK_NSECT ? (uint64_t)v[i] : 0u;
+    if (reset) {
+        memset(v, 0, sizeof v);
+        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_sections), v, sizeof v));
+    }
+    return BK_OK;
+#else
+    (void)reset;
+    for (int i = 0; i < n; ++i) out[i] = 0u;
+    return set_err(h, BK_EINVAL, "bk_debug_sections: library built without -DBK_SECTION_PROF%s", "");
+#endif
 }
 
 int bk_last_kernel_ms(bk_handle h, float* ms) {

@@ -10,7 +10,7 @@ i=0
 while read -r counters; do
   [ -z "$counters" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters -d $OUT/pmc$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/pmc$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $counters -d $OUT/pmc$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc$i.log 2>&1
   rc=$?
   echo "pass $i ($counters) rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

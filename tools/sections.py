@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Where does a playout / search ply spend its time?  (GPU box; diagnostic only.)
+
+Builds (on the CPU side, beforehand: `python tools/sections.py --build`) a second copy
+of the HIP library with -DBK_SECTION_PROF into tools/_prof/, then (on the box) loads it
+through BK_LIB_PATH, runs k_rollout (naive order), k_rollout_fr (frontier order) and
+k_mcts on config-3-like inputs, and prints each section's share of the per-wave
+shader-clock cycles (bk_debug_sections)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tools", "_prof", "libblokus_hip_sections.so")
+
+NAMES = {0: "loop tail", 1: "game start/finish", 2: "derive+movegen counts", 3: "draw+pick+rows->LDS",
+         4: "locate", 5: "apply", 6: "frontier place", 8: "mcts: tree select/replay/backprop/start",
+         9: "mcts: derive+movegen", 10: "mcts: expand bookkeeping/draw+pick", 11: "mcts: locate_frontier",
+         12: "mcts: expand place/copies/TT", 13: "mcts: loop tail", 14: "mcts: rollout place"}
+
+
+def build():
+    sys.path.insert(0, ROOT)
+    from reinforcementlearning_blokus_amd import build as B
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    subprocess.check_call([B.hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+                           "-DBK_SECTION_PROF", "-Wno-unused-command-line-argument", "-o", LIB, B.SRC])
+    print(LIB)
+
+
+def run():
+    os.environ["BK_LIB_PATH"] = LIB
+    sys.path.insert(0, ROOT)
+    import ctypes as C
+
+    import numpy as np
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU, MctsTT, empty_state
+    from reinforcementlearning_blokus_amd.mcts.zobrist import ZobristHash, flat_keys, hash_states
+    gpu = BlokusGPU(0)
+    L = N.load()
+    buf = (C.c_uint64 * 16)()
+
+    def read(tag, extra):
+        rc = L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
+        assert rc == 0, rc
+        tot = sum(buf)
+        rows = {NAMES.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
+        print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows}), flush=True)
+
+    L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
+    G, R = 256, 1024
+    roots = gpu.advance(empty_state(), G, 20, seed=5, root_index=np.zeros(G, dtype=np.int32))
+    idx = np.repeat(np.arange(G, dtype=np.int32), R)
+    gpu.rollout(roots, G * R, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=1, root_index=idx)
+    read("k_rollout naive", {"kernel_ms": gpu.last_kernel_ms()})
+    froots, fsets = gpu.rollout_frontier(empty_state(), N.fset_new(1), G, semantics=N.SEM_ADVANCE,
+                                         rng=N.RNG_PHILOX, seed=5, max_plies=20,
+                                         root_index=np.zeros(G, dtype=np.int32))
+    gpu.rollout_frontier(froots, fsets, G * R, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=1, root_index=idx)
+    read("k_rollout_fr", {"kernel_ms": gpu.last_kernel_ms()})
+    for games in (4096, 65536):
+        froots, fsets = gpu.rollout_frontier(empty_state(), N.fset_new(1), games, semantics=N.SEM_ADVANCE,
+                                             rng=N.RNG_PHILOX, seed=5, max_plies=20,
+                                             root_index=np.zeros(games, dtype=np.int32))
+        keys = flat_keys(ZobristHash(seed=3))
+        mt = np.zeros((games, 625), np.uint32)
+        for g in range(games):
+            st = np.random.RandomState(g).get_state()
+            mt[g, :624], mt[g, 624] = st[1], st[2]
+        gpu.mcts(froots, fsets, froots["current_player"].copy(), hash_states(froots, keys), iterations=16,
+                 zobrist=keys[None], mt_state=mt, tt=MctsTT(games, cap=64), want_rewards=False)
+        read("k_mcts", {"games": games, "iterations": 16, "kernel_ms": gpu.last_kernel_ms()})
+
+
+if __name__ == "__main__":
+    build() if "--build" in sys.argv else run()
