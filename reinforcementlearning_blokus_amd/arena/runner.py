@@ -20,6 +20,7 @@ import numpy as np
 
 from ..agents.fast_mcts_agent import FastMCTSAgent
 from ..agents.gameplay_fast_mcts import GameplayFastMCTSAgent
+from ..agents.heuristic_agent import HeuristicAgent
 from ..agents.random_agent import RandomAgent
 from ..engine.board import Player
 from ..engine.game import BlokusGame
@@ -94,13 +95,19 @@ class _GameplayFastMCTSAdapter:
 
 
 def build_agent(config: AgentConfig, seed: int):
-    """Agent adapter from configuration (:415-492).  ``heuristic`` seats (and MCTS with
-    the heuristic rollout policy / learned evaluation) are not ported:
-    an ``mcts`` seat here rolls out uniformly at random on the GPU."""
+    """Agent adapter from configuration (:415-492).  ``mcts`` seats search with the
+    reference's default HeuristicAgent rollouts (MCTSAgent "exact" backend); learned
+    evaluation options are out of scope and rejected by MCTSAgent."""
     kind = config.type.lower()
     params = dict(config.params)
     if kind == "random":
         return _SelectActionAdapter(RandomAgent(seed=seed))
+    if kind == "heuristic":
+        agent = HeuristicAgent(seed=seed)
+        weights = params.get("weights")
+        if isinstance(weights, Mapping):
+            agent.set_weights(dict(weights))
+        return _SelectActionAdapter(agent)
     if kind == "mcts":
         deterministic = bool(params.get("deterministic_time_budget", True))
         iterations = int(params.get("iterations", 1000))

@@ -18,12 +18,12 @@ have three GPU backends:
   the ply loop run on the host, every legal-move list comes from the GPU in the
   reference's frontier order and the agent draws from its own stream -- bit-identical
   to the reference for RandomAgent, usable with any agent.
-* ``rollout_backend="kernel"`` (default without a rollout_agent): the whole playout
-  runs inside the persistent HIP rollout kernel (bk_rollout, BK_SEM_ROLLOUT, Philox
-  stream, naive move order): statistically the same random playout, not the same
-  random numbers.  The reference's default HeuristicAgent rollout policy is not
-  ported; without a rollout_agent this agent uses uniform random
-  rollouts.
+  Without a rollout_agent the reference's default applies, HeuristicAgent(seed=seed)
+  (mcts/mcts_agent.py:278-281), on this backend.
+* ``rollout_backend="kernel"`` (opt-in): the whole playout runs inside the persistent
+  HIP rollout kernel (bk_rollout, BK_SEM_ROLLOUT, Philox stream, naive move order) with
+  UNIFORM random moves: statistically a random playout, not the reference's numbers,
+  and not its heuristic policy.
 The learned-evaluator options of the reference are out of scope and rejected.
 """
 from __future__ import annotations
@@ -117,11 +117,13 @@ class MCTSAgent:
         self.move_generator = get_shared_generator()
         self.piece_generator = PieceGenerator()
         self.zobrist_hash = ZobristHash(seed=seed)
-        self.rollout_agent = rollout_agent
+        from ..agents.heuristic_agent import HeuristicAgent
         from ..agents.random_agent import RandomAgent
+        if rollout_agent is None and rollout_backend != "kernel":
+            rollout_agent = HeuristicAgent(seed=seed)  # the reference's default policy
+        self.rollout_agent = rollout_agent
         if rollout_backend is None:
-            rollout_backend = ("search" if isinstance(rollout_agent, RandomAgent) else
-                               "exact" if rollout_agent is not None else "kernel")
+            rollout_backend = "search" if isinstance(rollout_agent, RandomAgent) else "exact"
         self.rollout_backend = rollout_backend
         if self.rollout_backend not in ("search", "exact", "kernel"):
             raise ValueError("rollout_backend must be 'search', 'exact' or 'kernel'")

@@ -1,0 +1,113 @@
+"""HeuristicAgent through the drop-in API with GPU legal-move lists, against the
+reference (tests/golden/heuristic.json): 12-ply heuristic self-play from 16 positions,
+two full 4-heuristic games, MCTSAgent searches with the reference's default
+HeuristicAgent rollouts, and run_single_game records of mixed
+random/heuristic/mcts/fast_mcts arenas.  Tolerance: exact (moves, scores, RNG state)."""
+import pytest
+
+from reinforcementlearning_blokus_amd.agents.heuristic_agent import HeuristicAgent
+from reinforcementlearning_blokus_amd.engine.board import Player
+from reinforcementlearning_blokus_amd.engine.game import BlokusGame
+from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator, move_to_int
+from tests.conftest import load_golden
+from tests.helpers import POS, engine_board, sha_ints
+
+pytestmark = pytest.mark.gpu
+H = load_golden("heuristic.json")
+
+
+@pytest.mark.parametrize("i", range(len(H["cases"])))
+def test_selfplay_matches_reference(i):
+    c = H["cases"][i]
+    b = engine_board(POS[c["position"]])
+    legal = get_shared_generator().get_legal_moves(b, Player(c["player"]))
+    assert len(legal) == c["n_legal"]
+    assert sha_ints(move_to_int(m) for m in legal) == c["moves_sha"]
+    game = BlokusGame(enable_telemetry=False)
+    game.board = b
+    agents = {p: HeuristicAgent(seed=c["seed"] * 10 + p.value) for p in Player}
+    trace = []
+    for _ in range(12):
+        game._check_game_over()
+        if game.is_game_over():
+            break
+        p = game.get_current_player()
+        lm = game.get_legal_moves(p)
+        if not lm:
+            trace.append(-1)
+            game.board._update_current_player()
+            continue
+        mv = agents[p].select_action(game.board, p, lm)
+        trace.append(move_to_int(mv))
+        assert game.make_move(mv, p)
+    assert trace == c["selfplay_trace"]
+    for p in Player:
+        st = agents[p].rng.get_state()
+        assert [int(st[2]), sha_ints(int(x) for x in st[1])] == c["selfplay_rng"][str(p.value)]
+
+
+@pytest.mark.parametrize("i", range(len(H["games"])))
+def test_full_heuristic_game_matches_reference(i):
+    g = H["games"][i]
+    game = BlokusGame(enable_telemetry=False)
+    agents = {p: HeuristicAgent(seed=g["seed"] + p.value) for p in Player}
+    trace, passes, turns = [], 0, 0
+    while not game.is_game_over() and turns < 2500:
+        p = game.get_current_player()
+        lm = game.get_legal_moves(p)
+        turns += 1
+        if not lm:
+            passes += 1
+            trace.append(-1)
+            game.board._update_current_player()
+            game._check_game_over()
+            continue
+        mv = agents[p].select_action(game.board, p, lm)
+        trace.append(move_to_int(mv))
+        assert game.make_move(mv, p)
+    res = game.get_game_result()
+    assert trace == g["trace"]
+    assert [int(res.scores[p.value]) for p in Player] == g["scores"]
+    assert [int(w) for w in res.winner_ids] == g["winner_ids"]
+    assert (passes, turns) == (g["passes"], g["turns"])
+
+
+@pytest.mark.parametrize("i", range(len(H["mcts"])))
+def test_mcts_default_heuristic_rollouts_match_reference(i):
+    """MCTSAgent(seed=s) without a rollout agent = HeuristicAgent(seed=s) rollouts
+    (mcts/mcts_agent.py:278-281), host tree + GPU legal lists."""
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
+    c = H["mcts"][i]
+    b = engine_board(POS[c["position"]])
+    p = Player(c["player"])
+    agent = MCTSAgent(iterations=c["iterations"], seed=c["seed"], use_transposition_table=c["use_tt"],
+                      max_rollout_moves=c["max_rollout_moves"])
+    assert agent.rollout_backend == "exact" and isinstance(agent.rollout_agent, HeuristicAgent)
+    legal = get_shared_generator().get_legal_moves(b, p)
+    assert len(legal) == c["n_legal"]
+    mv = agent.select_action(b, p, legal)
+    assert move_to_int(mv) == c["move"]
+    assert agent.stats["rollout_rewards"] == c["rollout_rewards"]
+    assert agent.stats["transposition_hits"] == c["transposition_hits"]
+    st = agent.rollout_agent.rng.get_state()
+    assert [int(st[2]), sha_ints(int(x) for x in st[1])] == [c["rng_pos"], c["rng_sha"]]
+
+
+def test_mixed_arena_games_match_reference():
+    """run_single_game with random / heuristic / mcts (heuristic rollouts) / fast_mcts
+    seats (analytics/tournament/arena_runner.py:415-492, :578-777)."""
+    from reinforcementlearning_blokus_amd.arena.config import RunConfig, game_seed_from_run_seed, \
+        seat_assignment_for_game
+    from reinforcementlearning_blokus_amd.arena.runner import run_single_game
+    cfg = RunConfig.from_dict(H["arena_config"])
+    agents = {a.name: a for a in cfg.agents}
+    for ref in H["arena"]:
+        gi = ref["game_index"]
+        gs = game_seed_from_run_seed(cfg.seed, gi)
+        seats = seat_assignment_for_game([a.name for a in cfg.agents], gi, gs, cfg.seat_policy)
+        assert gs == ref["game_seed"] and seats == ref["seat_assignment"]
+        rec = run_single_game(run_id="fx3", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                              agent_configs=agents)
+        assert rec["error"] is None, rec["error"]
+        for k in ("final_scores", "winner_ids", "moves_made", "turn_count", "passes", "invalid_actions", "is_tie"):
+            assert rec[k] == ref[k], (gi, k)

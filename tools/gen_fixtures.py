@@ -32,6 +32,12 @@ What is recorded (all reference behaviour, nothing re-implemented here):
                           RandomAgent rollouts (mcts/mcts_agent.py:304-582): two
                           consecutive select_action calls per agent, the root children
                           (move, visits, total_reward), stats and rollout-RNG state
+* ``heuristic.json``   -- HeuristicAgent (agents/heuristic_agent.py): per-move
+                          _evaluate_move scores (float hex) and softmax probabilities for
+                          legal lists, select_action sequences in 12-ply heuristic
+                          self-play, full 4-heuristic games, MCTSAgent searches with its
+                          default HeuristicAgent rollouts, and run_single_game records of
+                          mixed random/heuristic/mcts/fast_mcts arenas
 """
 from __future__ import annotations
 
@@ -394,6 +400,139 @@ def gen_mcts_case(case):
             "rollout_seed": rseed, "zobrist_seed": zseed, "calls": calls}
 
 
+# (position index, seed): heuristic evaluation + 12-ply heuristic self-play
+HEUR_CASES = [(i, 300 + i) for i in (0, 1, 4, 6, 8, 10, 14, 18, 22, 26, 30, 34, 38, 42, 46, 50)]
+HEUR_FULL_LISTS = 6  # cases whose legal lists / score vectors are stored in full
+
+
+def _heur_case(case):
+    pos, seed = case
+    _setup()
+    from agents.heuristic_agent import HeuristicAgent
+    from engine.board import Player
+    from engine.game import BlokusGame
+    from engine.move_generator import get_shared_generator
+    from tests.utils_game_states import generate_random_valid_state
+    gid_of = _gid_map()
+    board, cur = generate_random_valid_state(*POSITION_SPECS[pos])
+    gen = get_shared_generator()
+    agent = HeuristicAgent(seed=seed)
+    legal = gen.get_legal_moves(board, cur)
+    scores = [agent._evaluate_move(board, cur, m) for m in legal]
+    probs = agent._softmax(__import__("numpy").array(scores), temperature=1.0) if legal else []
+    rec = {"position": pos, "seed": seed, "player": cur.value, "move_count": board.move_count,
+           "n_legal": len(legal), "moves_sha": _sha(move_int(gid_of, m) for m in legal),
+           "scores_sha": _sha(float(x).hex() for x in scores), "probs_sha": _sha(float(x).hex() for x in probs)}
+    if HEUR_CASES.index(case) < HEUR_FULL_LISTS:
+        rec["moves"] = [move_int(gid_of, m) for m in legal]
+        rec["scores"] = [float(x).hex() for x in scores]
+    # 12 plies of heuristic self-play (arena semantics: pass when stuck), agent per seat
+    game = BlokusGame(enable_telemetry=False)
+    game.board = board
+    agents = {p: HeuristicAgent(seed=seed * 10 + p.value) for p in Player}
+    trace = []
+    for _ in range(12):
+        game._check_game_over()
+        if game.is_game_over():
+            break
+        p = game.get_current_player()
+        lm = game.get_legal_moves(p)
+        if not lm:
+            trace.append(-1)
+            game.board._update_current_player()
+            continue
+        mv = agents[p].select_action(game.board, p, lm)
+        trace.append(move_int(gid_of, mv))
+        assert game.make_move(mv, p)
+    rec["selfplay_trace"] = trace
+    rec["selfplay_rng"] = {p.value: [int(agents[p].rng.get_state()[2]),
+                                     _sha(int(x) for x in agents[p].rng.get_state()[1])] for p in Player}
+    return rec
+
+
+def _heur_game(gseed):
+    """A full 4-HeuristicAgent game from the empty board (arena loop semantics)."""
+    _setup()
+    from agents.heuristic_agent import HeuristicAgent
+    from engine.board import Player
+    from engine.game import BlokusGame
+    gid_of = _gid_map()
+    game = BlokusGame(enable_telemetry=False)
+    agents = {p: HeuristicAgent(seed=gseed + p.value) for p in Player}
+    trace, passes, turns = [], 0, 0
+    while not game.is_game_over() and turns < 2500:
+        p = game.get_current_player()
+        lm = game.get_legal_moves(p)
+        turns += 1
+        if not lm:
+            passes += 1
+            trace.append(-1)
+            game.board._update_current_player()
+            game._check_game_over()
+            continue
+        mv = agents[p].select_action(game.board, p, lm)
+        trace.append(move_int(gid_of, mv))
+        assert game.make_move(mv, p)
+    res = game.get_game_result()
+    return {"seed": gseed, "trace": trace, "scores": [int(res.scores[p.value]) for p in Player],
+            "winner_ids": list(res.winner_ids), "passes": passes, "turns": turns}
+
+
+# MCTSAgent with its default rollout policy, HeuristicAgent(seed) (mcts/mcts_agent.py:278-281)
+HEUR_MCTS_CASES = [(12, 6, 3, True, 31), (20, 8, 4, True, 32), (30, 5, 6, False, 33), (44, 8, 2, True, 34)]
+
+
+def _heur_mcts_case(case):
+    pos, iters, max_roll, use_tt, seed = case
+    _setup()
+    from engine.move_generator import get_shared_generator
+    from mcts.mcts_agent import MCTSAgent, MCTSNode
+    from tests.utils_game_states import generate_random_valid_state
+    gid_of = _gid_map()
+    board, cur = generate_random_valid_state(*POSITION_SPECS[pos])
+    agent = MCTSAgent(iterations=iters, seed=seed, use_transposition_table=use_tt, max_rollout_moves=max_roll)
+    legal = get_shared_generator().get_legal_moves(board, cur)
+    root = MCTSNode(board, cur)
+    agent._run_mcts_with_iterations(root)
+    best = root.get_best_move()
+    st = agent.rollout_agent.rng.get_state()
+    return {"position": pos, "iterations": iters, "max_rollout_moves": max_roll, "use_tt": use_tt, "seed": seed,
+            "player": cur.value, "n_legal": len(legal), "move": move_int(gid_of, best),
+            "root_children": [[move_int(gid_of, ch.move), ch.visits, float(ch.total_reward)] for ch in root.children],
+            "rollout_rewards": [float(r) for r in agent.stats["rollout_rewards"]],
+            "transposition_hits": agent.stats["transposition_hits"],
+            "rng_pos": int(st[2]), "rng_sha": _sha(int(x) for x in st[1])}
+
+
+HEUR_ARENA = {"agents": [{"name": "r", "type": "random"}, {"name": "h", "type": "heuristic"},
+                         {"name": "m", "type": "mcts", "params": {"iterations": 3, "max_rollout_moves": 2}},
+                         {"name": "f", "type": "fast_mcts", "params": {"time_limit": 0.01}}],
+              "num_games": 4, "seed": 777001, "seat_policy": "round_robin", "output_root": "/tmp/arena_fx3"}
+
+
+def _heur_arena_game(gi):
+    _setup()
+    from analytics.tournament.arena_runner import (RunConfig, _seat_assignment_for_game, game_seed_from_run_seed,
+                                                   run_single_game)
+    cfg = RunConfig.from_dict(HEUR_ARENA)
+    gs = game_seed_from_run_seed(cfg.seed, gi)
+    seats = _seat_assignment_for_game([a.name for a in cfg.agents], gi, gs, cfg.seat_policy)
+    rec, _ = run_single_game(run_id="fx3", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                             agent_configs={a.name: a for a in cfg.agents})
+    keep = ("game_index", "game_seed", "seat_assignment", "winner_ids", "final_scores", "moves_made",
+            "turn_count", "passes", "invalid_actions", "is_tie", "error")
+    return {k: rec[k] for k in keep}
+
+
+def gen_heuristic():
+    with Pool(8) as pool:
+        cases = pool.map(_heur_case, HEUR_CASES)
+        games = pool.map(_heur_game, [9001, 9002])
+        searches = pool.map(_heur_mcts_case, HEUR_MCTS_CASES)
+        arena = pool.map(_heur_arena_game, range(HEUR_ARENA["num_games"]))
+    return {"cases": cases, "games": games, "mcts": searches, "arena_config": HEUR_ARENA, "arena": arena}
+
+
 def dump(name, obj):
     path = os.path.join(OUT, name)
     with open(path, "w") as f:
@@ -459,6 +598,8 @@ def main():
     if what in ("all", "mcts"):
         with Pool(8) as pool:
             dump("mcts.json", pool.map(gen_mcts_case, MCTS_CASES))
+    if what in ("all", "heuristic"):
+        dump("heuristic.json", gen_heuristic())
 
 
 if __name__ == "__main__":
