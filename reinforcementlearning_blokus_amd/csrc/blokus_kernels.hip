@@ -119,11 +119,13 @@ __device__ __forceinline__ void derive_rows(const uint32_t (&own)[20], const uin
 // ------------------------------------------------------------------------------------
 // the stencil scan
 // ------------------------------------------------------------------------------------
-// Mover planes.  B/C = blocked / corner rows; BP/CP = the same for a horizontal
-// pair of cells (BP[R] = B[R] | B[R] >> 1): a run of two cells of a piece row costs one
-// term instead of two.  287 terms cover the 410 cells of the 91 orientations.
+// Mover planes.  B/C = blocked / corner rows; BP/CP = the same for a horizontal pair of
+// cells (BP[R] = B[R] | B[R] >> 1), BV/CV for a vertical pair (BV[R] = B[R] | B[R + 1]):
+// a pair of cells of a piece costs one term instead of two.  The stencil table
+// (tools/gen_tables.py) covers the 410 cells of the 91 orientations with the fewest
+// terms.
 struct Planes {
-    uint32_t B[20], C[20], BP[20], CP[20];
+    uint32_t B[20], C[20], BP[20], CP[20], BV[20], CV[20];
 };
 
 __device__ __forceinline__ void make_pairs(Planes& P) {
@@ -131,6 +133,8 @@ __device__ __forceinline__ void make_pairs(Planes& P) {
     for (int R = 0; R < 20; ++R) {
         P.BP[R] = P.B[R] | (P.B[R] >> 1);
         P.CP[R] = P.C[R] | (P.C[R] >> 1);
+        P.BV[R] = R < 19 ? (P.B[R] | P.B[R + 1]) : P.B[R];  // row 19: never a pair's top
+        P.CV[R] = R < 19 ? (P.C[R] | P.C[R + 1]) : P.C[R];
     }
 }
 
@@ -148,7 +152,7 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
 #define LUT_ANDN 0x30    // a & ~b
 #define BITOP3(a, b, c, lut) __builtin_amdgcn_bitop3_b32((a), (b), (c), (lut))
 
-// One stencil class: height H, static term sequence T... (t = piece row * 2 + pair).
+// One stencil class: height H, static term sequence T... (t = piece row * 4 + kind).
 // Term 0 sits at column 0 (no shift); term k >= 1 is shifted by the uniform column
 // sh[k].  For every anchor row r < 21 - H calls f(r, ok) with ok = legal anchor
 // columns (bit x = column x).
@@ -160,14 +164,14 @@ struct StencilClass {
 
     template <int K>
     __device__ __forceinline__ static uint32_t tb(const Planes& P, int r, const uint32_t (&sh)[5]) {
-        constexpr int d = ts[K] >> 1;
-        const uint32_t v = (ts[K] & 1) ? P.BP[r + d] : P.B[r + d];
+        constexpr int d = ts[K] >> 2, kind = ts[K] & 3;
+        const uint32_t v = kind == 1 ? P.BP[r + d] : kind == 2 ? P.BV[r + d] : P.B[r + d];
         return K == 0 ? v : v >> sh[K];
     }
     template <int K>
     __device__ __forceinline__ static uint32_t tc(const Planes& P, int r, const uint32_t (&sh)[5]) {
-        constexpr int d = ts[K] >> 1;
-        const uint32_t v = (ts[K] & 1) ? P.CP[r + d] : P.C[r + d];
+        constexpr int d = ts[K] >> 2, kind = ts[K] & 3;
+        const uint32_t v = kind == 1 ? P.CP[r + d] : kind == 2 ? P.CV[r + d] : P.C[r + d];
         return K == 0 ? v : v >> sh[K];
     }
     // OR of terms K.. into (b, c); the last C term folds into ok
@@ -220,6 +224,13 @@ struct StencilClass {
 // dead once the move's orientation is picked; the same bytes then hold the mover's
 // B/C rows 0..19 as [row][lane]{B, C} pairs for locate_move_lds.
 #define ROLL_WORDS_PER_WAVE (40 * WAVE)
+// resident 256-lane blocks per CU for k_rollout / k_advance (the launch bound).  3 (168
+// VGPRs): with the vertical-pair planes (tools/gen_tables.py BK_GEN_VPAIR=1, 243
+// instead of 287 terms) the kernel needs 2 (226 VGPRs) and measured 42.2 M vs 48.7 M
+// playouts/s -- the lost latency hiding costs more than the 15 % fewer stencil ops
+#ifndef ROLL_BLOCKS_PER_CU
+#define ROLL_BLOCKS_PER_CU 3
+#endif
 // frontier-order kernel: 64 dwords per lane; after the move is located the area also
 // stages the mover's frontier table ([slot][lane] int16, up to 128 slots)
 #define ROLL_WORDS_FR (64 * WAVE)
@@ -1293,8 +1304,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
 
 // Two entry points over one body so profiles separate root generation (bk_advance)
 // from the measured playouts (bk_rollout).
-__global__ __launch_bounds__(BLOCK, 3) void k_rollout(RolloutArgs a) { rollout_body<false>(a); }
-__global__ __launch_bounds__(BLOCK, 3) void k_advance(RolloutArgs a) { rollout_body<false>(a); }
+__global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_rollout(RolloutArgs a) { rollout_body<false>(a); }
+__global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_advance(RolloutArgs a) { rollout_body<false>(a); }
 // reference frontier order (compat parity mode)
 __global__ __launch_bounds__(BLOCK, 2) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
 

@@ -47,6 +47,12 @@ def orientations():
     return table
 
 
+# stencil term kinds: one cell, a horizontal pair (plane BP = B | B >> 1), a vertical
+# pair (plane BV[R] = B[R] | B[R + 1])
+KINDS = {"s": 0, "p": 1, "v": 2}
+VPAIR = os.environ.get("BK_GEN_VPAIR", "0") == "1"  # measured: 2 waves/SIMD needed, net slower
+
+
 def _placements(cells):
     cs = set(cells)
     out = []
@@ -54,11 +60,13 @@ def _placements(cells):
         out.append(("s", r, c, frozenset([(r, c)])))
         if (r, c + 1) in cs:
             out.append(("p", r, c, frozenset([(r, c), (r, c + 1)])))
+        if VPAIR and (r + 1, c) in cs:
+            out.append(("v", r, c, frozenset([(r, c), (r + 1, c)])))
     return out
 
 
 def stencil_terms(cells):
-    """Cover an orientation's cells with the fewest horizontal singles/pairs (overlap
+    """Cover an orientation's cells with the fewest singles / horizontal / vertical pairs (overlap
     allowed: the stencil ORs shifted rows, so covering a cell twice is harmless).
     Returns [(kind, d, c), ...] with a column-0 term first (it needs no shift), the
     rest sorted by (d, kind, c)."""
@@ -80,11 +88,11 @@ def render_classes(table):
     per-orientation (uniform) operands.  Per orientation 2 words in class order:
     w0 = piece_id | g << 8, w1 = column of term k (k >= 1) at bits 3(k-1).
     BK_CLASS_LIST(X) expands X(i0, i1, height, t0, t1, ...) per class with
-    t = d * 2 + (1 if pair else 0)."""
+    t = d * 4 + kind (KINDS)."""
     classes = {}
     for g, (pid, _o, cells, h, _w) in enumerate(table):
         terms = stencil_terms(cells)
-        key = (h, tuple(d * 2 + (1 if k == "p" else 0) for k, d, _c in terms))
+        key = (h, tuple(d * 4 + KINDS[k] for k, d, _c in terms))
         w1 = sum(c << (3 * (j - 1)) for j, (_k, _d, c) in enumerate(terms) if j > 0)
         classes.setdefault(key, []).append((pid | (g << 8), w1))
     order = sorted(classes, key=lambda k: (k[0], len(k[1]), k[1]))
