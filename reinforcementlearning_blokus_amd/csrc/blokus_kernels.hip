@@ -306,9 +306,10 @@ __device__ __forceinline__ void all_rows(const Planes& P, F&& f) {
 
 // orientation holding the k-th legal move (naive order: g ascending) and its rank in it
 __device__ __forceinline__ int pick_orient(const uint32_t* cnt, int lane, uint32_t k, uint32_t& kk) {
-    uint32_t run = 0;
-    int gs = BK_NUM_ORIENTS - 1;
-    uint32_t before = 0;
+    // dword level first (the three 10-bit fields summed), then the field inside the
+    // dword that holds index k
+    uint32_t run = 0, before = 0, hit = 0;
+    int hd = CNT_DWORDS - 1;
     bool found = false;
 #pragma unroll 1
     for (int h0 = 0; h0 < CNT_DWORDS; h0 += 8) {  // 8 LDS reads in flight per batch
@@ -317,16 +318,28 @@ __device__ __forceinline__ int pick_orient(const uint32_t* cnt, int lane, uint32
         for (int j = 0; j < 8; ++j) v[j] = (h0 + j < CNT_DWORDS) ? cnt[(h0 + j) * WAVE + lane] : 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-#pragma unroll
-            for (int f = 0; f < 3; ++f) {
-                const uint32_t c = (v[j] >> (10 * f)) & 0x3FFu;
-                if (!found && k < run + c) { gs = 3 * (h0 + j) + f; before = run; found = true; }
-                run += c;
-            }
+            const uint32_t s = (v[j] & 0x3FFu) + ((v[j] >> 10) & 0x3FFu) + (v[j] >> 20);
+            const bool in = !found && k < run + s;
+            hd = in ? h0 + j : hd;
+            before = in ? run : before;
+            hit = in ? v[j] : hit;
+            found |= in;
+            run += s;
         }
     }
-    kk = k - before;
-    return gs;
+    uint32_t r = k - before;
+    const uint32_t c0 = hit & 0x3FFu, c1 = (hit >> 10) & 0x3FFu;
+    int f = 2;
+    if (r < c0) {
+        f = 0;
+    } else if (r < c0 + c1) {
+        f = 1;
+        r -= c0;
+    } else {
+        r -= c0 + c1;
+    }
+    kk = r;
+    return found ? 3 * hd + f : BK_NUM_ORIENTS - 1;
 }
 
 // Recompute orientation gs (per-lane, divergent) row r_ok values with per-lane
