@@ -117,6 +117,15 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise NativeUnavailable(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        # One HIP runtime per process.  torch bundles its own libamdhip64 (+ HSA runtime)
+        # with the same soname as /opt/rocm's (libamdhip64.so.7).  Loaded after torch,
+        # this library binds torch's copy; loaded before, torch later pulls in a second
+        # runtime that finds no GPU ("No HIP GPUs are available"), measured with
+        # tools/runtime_order_probe.py.  A plain import touches no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         try:
             L = C.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - environment specific
