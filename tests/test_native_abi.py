@@ -58,3 +58,21 @@ def test_gpu_free_container_fails_loudly():
         pass
     with pytest.raises(N.NativeUnavailable):
         N.Handle(0)
+
+
+def test_one_hip_runtime_per_process():
+    """_native.load() imports torch first, so the library binds torch's libamdhip64 (same
+    soname) instead of pulling in /opt/rocm's as a second runtime (two runtimes in one
+    process leave torch without a GPU; tools/runtime_order_probe.py).  Checked in a
+    fresh interpreter from the process's memory map; no GPU call is made."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from reinforcementlearning_blokus_amd import _native as N\n"
+            "N.load()\n"
+            "libs = sorted({l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l})\n"
+            "print(len(libs)); print(libs)\n") % ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    n = int(out.stdout.splitlines()[0])
+    assert n == 1, out.stdout
