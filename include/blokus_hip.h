@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 1
+#define BK_ABI_VERSION 2
 #define BK_BOARD 20
 #define BK_CELLS 400
 #define BK_PLAYERS 4
@@ -259,8 +259,15 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
  * TT per game: tt_keys/tt_vals[g * cfg.tt_cap ...] open addressing (linear probing,
  * slot = key & (tt_cap - 1), empty slot = NaN value), tt_count[g] entries; in/out so the
  * table persists across an agent's searches like the reference's dict.
- * nodes[g * cfg.node_cap ...]: the tree (node 0 = root; children of a node are a block
- * reserved at its first expansion, in expansion order); left on return for inspection.
+ * nodes[g * cfg.node_cap ...]: the tree (node 0 = root).  A node's children are one
+ * contiguous block in expansion order; the block holds min(n_legal, 4) slots at the
+ * first expansion and is moved to a block twice as large (capped at n_legal) each time
+ * it fills, so a search of I iterations never needs more than 4*I + 1 slots.  Left on
+ * return for inspection.
+ * Chunked searches: a launch with cfg.iter_stop = k stops every search after k
+ * iterations; a later launch with cfg.resume = 1 (same buffers, larger iter_stop)
+ * continues them from nodes / out / tt / mt_state exactly where they stopped.  The
+ * result equals one launch of cfg.iterations.
  * rewards / hit_flags (optional, [g * cfg.iterations + i]): per iteration the simulated
  * reward and 1 if it came from the TT (stats["rollout_rewards"] = the non-hit ones).
  * out[g].status != 0 means the search stopped early (see BK_MCTS_E*): enlarge the pool /
@@ -285,6 +292,10 @@ typedef struct bk_mcts_cfg {
     int32_t node_cap;          /* node slots per game                                  */
     int32_t tt_cap;            /* TT slots per game, power of two (>= 2 when use_tt)   */
     int32_t time_limit_us;     /* > 0: stop at the first iteration boundary past it    */
+    int32_t iter_stop;         /* > 0: this launch stops each search once it has run
+                                  iter_stop iterations in total (chunked searches)      */
+    int32_t resume;            /* 1: continue the searches left in nodes / out / tt /
+                                  mt_state by an earlier launch (iter_stop chunks)      */
 } bk_mcts_cfg;
 
 #define BK_MCTS_EPOOL 1u   /* node pool full                    */

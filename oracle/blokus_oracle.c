@@ -436,6 +436,20 @@ void or_pack_state(const or_board* b, bk_state* s) {
    given iteration-order lists into fresh sets when provided (layout may then differ
    from the reference's; the SET is right), else recomputed from the grid
    (engine/board.py:261-313 _compute_full_frontier, row-major). */
+/* Load player p's frontier set table slot for slot (a bk_fset record's layout: key -1
+   unused, -2 dummy, else r*20+c), so a board built from a packed state carries the exact
+   CPython table of the position (test infrastructure: GPU-generated roots). */
+int or_set_frontier_table(or_board* b, int p, const int16_t* key, int mask, int fill, int used) {
+    if (p < 0 || p > 3 || mask + 1 > OR_SET_MAX || ((mask + 1) & mask) != 0) return -1;
+    or_pyset* s = &b->fr[p];
+    s->mask = mask; s->fill = fill; s->used = used;
+    for (int i = 0; i <= mask; ++i) {
+        s->key[i] = key[i];
+        s->hash[i] = key[i] >= 0 ? g_cell_hash[key[i]] : key[i] == K_DUMMY ? -1 : 0;
+    }
+    return 0;
+}
+
 int or_unpack_state(or_board* b, const bk_state* s, const int32_t* frontier_lists, const int32_t* frontier_lens) {
     or_init();
     memset(b, 0, sizeof *b);

@@ -97,6 +97,7 @@ def lib():
             "or_zobrist_hash": (C.c_uint64, [P(Board), P(C.c_uint64)]),
             "or_batch_playouts": (C.c_int, [P(State), C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
                                             C.c_int, P(Result)]),
+            "or_set_frontier_table": (C.c_int, [P(Board), C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
             "or_mcts": (C.c_int, [P(Board), C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int,
                                   C.c_void_p, P(MT), C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                   P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_void_p,
@@ -170,6 +171,20 @@ def unpack(s, frontier_lists=None):
         arr = (C.c_int32 * max(1, len(flat)))(*flat)
         lens = (C.c_int32 * 4)(*[len(fl) for fl in frontier_lists])
         lib().or_unpack_state(C.byref(b), C.byref(s), arr, lens)
+    return b
+
+
+def board_from(state_bytes, fset):
+    """An oracle board from a packed bk_state (bytes) and its bk_fset record (numpy
+    FSET_DTYPE element): the position with its exact frontier-set table layouts."""
+    s = State.from_buffer_copy(bytes(state_bytes))
+    b = unpack(s)
+    for p in range(4):
+        key = np.ascontiguousarray(fset["key"][p], dtype=np.int16)
+        rc = lib().or_set_frontier_table(C.byref(b), p, key.ctypes.data, int(fset["mask"][p]), int(fset["fill"][p]),
+                                         int(fset["used"][p]))
+        if rc != 0:
+            raise ValueError("bad frontier table")
     return b
 
 

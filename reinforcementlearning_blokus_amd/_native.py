@@ -79,10 +79,10 @@ assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRoll
 class BkMctsCfg(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("max_rollout_moves", C.c_int32), ("exploration", C.c_double),
                 ("use_tt", C.c_int32), ("node_cap", C.c_int32), ("tt_cap", C.c_int32),
-                ("time_limit_us", C.c_int32)]
+                ("time_limit_us", C.c_int32), ("iter_stop", C.c_int32), ("resume", C.c_int32)]
 
 
-assert C.sizeof(BkMctsCfg) == 32
+assert C.sizeof(BkMctsCfg) == 40
 MCTS_NODE_DTYPE = np.dtype([("total", "<f8"), ("visits", "<u4"), ("child0", "<i4"), ("move", "<u2"),
                             ("n_exp", "<u2"), ("n_legal", "<u2"), ("flags", "<u2")])
 assert MCTS_NODE_DTYPE.itemsize == 24
@@ -104,6 +104,7 @@ RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("statu
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
 assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
 
+ABI_VERSION = 2  # include/blokus_hip.h BK_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -130,6 +131,10 @@ def load():
             L = C.CDLL(LIB_PATH)
         except OSError as e:  # pragma: no cover - environment specific
             raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        L.bk_abi_version.restype, L.bk_abi_version.argtypes = C.c_int, []
+        if L.bk_abi_version() != ABI_VERSION:
+            raise NativeUnavailable(f"{LIB_PATH} has ABI {L.bk_abi_version()}, this package needs {ABI_VERSION}: "
+                                    "rebuild it (__graft_entry__.build())")
         P, vp = C.POINTER, C.c_void_p
         sigs = {
             "bk_abi_version": (C.c_int, []),

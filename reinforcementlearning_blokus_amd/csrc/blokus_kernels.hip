@@ -1709,20 +1709,52 @@ __device__ __forceinline__ void mc_load_root(const MctsArgs& a, Mc& m, const Sla
 
 __device__ __forceinline__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab) {
     m.game = g;
-    m.it = 0;
     m.mode = MC_SELECT;
-    m.nodes_used = 1;
     m.tt_cnt = a.cfg.use_tt ? a.tt_count[g] : 0;
-    m.hits = m.rollouts = 0;
     m.root_player = a.players[g] & 3;
     m.root_cp = a.roots[g].current_player & 3;
-    m.status = 0;
     m.mt_pos = a.mt[(size_t)g * (FM_N + 1) + FM_N];
     m.t0 = wall_clock64();
-    bk_mcts_node* root = a.nodes + (size_t)g * a.cfg.node_cap;
-    root->total = 0.0; root->visits = 0; root->child0 = -1;
-    root->move = 0xFFFFu; root->n_exp = 0; root->n_legal = 0; root->flags = 0;
+    if (a.cfg.resume) {  // a chunked search: carry on where the previous launch stopped
+        const bk_mcts_out o = a.out[g];
+        m.it = o.iterations_run;
+        m.nodes_used = o.nodes_used;
+        m.hits = o.tt_hits;
+        m.rollouts = o.rollouts;
+        m.status = o.status;
+    } else {
+        m.it = 0;
+        m.nodes_used = 1;
+        m.hits = m.rollouts = 0;
+        m.status = 0;
+        bk_mcts_node* root = a.nodes + (size_t)g * a.cfg.node_cap;
+        root->total = 0.0; root->visits = 0; root->child0 = -1;
+        root->move = 0xFFFFu; root->n_exp = 0; root->n_legal = 0; root->flags = 0;
+    }
     if (!mc_copy_tables(&L->root, a.root_sets + g, htab)) m.status |= BK_MCTS_EFSET;  // MCTSNode: board.copy()
+}
+
+// Slot for the next child of node nd (n_legal known, n_exp < n_legal).  The children
+// block holds min(n_legal, 4) slots at the first expansion and moves to a block twice
+// as large (capped at n_legal) whenever it is full, so a search of I iterations uses at
+// most 4 * I + 1 slots.  Children keep their expansion order; nothing points into a
+// block but its parent's child0 (paths are rebuilt from the root by every selection).
+// -1: the pool is full.
+__device__ __forceinline__ int32_t mc_child_slot(bk_mcts_node* pool, bk_mcts_node* nd, Mc& m, int32_t node_cap) {
+    const uint32_t ne = nd->n_exp, nl = nd->n_legal;
+    const bool grow = ne == 0u || (ne >= 4u && (ne & (ne - 1u)) == 0u);
+    if (grow) {
+        const uint32_t want = ne == 0u ? 4u : 2u * ne;
+        const uint32_t ncap = want < nl ? want : nl;
+        if ((uint64_t)m.nodes_used + ncap > (uint64_t)node_cap) return -1;
+        const int32_t nb = m.nodes_used;
+        m.nodes_used += (int32_t)ncap;
+        const int32_t ob = nd->child0;
+#pragma unroll 1
+        for (uint32_t k = 0; k < ne; ++k) pool[nb + k] = pool[ob + k];
+        nd->child0 = nb;
+    }
+    return nd->child0 + (int32_t)ne;
 }
 
 __device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m) {
@@ -1893,7 +1925,8 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
             }
             const bool timed_out = a.cfg.time_limit_us > 0 &&
                                    wall_clock64() - m.t0 >= a.limit_ticks;
-            if (m.it >= a.cfg.iterations || timed_out || m.status) { mc_finish_game(a, m); continue; }
+            const bool chunk_end = a.cfg.iter_stop > 0 && m.it >= a.cfg.iter_stop;
+            if (m.it >= a.cfg.iterations || chunk_end || timed_out || m.status) { mc_finish_game(a, m); continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
             if (m.status) continue;
@@ -1929,20 +1962,10 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
         if (m.mode == MC_EXPAND) {
             bk_mcts_node* nd = pool + m.node;
             uint32_t n_legal = nd->n_legal, n_exp = nd->n_exp;
-            int32_t child0 = nd->child0;
             if (!(nd->flags & BK_MCTS_NODE_EVALUATED)) {  // MCTSNode._initialize_untried_moves
                 n_legal = total;
-                if (total > 0u) {
-                    if ((uint64_t)m.nodes_used + total > (uint64_t)a.cfg.node_cap) {
-                        m.status |= BK_MCTS_EPOOL;
-                        m.mode = MC_SELECT;
-                        continue;
-                    }
-                    child0 = m.nodes_used;
-                    m.nodes_used += (int32_t)total;
-                }
                 nd->n_legal = (uint16_t)n_legal;
-                nd->child0 = child0;
+                nd->child0 = -1;
                 nd->flags = BK_MCTS_NODE_EVALUATED;
             }
             if (n_legal != total) {  // an evaluated node's list cannot change
@@ -1987,7 +2010,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
         bool ok = true;
         if (expand) {
             bk_mcts_node* nd = pool + m.node;
-            c = (uint32_t)nd->child0 + nd->n_exp;
+            const int32_t cs = mc_child_slot(pool, nd, m, a.cfg.node_cap);
+            if (cs < 0) { m.status |= BK_MCTS_EPOOL; m.mode = MC_SELECT; continue; }
+            c = (uint32_t)cs;
             nd->n_exp = (uint16_t)(nd->n_exp + 1u);
             bk_mcts_node ch;
             ch.total = 0.0; ch.visits = 0; ch.child0 = -1;
@@ -2528,8 +2553,11 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     if (!roots || !root_sets || !players || !root_hash || !zobrist || n_zobrist < 1 || !zobrist_index ||
         !mt_state || !log_table || log_len < 1 || !out || (rewards == nullptr) != (hit_flags == nullptr))
         return set_err(h, BK_EINVAL, "bk_mcts: missing buffer%s", "");
-    if (cfg->iterations < 0 || cfg->max_rollout_moves <= 0 || cfg->node_cap < 1 || cfg->time_limit_us < 0)
-        return set_err(h, BK_EINVAL, "bk_mcts: bad cfg (iterations/max_rollout_moves/node_cap)%s", "");
+    if (cfg->iterations < 0 || cfg->max_rollout_moves <= 0 || cfg->node_cap < 1 || cfg->time_limit_us < 0 ||
+        cfg->iter_stop < 0 || (cfg->resume != 0 && cfg->resume != 1))
+        return set_err(h, BK_EINVAL, "bk_mcts: bad cfg (iterations/max_rollout_moves/node_cap/iter_stop/resume)%s", "");
+    if (cfg->resume && !nodes)
+        return set_err(h, BK_EINVAL, "bk_mcts: resume needs the caller's nodes buffer%s", "");
     if (cfg->use_tt && (!tt_keys || !tt_vals || !tt_count || cfg->tt_cap < 2 || (cfg->tt_cap & (cfg->tt_cap - 1))))
         return set_err(h, BK_EINVAL, "bk_mcts: use_tt needs tt buffers and a power-of-two tt_cap%s", "");
     if (mem == BK_MEM_HOST) {
@@ -2559,10 +2587,10 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         {tt_vals, sizeof(double) * ttc * n, 3, nullptr},
         {tt_count, cfg->use_tt ? sizeof(int32_t) * n : 0, 3, nullptr},
         {log_table, sizeof(double) * (size_t)log_len, 1, nullptr},
-        {nodes, sizeof(bk_mcts_node) * (size_t)cfg->node_cap * n, 2, nullptr},
-        {rewards, sizeof(double) * it * n, 2, nullptr},
-        {hit_flags, it * n, 2, nullptr},
-        {out, sizeof(bk_mcts_out) * n, 2, nullptr},
+        {nodes, sizeof(bk_mcts_node) * (size_t)cfg->node_cap * n, cfg->resume ? 3 : 2, nullptr},
+        {rewards, sizeof(double) * it * n, cfg->resume ? 3 : 2, nullptr},
+        {hit_flags, it * n, cfg->resume ? 3 : 2, nullptr},
+        {out, sizeof(bk_mcts_out) * n, cfg->resume ? 3 : 2, nullptr},
     };
     const int NSEC = (int)(sizeof sec / sizeof sec[0]);
     const int NODES = 11;

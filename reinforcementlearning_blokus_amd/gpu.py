@@ -219,7 +219,7 @@ class BlokusGPU:
     def mcts(self, roots, root_sets, players, root_hash, *, iterations: int, zobrist, mt_state,
              zobrist_index=None, tt: "MctsTT" = None, max_rollout_moves: int = 50, exploration: float = 1.414,
              log_table=None, node_cap: int = 0, time_limit_us: int = 0, want_rewards: bool = True,
-             want_nodes: bool = False):
+             want_nodes: bool = False, chunk: int = 0):
         """MCTSAgent.select_action searches for a batch of positions, whole on the GPU
         (bk_mcts; mcts/mcts_agent.py:304-582 with RandomAgent rollouts).
 
@@ -228,8 +228,10 @@ class BlokusGPU:
         key tables (cells x 5, turn x 4, player x piece), zobrist_index[g] picks one.
         mt_state: uint32[n, 625] numpy MT19937 states (key then pos), advanced in place.
         tt: an MctsTT (one table per game, kept across calls) or None (no TT).
-        Returns dict(out=MCTS_OUT_DTYPE[n], rewards, hit_flags, nodes).  A search that
-        outgrows its node pool is re-run from the saved inputs with a larger pool."""
+        node_cap: node slots per search (default 4 * iterations + 1, which the kernel's
+        child-block growth never exceeds).  chunk > 0: run the searches in launches of
+        `chunk` iterations (cfg.iter_stop / cfg.resume), same result as one launch.
+        Returns dict(out=MCTS_OUT_DTYPE[n], rewards, hit_flags, nodes)."""
         n = len(roots)
         roots = np.ascontiguousarray(roots, dtype=STATE_DTYPE)
         root_sets = np.ascontiguousarray(root_sets, dtype=N.FSET_DTYPE)
@@ -239,32 +241,35 @@ class BlokusGPU:
         zi = np.zeros(n, np.int32) if zobrist_index is None else np.ascontiguousarray(zobrist_index, dtype=np.int32)
         assert mt_state.dtype == np.uint32 and mt_state.shape == (n, 625) and mt_state.flags.c_contiguous
         assert len(root_sets) == n and len(pl) == n and len(rh) == n and len(zi) == n
+        assert not (chunk and time_limit_us), "chunked searches run a fixed iteration count"
         if log_table is None:
             log_table = mcts_log_table(iterations)
         lt = np.ascontiguousarray(log_table, dtype=np.float64)
         if tt is not None:
             tt.reserve(iterations + 1)
             assert tt.keys.shape[0] == n
-        cap = int(node_cap) or 1 + (iterations + 1) * 256
+        cap = int(node_cap) or mcts_node_cap(iterations)
         mt0 = mt_state.copy()
         tt0 = tt.snapshot() if tt is not None else None
+        stops = mcts_chunks(iterations, chunk)
         while True:
-            cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(tt is not None), cap,
-                              tt.cap if tt is not None else 0, int(time_limit_us))
             out = np.zeros(n, dtype=N.MCTS_OUT_DTYPE)
             rewards = np.zeros((n, max(iterations, 1))) if want_rewards else None
             flags = np.zeros((n, max(iterations, 1)), np.uint8) if want_rewards else None
-            nodes = np.zeros((n, cap), dtype=N.MCTS_NODE_DTYPE) if want_nodes else None
+            nodes = np.zeros((n, cap), dtype=N.MCTS_NODE_DTYPE) if (want_nodes or len(stops) > 1) else None
             ptr = lambda x: x.ctypes.data if x is not None else 0  # noqa: E731
             self.handle.set_stream(None)
-            self.handle.mcts(roots.ctypes.data, root_sets.ctypes.data, pl.ctypes.data, rh.ctypes.data, n, cfg,
-                             zob.ctypes.data, len(zob), zi.ctypes.data, mt_state.ctypes.data,
-                             ptr(tt.keys) if tt is not None else 0, ptr(tt.vals) if tt is not None else 0,
-                             ptr(tt.count) if tt is not None else 0, lt.ctypes.data, len(lt), ptr(nodes),
-                             ptr(rewards), ptr(flags), out.ctypes.data, N.MEM_HOST)
+            for j, stop in enumerate(stops):
+                cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(tt is not None), cap,
+                                  tt.cap if tt is not None else 0, int(time_limit_us), stop, int(j > 0))
+                self.handle.mcts(roots.ctypes.data, root_sets.ctypes.data, pl.ctypes.data, rh.ctypes.data, n, cfg,
+                                 zob.ctypes.data, len(zob), zi.ctypes.data, mt_state.ctypes.data,
+                                 ptr(tt.keys) if tt is not None else 0, ptr(tt.vals) if tt is not None else 0,
+                                 ptr(tt.count) if tt is not None else 0, lt.ctypes.data, len(lt), ptr(nodes),
+                                 ptr(rewards), ptr(flags), out.ctypes.data, N.MEM_HOST)
             st = out["status"]
             if (st & N.MCTS_EPOOL).any() and not (st & ~np.uint32(N.MCTS_EPOOL)).any():
-                mt_state[:] = mt0  # roll back and retry with a bigger pool
+                mt_state[:] = mt0  # roll back and retry with a bigger pool (only for a caller-set cap)
                 if tt is not None:
                     tt.restore(tt0)
                 cap = cap * 2 + 1
@@ -272,6 +277,79 @@ class BlokusGPU:
             if st.any():
                 raise RuntimeError(f"bk_mcts: search stopped early, status bits {sorted(set(st[st != 0].tolist()))}")
             return {"out": out, "rewards": rewards, "hit_flags": flags, "nodes": nodes, "node_cap": cap}
+
+    def mcts_device(self, roots, root_sets, players, root_hash, zobrist, zobrist_index, mt_state, log_table, nodes,
+                    out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
+                    hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
+                    on_chunk=None):
+        """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
+        BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
+        (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
+        Layouts as in mcts(): roots uint8[n,256], root_sets uint8[n,2080], players
+        uint8[n], root_hash/zobrist int64, zobrist_index int32[n], mt_state int32[n,625],
+        log_table float64, nodes uint8[n, node_cap*24], out uint8[n,32], tt_keys int64 /
+        tt_vals float64 [n, tt_cap] (NaN = empty) + tt_count int32[n] (all or none),
+        rewards float64 / hit_flags uint8 [n, iterations] (optional).  chunk > 0 splits
+        the searches into launches of `chunk` iterations; on_chunk(done_iterations) is
+        called after each.  Raises if any search reports a nonzero status."""
+        import torch
+        n = roots.shape[0]
+        use_tt = tt_keys is not None
+        node_cap = nodes.shape[1] // N.MCTS_NODE_DTYPE.itemsize
+        tensors = dict(roots=(roots, torch.uint8, (n, 256)), root_sets=(root_sets, torch.uint8, (n, N.FSET_DTYPE.itemsize)),
+                       players=(players, torch.uint8, (n,)), root_hash=(root_hash, torch.int64, (n,)),
+                       zobrist_index=(zobrist_index, torch.int32, (n,)), mt_state=(mt_state, torch.int32, (n, 625)),
+                       nodes=(nodes, torch.uint8, (n, node_cap * N.MCTS_NODE_DTYPE.itemsize)),
+                       out=(out, torch.uint8, (n, N.MCTS_OUT_DTYPE.itemsize)))
+        if use_tt:
+            cap = tt_keys.shape[1]
+            tensors.update(tt_keys=(tt_keys, torch.int64, (n, cap)), tt_vals=(tt_vals, torch.float64, (n, cap)),
+                           tt_count=(tt_count, torch.int32, (n,)))
+        if rewards is not None:
+            tensors.update(rewards=(rewards, torch.float64, (n, iterations)),
+                           hit_flags=(hit_flags, torch.uint8, (n, iterations)))
+        for name, (t, dt, shape) in tensors.items():
+            _check_device_tensor(t, name, dt, shape, self.device)
+        _check_device_tensor(zobrist, "zobrist", torch.int64, (zobrist.shape[0], N.MCTS_ZOBRIST_WORDS), self.device)
+        _check_device_tensor(log_table, "log_table", torch.float64, (log_table.shape[0],), self.device)
+        self._stream_from_torch()
+        d = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        for j, stop in enumerate(mcts_chunks(iterations, chunk)):
+            cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
+                              tt_keys.shape[1] if use_tt else 0, 0, stop, int(j > 0))
+            self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
+                             d(zobrist_index), d(mt_state), d(tt_keys), d(tt_vals), d(tt_count), d(log_table),
+                             log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)
+            if on_chunk is not None:
+                on_chunk(stop or iterations)
+        st = out.view(torch.int32)[:, 6]
+        bad = int((st != 0).sum().item())
+        if bad:
+            raise RuntimeError(f"bk_mcts: {bad} searches stopped early, status bits "
+                               f"{sorted(set(st[st != 0].tolist()))[:8]}")
+
+
+def _check_device_tensor(t, name, dtype, shape, device):
+    """The C-ABI reads raw device pointers: insist on the exact dtype, shape,
+    contiguity and device so a mismatch fails here instead of in the kernel."""
+    if not t.is_cuda or t.device.index != device:
+        raise ValueError(f"{name}: expected a tensor on cuda:{device}, got {t.device}")
+    if t.dtype != dtype or tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: expected {dtype} {tuple(shape)}, got {t.dtype} {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def mcts_node_cap(iterations: int) -> int:
+    """Node slots one search of `iterations` can need (bk_mcts child-block growth)."""
+    return 4 * int(iterations) + 1
+
+
+def mcts_chunks(iterations: int, chunk: int):
+    """cfg.iter_stop per launch: [0] (one launch) or chunk, 2*chunk, ..., iterations."""
+    if not chunk or chunk >= iterations:
+        return [0]
+    return list(range(chunk, iterations, chunk)) + [iterations]
 
 
 def mcts_log_table(iterations: int) -> np.ndarray:

@@ -1,0 +1,143 @@
+"""Config 5 (BASELINE.json configs[4]): 65,536 concurrent MCTSAgent searches x 4,096
+iterations with the Zobrist transposition table in HBM (bk_mcts, device-resident,
+chunked launches), checked bit-exact against the pinned oracle (or_mcts,
+oracle/blokus_oracle.c, itself pinned by tests/golden/mcts.json) on a strided sample of
+the searches and by size-independent properties on all of them.
+
+Reference: mcts/mcts_agent.py:304-437 (search), :572-582 (backpropagation),
+mcts/zobrist.py:155-220 (TT).  Tolerance: exact (integer rewards, IEEE double UCB1)."""
+import os
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from reinforcementlearning_blokus_amd import _native as N
+from tests.helpers import mt_array
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    return BlokusGPU(0)
+
+
+def _progress(msg):
+    """Progress for long GPU steps: pytest captures stdout, so also append to a file
+    under gpurun_out/ (what the GPU box watches for signs of life)."""
+    root = os.environ.get("GRAFT_REPO_ROOT")
+    if root:
+        os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(root, "gpurun_out", "config5_progress.log"), "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
+def _oracle_search(batch, g, ztabs, rewards_needed=True):
+    """or_mcts for game g of an MctsBatch: same position (exact frontier tables), player,
+    zobrist table, rollout stream and a fresh TT."""
+    b = O.board_from(batch.roots_np[g].tobytes(), batch.sets_np[g])
+    m = O.numpy_mt(0)
+    m.mt[:] = batch.mt0[g, :624].tolist()
+    m.mti = int(batch.mt0[g, 624])
+    tt = O.TT()
+    ref = O.mcts(b, int(batch.players_np[g]), batch.iterations, 1.414, batch.max_rollout_moves,
+                 ztabs[int(batch.zidx_np[g])], m, tt)
+    return ref, tt.count, mt_array(m)
+
+
+def _check_against_oracle(batch, games, threads=16):
+    ztabs = [O.zobrist_table(t) for t in range(len(batch.zobrist_np))]
+    for t, z in enumerate(ztabs):  # the agent-side key tables are the oracle's
+        assert np.array_equal(z.astype(np.uint64), batch.zobrist_np[t])
+    res = batch.results()
+    mt = batch.mt.cpu().numpy().view(np.uint32)
+    with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside or_mcts
+        refs = list(ex.map(lambda g: _oracle_search(batch, g, ztabs), games))
+    for g, (ref, tt_count, mt_ref) in zip(games, refs):
+        assert int(res[g]["best_move"]) == ref["move"], g
+        assert [list(x) for x in batch.root_children(g)] == [list(x) for x in ref["children"]], g
+        if batch.rewards is not None:
+            assert batch.rewards[g].cpu().numpy().tolist() == ref["rewards"].tolist(), g
+            assert batch.hit_flags[g].cpu().numpy().tolist() == ref["hit_flags"].tolist(), g
+        assert int(batch.tt_count[g]) == tt_count, g
+        assert np.array_equal(mt[g], mt_ref), g
+
+
+def _check_properties(batch):
+    res = batch.results()
+    it = batch.iterations
+    assert (res["status"] == 0).all()
+    assert (res["iterations_run"] == it).all()
+    assert (res["tt_hits"] + res["rollouts"] == it).all()
+    assert (res["nodes_used"] <= batch.node_cap).all()
+    assert (res["nodes_used"] >= np.minimum(res["root_children"], it) + 1).all()
+    assert (batch.tt_count.cpu().numpy() == res["rollouts"]).all()  # fresh TTs: one insert per rollout
+    root = batch.nodes[:, :N.MCTS_NODE_DTYPE.itemsize].cpu().numpy().view(N.MCTS_NODE_DTYPE).reshape(-1)
+    assert (root["visits"] == it).all()  # every iteration backpropagates through the root
+    has_move = res["root_children"] > 0
+    assert (res["best_move"][has_move] >= 0).all()
+
+
+def test_chunked_search_equals_one_launch(gpu):
+    """cfg.iter_stop / cfg.resume: a search run as several launches is the same search."""
+    from reinforcementlearning_blokus_amd.gpu import MctsTT
+    from reinforcementlearning_blokus_amd.workloads import frontier_roots, numpy_mt_states
+    from reinforcementlearning_blokus_amd.mcts.zobrist import ZobristHash, flat_keys, hash_states
+    roots, sets = frontier_roots(gpu, 24, 18, seed=4242)
+    zob = flat_keys(ZobristHash(seed=3))
+    rh = hash_states(roots, zob)
+    pl = roots["current_player"] & 3
+    runs = []
+    for chunk in (0, 37, 64):
+        mt = numpy_mt_states(range(100, 124))
+        tt = MctsTT(24)
+        r = gpu.mcts(roots, sets, pl, rh, iterations=300, zobrist=zob[None], mt_state=mt, tt=tt,
+                     max_rollout_moves=20, want_nodes=True, chunk=chunk)
+        runs.append((r["out"].tobytes(), r["rewards"].tobytes(), r["hit_flags"].tobytes(), mt.tobytes(),
+                     tt.keys.tobytes(), tt.count.tobytes(), r["nodes"].tobytes()))
+    assert runs[0] == runs[1] == runs[2]
+
+
+def test_child_blocks_stay_within_four_slots_per_iteration(gpu):
+    """Child blocks grow 4, 8, 16 ... (capped at n_legal): nodes_used <= 4 * iterations + 1,
+    so the default pool never overflows, even when every iteration expands the root."""
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    roots, sets = frontier_roots(gpu, 256, 12, seed=99)
+    batch = MctsBatch(gpu, roots, sets, iterations=700, seed0=7, max_rollout_moves=4)
+    batch.run()
+    _check_properties(batch)
+
+
+def test_device_batch_matches_oracle(gpu):
+    """The config-5 code path (MctsBatch: device buffers, 8 zobrist tables, TT in HBM,
+    chunked launches) on 256 searches x 160 iterations, 24 of them against or_mcts."""
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    roots, sets = frontier_roots(gpu, 256, 20, seed=31337)
+    batch = MctsBatch(gpu, roots, sets, iterations=160, seed0=1000, want_rewards=True)
+    batch.run(chunk=50)
+    _check_properties(batch)
+    _check_against_oracle(batch, list(range(0, 256, 11)))
+
+
+@pytest.mark.timeout(900)
+def test_config5_full_scale(gpu):
+    """65,536 concurrent searches x 4,096 iterations (TT on, 50-ply RandomAgent rollouts)
+    from 20-ply positions, in 16 launches of 256 iterations; every search checked by
+    properties, a strided sample of 16 bit-exact against or_mcts."""
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    n, iters = 65536, 4096
+    roots, sets = frontier_roots(gpu, n, 20, seed=20260305)
+    batch = MctsBatch(gpu, roots, sets, iterations=iters, seed0=500_000, want_rewards=True)
+    t0 = time.perf_counter()
+    batch.run(chunk=256, on_chunk=lambda k: _progress(f"config5 {k}/{iters} iterations, "
+                                                      f"{time.perf_counter() - t0:.1f} s"))
+    dt = time.perf_counter() - t0
+    _progress(f"config5 done: {n * iters / dt / 1e6:.2f} M simulations/s")
+    _check_properties(batch)
+    t1 = time.perf_counter()
+    _check_against_oracle(batch, list(range(0, n, n // 16)))
+    _progress(f"config5 oracle sample checked in {time.perf_counter() - t1:.1f} s")
