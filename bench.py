@@ -1,22 +1,31 @@
 #!/usr/bin/env python3
 """Headline benchmark: MCTS random-rollout simulations/sec (20x20, 4 players).
 
-One "step" = one batch of the config-3 workload (BASELINE.json configs[2]):
-256 concurrent self-play games, 1,024 random rollouts per game-move, i.e. 262,144
-terminal random playouts (arena semantics: pass when stuck, game over when nobody
-can move, GameResult scoring) from 256 synthetic mid-game positions (20 random
-plies from the empty board), all resident in HBM before the timed region.
+Default workload (`--workload config3`, BASELINE.json configs[2]) -- one "step" = 256
+concurrent self-play games x 1,024 random rollouts per game-move = 262,144 terminal
+random playouts (arena semantics: pass when stuck, game over when nobody can move,
+GameResult scoring) from 256 synthetic mid-game positions (20 random plies from the
+empty board), all resident in HBM before the timed region.
 
-N>1: one process per GPU (torchrun), each rank plays its own 256 games (weak
-scaling, no data-path collective); after the timed region the per-rank result
-checksums are all-gathered over RCCL.
+Other workloads (one JSON line each, same contract):
+  --workload config5  BASELINE.json configs[4]: 65,536 concurrent MCTSAgent searches x
+                      4,096 iterations (UCT + Zobrist TT in HBM + 50-ply RandomAgent
+                      rollouts, reference frontier move order, bit-exact); one step =
+                      the whole batch of searches.  N>1: the 65,536 games are sharded
+                      over the ranks (strong scaling).
+  --workload config2  BASELINE.json configs[1]: batched legal-move generation for 4,096
+                      synthetic mid-game boards (plies 16..40), player to move (and
+                      --all-players: all 4); one step = one bk_movegen launch.
 
-Prints ONE JSON line on rank 0.
+N>1: one process per GPU (torchrun), weak scaling for config3 (each rank plays its own
+256 games, no data-path collective); after the timed region the per-rank results are
+all-gathered over RCCL.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -33,50 +42,102 @@ VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 # Single-issue rate (one wave64 VALU op per 4 cycles per SIMD): what any stream holding
 # slow ops (v_bcnt, SGPR operands, left shifts ...) gets -- k_rollout's case
 VALU_SINGLE_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+# Reference engine (Python) rates measured in the build container (SURVEY.md 6,
+# BASELINE.md): it cannot run on the GPU box, so these are carried, not re-timed.
+REF_PY_ARENA_SIMS_PER_CORE = 5.5      # terminal random playout from ply 20
+REF_PY_MCTS_RANDOM_SIMS = 8.6         # MCTSAgent + RandomAgent rollouts, 100 iterations
+REF_PY_MOVEGEN_BOARDS_PER_CORE = 162  # get_legal_moves at ply 20
+REF_CONTAINER = "8-vCPU Intel Xeon build container, Python 3.10.12, numpy 2.2.6"
+# SURVEY 8(d) algorithmic bytes
+STATE_B, RESULT_B = 256, 32
+MOVEGEN_B = 256 + 5096  # state in + dense 91 x 400-bit mask out, per board-player
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--games", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 20; config5: 1)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; config5: 1, "
+                                                              "a 64-iteration chunk)")
+    ap.add_argument("--workload", choices=("config3", "config5", "config2"), default="config3")
+    ap.add_argument("--games", type=int, default=None, help="config3: 256; config5: 65536 (whole job)")
     ap.add_argument("--rollouts", type=int, default=1024)
+    ap.add_argument("--iterations", type=int, default=4096, help="config5 MCTS iterations per search")
+    ap.add_argument("--chunk", type=int, default=512, help="config5 iterations per launch")
+    ap.add_argument("--boards", type=int, default=4096, help="config2 boards")
+    ap.add_argument("--all-players", action="store_true", help="config2: all 4 players of every board")
     ap.add_argument("--root-plies", type=int, default=20)
     ap.add_argument("--seed", type=int, default=20260301)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
-                    help="in-kernel move order: naive (default) or the reference's frontier order "
+                    help="config3 in-kernel move order: naive (default) or the reference's frontier order "
                          "(CPython set tables carried per game)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 1 if a.workload == "config5" else (200 if a.workload == "config2" else 20)
+    if a.warmup is None:
+        a.warmup = 1 if a.workload == "config5" else 3
+    return a
 
 
-def cpu_baseline(roots_np, seconds: float):
-    """Oracle (C restatement, reference frontier algorithm + game-over check after every
-    move) timed on this host's cores on a bounded sample of the same workload."""
+# ------------------------------------------------------------------ host CPU facts
+def host_cpu():
+    """Cores this process may really use on this host (affinity, capped by the cgroup
+    CPU quota: on the GPU box nproc shows the whole machine) and the CPU model."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, math.floor(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cores = min(aff, quota) if quota else aff
+    return {"cores": cores, "affinity_cpus": aff, "cgroup_quota_cpus": quota, "model": model}
+
+
+def ref_python(value, per_core, cores, what):
+    return {"value_per_core": per_core, "unit": "sims/s", "what": what,
+            "where": f"reference Python engine measured in the {REF_CONTAINER} (SURVEY.md 6); "
+                     "the reference cannot run on the GPU box",
+            "gpu_over_ref_1core": value / per_core, "gpu_over_ref_all_cores": value / (per_core * cores)}
+
+
+def cpu_baseline_playouts(roots_np, seconds, order):
+    """oracle/blokus_oracle.c (C restatement of the reference engine) timed on this
+    host's cores on a bounded sample of the same workload, in the SAME move order as the
+    GPU line, game-over check after every move like the reference."""
     from oracle import pyoracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    cpu = host_cpu()
+    threads = cpu["cores"]
+    o = O.ORDER_NAIVE if order == "naive" else O.ORDER_FRONTIER
     st = (O.State * len(roots_np)).from_buffer_copy(roots_np.tobytes())
-    n = 16 * threads
+    n = 8 * threads
     t0 = time.perf_counter()
-    O.batch_playouts(st, n, 1, threads=threads)
+    O.batch_playouts(st, n, 1, threads=threads, order=o)
     dt = time.perf_counter() - t0
-    # scale the sample to ~`seconds` of wall time
-    n2 = max(n, int(n * seconds / max(dt, 1e-3)))
+    n2 = max(n, int(n * seconds / max(dt, 1e-3)))  # scale the sample to ~`seconds`
     t0 = time.perf_counter()
-    O.batch_playouts(st, n2, 2, threads=threads)
+    O.batch_playouts(st, n2, 2, threads=threads, order=o)
     dt = time.perf_counter() - t0
-    return {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port",
-            "sample": f"{n2} arena playouts from the same {len(roots_np)} roots, "
-                      f"oracle/blokus_oracle.c (reference frontier movegen order), {threads} threads, {dt:.1f} s"}
+    return {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+            "host": cpu, "order": order,
+            "sample": f"{n2} arena playouts from the same {len(roots_np)} roots, oracle/blokus_oracle.c in "
+                      f"{order} move order, {threads} threads (one per usable core), {dt:.1f} s"}
 
 
-def main():
-    args = parse()
-    import numpy as np
+# ------------------------------------------------------------------ common
+def setup():
     import torch
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -85,29 +146,78 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local, dist
+
+
+def barrier_sync(dist):
+    import torch
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def reduce_max_sum(dist, dev, tmax, sums):
+    import torch
+    t = torch.tensor([tmax], dtype=torch.float64, device=dev)
+    s = torch.tensor(sums, dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+    return float(t.item()), [float(x) for x in s.tolist()]
+
+
+def traffic_for(kernel):
+    """PMC bytes / VALU instructions per launch of `kernel` from the committed profile
+    summary (tools/summarize_prof.py), if it covers that kernel."""
+    tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
+    try:
+        tj = json.load(open(tpath))
+    except (OSError, ValueError):
+        return None, None
+    per = tj.get("kernels", {}).get(kernel)
+    if per:
+        return per.get("bytes_per_launch"), per.get("valu_insts_per_launch")
+    if tj.get("kernel", "k_rollout") == kernel:
+        return tj.get("bytes_per_launch"), tj.get("valu_insts_per_launch")
+    return None, None
+
+
+def compute_roofline(valu_insts, avg_ms):
+    valu_tops = valu_insts * 64 / (avg_ms * 1e-3) / 1e12 if valu_insts else None
+    return {"bound": "valu_int32", "achieved": valu_tops, "peak": VALU_PEAK_TOPS, "unit": "Tlane-op/s",
+            "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None, "peak_single_issue": VALU_SINGLE_TOPS,
+            "frac_single_issue": valu_tops / VALU_SINGLE_TOPS if valu_tops else None,
+            "valu_insts_per_launch": valu_insts}
+
+
+# ------------------------------------------------------------------ config 3
+def run_config3(args, world, rank, local, dist):
+    import numpy as np
+    import torch
 
     from reinforcementlearning_blokus_amd import _native as N
     from reinforcementlearning_blokus_amd.gpu import BlokusGPU, empty_state
 
+    games = args.games or 256
     gpu = BlokusGPU(local)
     dev = torch.device("cuda", local)
     seed = args.seed + 1_000_003 * rank
     # synthetic mid-game roots, generated on the GPU (BK_SEM_ADVANCE from the empty board)
     if args.order == "frontier":
-        roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), args.games,
+        roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), games,
                                                  semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=seed,
                                                  max_plies=args.root_plies,
-                                                 root_index=np.zeros(args.games, dtype=np.int32))
-        sets = torch.from_numpy(sets_np.view(np.uint8).reshape(args.games, -1).copy()).to(dev)
+                                                 root_index=np.zeros(games, dtype=np.int32))
+        sets = torch.from_numpy(sets_np.view(np.uint8).reshape(games, -1).copy()).to(dev)
     else:
-        roots_np = gpu.advance(empty_state(), args.games, args.root_plies, seed=seed,
-                               root_index=np.zeros(args.games, dtype=np.int32))
-    roots = torch.from_numpy(roots_np.view(np.uint8).reshape(args.games, 256)).to(dev)
-    n = args.games * args.rollouts
+        roots_np = gpu.advance(empty_state(), games, args.root_plies, seed=seed,
+                               root_index=np.zeros(games, dtype=np.int32))
+    roots = torch.from_numpy(roots_np.view(np.uint8).reshape(games, 256)).to(dev)
+    n = games * args.rollouts
     # game j's rollouts are contiguous (one wave plays 64 rollouts of the same game)
     idx = torch.arange(n, dtype=torch.int32, device=dev) // args.rollouts
     out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-
     stream = torch.cuda.Stream(dev)  # our kernels and the timing events share this stream
     plies_acc = torch.zeros(1, dtype=torch.int64, device=dev)
 
@@ -115,9 +225,9 @@ def main():
         if args.order == "frontier":
             gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k,
                                  root_index=idx, out=out)
-            return
-        gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k, root_index=idx,
-                    out=out)
+        else:
+            gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k, root_index=idx,
+                        out=out)
 
     def count_plies():
         plies_acc.add_(out[:, 10:12].contiguous().view(torch.int16).to(torch.int64).sum())
@@ -127,10 +237,7 @@ def main():
             step(k)
             count_plies()
         plies_acc.zero_()
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
+        barrier_sync(dist)
         events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(args.steps)]
         t0 = time.perf_counter()
@@ -139,74 +246,270 @@ def main():
             step(1000 + k)
             events[k][1].record(stream)
             count_plies()
-        torch.cuda.synchronize()
-        if dist:
-            dist.barrier()
-        torch.cuda.synchronize()
+        barrier_sync(dist)
         elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in events]
-    plies = int(plies_acc.item())
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    tot = torch.tensor([n * args.steps, plies], dtype=torch.float64, device=dev)
+    elapsed, (sims, all_plies) = reduce_max_sum(dist, dev, elapsed, [n * args.steps, int(plies_acc.item())])
     if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         # RCCL gather of the last step's terminal results (32 B per playout) over xGMI,
         # outside the timed region; rank r's playouts are global games r (mod W)
         from reinforcementlearning_blokus_amd.shard import gather_results
         gather_results(out, n * world, rank, world, dist)
-    elapsed = float(t.item())
-    sims, all_plies = float(tot[0].item()), float(tot[1].item())
     value = sims / elapsed
+    if rank != 0:
+        return None
+    avg_ms = sum(kernel_ms) / len(kernel_ms)
+    plies_per_sim = all_plies / sims
+    bytes_per_sim = 2.0 * STATE_B * plies_per_sim + RESULT_B  # 256 B read + write per ply
+    achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
+    kname = "k_rollout_fr" if args.order == "frontier" else "k_rollout"
+    traffic, valu_insts = traffic_for(kname)
+    line = {
+        "metric": METRIC, "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "config3: 256 concurrent games x 1024 random rollouts (arena semantics, "
+                               f"{args.order} move order, Philox RNG) from GPU-generated 20-ply positions",
+                   "games": games, "rollouts_per_game": args.rollouts, "root_plies": args.root_plies,
+                   "playouts_per_step": n, "parallelism": f"dp{world} (independent games per rank)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "kernel_ms": avg_ms,
+                     "plies_per_sim": plies_per_sim, "bytes_per_sim": bytes_per_sim},
+        "compute_roofline": compute_roofline(valu_insts, avg_ms),
+    }
+    if not args.no_cpu_baseline and world == 1:
+        cb = cpu_baseline_playouts(roots_np, args.cpu_seconds, args.order)
+        cb["gpu_over_cpu"] = value / cb["value"]
+        cb["reference_python"] = ref_python(value, REF_PY_ARENA_SIMS_PER_CORE, cb["cores"],
+                                            "terminal random playout from ply 20, telemetry off")
+        line["cpu_baseline"] = cb
+    return line
 
-    if rank == 0:
-        avg_ms = sum(kernel_ms) / len(kernel_ms)
-        plies_per_sim = all_plies / sims
-        # SURVEY 8(d) algorithmic bytes: 256 B state read + 256 B write per ply, 32 B result
-        bytes_per_sim = 512.0 * plies_per_sim + 32.0
-        achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
-        traffic = valu_insts = None
-        tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
-        if os.path.exists(tpath) and args.order == "naive":  # PMC pass is of k_rollout
-            try:
-                tj = json.load(open(tpath))
-                traffic, valu_insts = tj.get("bytes_per_launch"), tj.get("valu_insts_per_launch")
-            except (OSError, ValueError):
-                traffic = valu_insts = None
-        # VALU view (the real limiter): wave64 VALU instructions per launch
-        # from the committed PMC pass (SQ_INSTS_VALU, same workload) x 64 lanes over the
-        # live launch time, against the dual-issue int32 VALU peak of 32 lanes/clk/SIMD
-        valu_tops = valu_insts * 64 / (avg_ms * 1e-3) / 1e12 if valu_insts else None
-        line = {
-            "metric": METRIC,
-            "value": value,
-            "unit": "sims/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic",
-            "config": {"workload": "config3: 256 concurrent games x 1024 random rollouts (arena semantics, "
-                                   f"{args.order} move order, Philox RNG) from GPU-generated 20-ply positions",
-                       "games": args.games, "rollouts_per_game": args.rollouts, "root_plies": args.root_plies,
-                       "playouts_per_step": n, "parallelism": f"dp{world} (independent games per rank)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_rollout_fr" if args.order == "frontier" else "k_rollout",
-                         "kernel_ms": avg_ms, "plies_per_sim": plies_per_sim},
-            "compute_roofline": {"bound": "valu_int32", "achieved": valu_tops, "peak": VALU_PEAK_TOPS,
-                                 "unit": "Tlane-op/s", "frac": valu_tops / VALU_PEAK_TOPS if valu_tops else None,
-                                 "peak_single_issue": VALU_SINGLE_TOPS,
-                                 "frac_single_issue": valu_tops / VALU_SINGLE_TOPS if valu_tops else None,
-                                 "valu_insts_per_launch": valu_insts},
-        }
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(roots_np, args.cpu_seconds)
-            line["cpu_baseline"]["gpu_over_cpu"] = value / line["cpu_baseline"]["value"]
+
+# ------------------------------------------------------------------ config 5
+def run_config5(args, world, rank, local, dist):
+    import numpy as np
+    import torch
+
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    from reinforcementlearning_blokus_amd.shard import shard_indices
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+
+    total = args.games or 65536
+    gpu = BlokusGPU(local)
+    dev = torch.device("cuda", local)
+    # the job's games are global indices 0..total-1 (position, rollout seed and zobrist
+    # table are functions of the index); rank r searches games r (mod W)
+    mine = shard_indices(total, rank, world)
+    roots_all, sets_all = frontier_roots(gpu, total, args.root_plies, seed=args.seed, distinct=None)
+    roots, sets = roots_all[mine], sets_all[mine]
+    batch = MctsBatch(gpu, roots, sets, iterations=args.iterations, seed0=0, index=mine)
+    stream = torch.cuda.current_stream(dev)
+    kms = []
+
+    def timed_run(stop_after=None):
+        kms.clear()
+        batch.reset()
+        batch.run(chunk=args.chunk, stop_after=stop_after, on_chunk=lambda k: kms.append(gpu.last_kernel_ms()))
+
+    for _ in range(args.warmup):  # warmup: the first 64 iterations of the same searches
+        timed_run(stop_after=64)
+    barrier_sync(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        timed_run()
+    barrier_sync(dist)
+    elapsed = time.perf_counter() - t0
+    res = batch.results()
+    sims_local = int(res["iterations_run"].sum()) * args.steps
+    plies_local = int(res["rollout_plies"].astype(np.int64).sum())
+    elapsed, (sims, plies, hits, rollouts) = reduce_max_sum(
+        dist, dev, elapsed, [sims_local, plies_local * args.steps, int(res["tt_hits"].sum()) * args.steps,
+                             int(res["rollouts"].sum()) * args.steps])
+    del stream
+    if rank != 0:
+        return None
+    value = sims / elapsed
+    kernel_ms = sum(kms)  # last step's launches (HIP events per chunk)
+    # SURVEY 8(d) bytes: 256 B state read + write per rollout ply + 32 B result per
+    # simulation; plus the tree/TT traffic a search cannot avoid: one TT probe (16 B),
+    # one node write (24 B) and a root-to-leaf path update per iteration (~2 x 24 B)
+    sims_rank0 = int(res["iterations_run"].sum())
+    bytes_rank0 = 2.0 * STATE_B * plies_local + (RESULT_B + 16 + 24 + 48) * sims_rank0
+    achieved = bytes_rank0 / (kernel_ms * 1e-3) / 1e9
+    traffic, valu_insts = traffic_for("k_mcts")
+    line = {
+        "metric": METRIC, "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32+f64", "data": "synthetic",
+        "config": {"workload": f"config5: {total} concurrent MCTSAgent searches x {args.iterations} iterations "
+                               "(UCT, Zobrist TT in HBM, 50-ply RandomAgent rollouts, reference frontier move "
+                               f"order, bit-exact) from GPU-generated {args.root_plies}-ply positions",
+                   "games": total, "iterations": args.iterations, "chunk": args.chunk,
+                   "simulations_per_step": total * args.iterations,
+                   "rollout_plies_per_sim": plies / sims, "tt_hit_rate": hits / sims,
+                   "parallelism": f"dp{world} (games sharded r mod {world})"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_mcts",
+                     "kernel_ms": kernel_ms, "launches": len(kms)},
+        "compute_roofline": compute_roofline(valu_insts / max(1, len(kms)) if valu_insts else None,
+                                             kernel_ms / max(1, len(kms))),
+    }
+    if not args.no_cpu_baseline and world == 1:
+        cb = cpu_baseline_mcts(roots, sets, batch, args.cpu_seconds)
+        cb["gpu_over_cpu"] = value / cb["value"]
+        cb["reference_python"] = ref_python(value, REF_PY_MCTS_RANDOM_SIMS, cb["cores"],
+                                            "MCTSAgent + RandomAgent rollouts, 100 iterations (one search)")
+        line["cpu_baseline"] = cb
+    return line
+
+
+def cpu_baseline_mcts(roots, sets, batch, seconds):
+    """or_mcts (C restatement of MCTSAgent.select_action, pinned by tests/golden/mcts.json)
+    on this host's cores: the same positions, zobrist tables and rollout streams, fewer
+    iterations per search (bounded sample)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import pyoracle as O
+    cpu = host_cpu()
+    threads = cpu["cores"]
+    ztabs = [O.zobrist_table(t) for t in range(len(batch.zobrist_np))]
+
+    def one(g, iters):
+        b = O.board_from(roots[g].tobytes(), sets[g])
+        m = O.numpy_mt(0)
+        m.mt[:] = batch.mt0[g, :624].tolist()
+        m.mti = int(batch.mt0[g, 624])
+        O.mcts(b, int(batch.players_np[g]), iters, 1.414, 50, ztabs[int(batch.zidx_np[g])], m, O.TT())
+        return iters
+
+    def run(n_search, iters):
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside or_mcts
+            sims = sum(ex.map(lambda g: one(g, iters), range(n_search)))
+        return sims, time.perf_counter() - t0
+
+    iters = 128
+    _, dt = run(threads, iters)
+    n_search = max(threads, int(threads * seconds / max(dt, 1e-3)))
+    n_search = min(n_search, len(roots))
+    sims, dt = run(n_search, iters)
+    return {"value": sims / dt, "unit": "sims/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+            "host": cpu, "order": "frontier",
+            "sample": f"{n_search} of the same searches at {iters} iterations each (oracle/blokus_oracle.c "
+                      f"or_mcts), {threads} threads (one per usable core), {dt:.1f} s"}
+
+
+# ------------------------------------------------------------------ config 2
+def run_config2(args, world, rank, local, dist):
+    import numpy as np
+    import torch
+
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU, empty_state
+
+    gpu = BlokusGPU(local)
+    dev = torch.device("cuda", local)
+    nb = args.boards
+    # 4,096 synthetic mid-game boards, plies uniform in 16..40 (SURVEY 8(d) config 2)
+    rng = np.random.RandomState(args.seed + rank)
+    plies = rng.randint(16, 41, size=nb)
+    parts = []
+    for m in range(16, 41):
+        k = int((plies == m).sum())
+        if k:
+            parts.append(gpu.advance(empty_state(), k, m, seed=args.seed * 41 + m + 1000 * rank,
+                                     root_index=np.zeros(k, dtype=np.int32)))
+    boards = np.concatenate(parts)
+    if args.all_players:
+        st = np.repeat(boards, 4)
+        pl = np.tile(np.arange(4, dtype=np.uint8), nb)
+    else:
+        st, pl = boards, (boards["current_player"] & 3).astype(np.uint8)
+    n = len(st)
+    states = torch.from_numpy(st.view(np.uint8).reshape(n, 256).copy()).to(dev)
+    players = torch.from_numpy(pl.copy()).to(dev)
+    stream = torch.cuda.Stream(dev)
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            cnt, rows = gpu.movegen(states, players)
+        barrier_sync(dist)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.steps):
+            cnt, rows = gpu.movegen(states, players)
+        e1.record(stream)
+        barrier_sync(dist)
+        elapsed = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    moves = int(cnt.to(torch.int64).sum().item())
+    elapsed, (pairs,) = reduce_max_sum(dist, dev, elapsed, [n * args.steps])
+    if rank != 0:
+        return None
+    value = pairs / elapsed
+    achieved = n * MOVEGEN_B / (kernel_ms * 1e-3) / 1e9
+    traffic, valu_insts = traffic_for("k_movegen")
+    line = {
+        "metric": "batched legal-move generation (board-players/s, 20x20, 4p)", "value": value,
+        "unit": "board-players/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": f"config2: {nb} synthetic mid-game boards (plies 16..40) x "
+                               f"{'all 4 players' if args.all_players else 'player to move'}: dense legal "
+                               "masks + counts (bk_movegen)", "boards": nb, "board_players": n,
+                   "legal_moves_per_board_player": moves / n, "us_per_batch": kernel_ms * 1e3,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen",
+                     "kernel_ms": kernel_ms, "bytes_per_board_player": MOVEGEN_B,
+                     "bytes_written_per_board_player": 256 + 91 * 20 * 4 + 4},
+        "compute_roofline": compute_roofline(valu_insts, kernel_ms),
+    }
+    if not args.no_cpu_baseline and world == 1:
+        line["cpu_baseline"] = cpu_baseline_movegen(st, pl, args.cpu_seconds, value)
+    return line
+
+
+def cpu_baseline_movegen(st, pl, seconds, value):
+    """oracle legal-move generation (reference frontier algorithm) on this host's cores."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import pyoracle as O
+    cpu = host_cpu()
+    threads = cpu["cores"]
+    boards = [O.unpack(O.State.from_buffer_copy(st[i].tobytes())) for i in range(len(st))]
+
+    def work(lo, hi):
+        for i in range(lo, hi):
+            O.legal_moves(boards[i], int(pl[i]), O.ORDER_FRONTIER)
+        return hi - lo
+
+    def run(n):
+        step = max(1, n // threads)
+        spans = [(i, min(n, i + step)) for i in range(0, n, step)]
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            done = sum(ex.map(lambda s: work(*s), spans))
+        return done, time.perf_counter() - t0
+
+    n, dt = run(min(len(boards), 4 * threads))
+    n2 = min(len(boards), max(n, int(n * seconds / max(dt, 1e-3))))
+    n2, dt = run(n2)
+    r = n2 / dt
+    return {"value": r, "unit": "board-players/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+            "host": cpu, "gpu_over_cpu": value / r,
+            "sample": f"{n2} of the same board-players, oracle/blokus_oracle.c frontier movegen, {threads} threads, "
+                      f"{dt:.1f} s (ctypes calls; the GIL is released inside)",
+            "reference_python": ref_python(value, REF_PY_MOVEGEN_BOARDS_PER_CORE, threads,
+                                           "get_legal_moves at ply 20 (boards/s/core)")}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = setup()
+    run = {"config3": run_config3, "config5": run_config5, "config2": run_config2}[args.workload]
+    line = run(args, world, rank, local, dist)
+    if line is not None:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -99,7 +99,8 @@ typedef struct bk_result {
     int16_t scores[BK_PLAYERS]; /* ARENA: BlokusGame.get_score (board + corner + centre bonus);
                                    ROLLOUT: Board.get_score (engine/board.py:562)             */
     uint8_t winner_mask;        /* bit p: p in GameResult.winner_ids (engine/game.py:216)    */
-    uint8_t status;             /* 0 ok; bit0: rng stream overflow (compat mode)             */
+    uint8_t status;             /* 0 ok; bit0: rng stream overflow (compat mode); bit1:
+                                   frontier table overflow; bit2: bad root_index (device path) */
     uint16_t plies;             /* moves placed during the playout                          */
     uint16_t passes;            /* arena passes (arena_runner.py:660-664)                   */
     uint16_t turns;             /* arena turn_count                                         */
@@ -120,6 +121,11 @@ int bk_destroy(bk_handle h);
    torch's default stream); BK_STREAM_OWN restores the handle's own stream. */
 #define BK_STREAM_OWN ((void*)~(uintptr_t)0)
 int bk_set_stream(bk_handle h, void* stream);
+/* Wait for the handle's stream.  Device-path launches (BK_MEM_DEVICE) return before the
+   kernel ends, so their input errors and guard trips surface here: BK_EOVERFLOW if a
+   persistent kernel's iteration guard tripped (results incomplete), BK_EINVAL if a
+   root_index entry was outside [0, n_roots) (that playout ran from root 0 with status
+   bit 2); both cleared once reported. */
 int bk_synchronize(bk_handle h);
 int bk_last_error(bk_handle h, char* buf, size_t len);
 
@@ -216,8 +222,9 @@ int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_
  * legal_offset[i+1]) (any int payload; only the count and order matter: expansion pops
  * the LAST entry first, fast_mcts_agent.py:62).  Each iteration expands an untried
  * child or picks the UCB1 argmax (first max in child order; exploration term
- * c*sqrt(2*log(root_visits)/visits) with log taken from log_table, which the host fills
- * with CPython math.log(i) for i < log_len), then adds reward = base[i] +
+ * c*(2*log(root_visits)/visits)**0.5 with log taken from log_table, which the host fills
+ * with CPython math.log(i) for i < log_len, and ** 0.5 reproduced bit for bit through the
+ * pow_fix tables of bk_pow_half_fix below), then adds reward = base[i] +
  * random()*0.1, random() being CPython random.Random's genrand_res53 from the state
  * mt_state[i] (625 words: random.getstate()[1]); a NaN base[i] means reward 0.0 with no
  * draw (empty cached legal list, fast_mcts_agent.py:255).  mt_state is in/out: the
@@ -240,7 +247,33 @@ typedef struct bk_fastmcts_out {
 
 int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,
                 const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
+                const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_len,
                 double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem);
+
+/*
+ * The exploration term is (2 * math.log(N) / v) ** 0.5 (fast_mcts_agent.py:52): CPython
+ * float ** calls C pow(), which in glibc is not correctly rounded, so for ~0.085 % of
+ * (N, v) it is one ulp off the correctly rounded sqrt() a GPU computes.  The kernel takes
+ * sqrt and applies the listed corrections.  bk_pow_half_fix computes them on the host with
+ * the process's own libm pow() (the function CPython calls):
+ *   for N in [0, log_len), v in [1, N]: x = (2.0 * log_table[N]) / v; if pow(x, 0.5) !=
+ *   sqrt(x), entry (v << 1) | (pow > sqrt) in entries[offsets[N] .. offsets[N + 1]).
+ * offsets: log_len + 1 ints.  Returns BK_OK; BK_EOVERFLOW with *n_entries = the count
+ * needed when cap is too small; BK_EINVAL if pow and sqrt ever differ by more than 1 ulp.
+ * bk_fastmcts reads offsets / entries as pow_fix_offsets / pow_fix_entries (pow_fix_len =
+ * the entry count); the same log_table must be passed to both.
+ */
+int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, int32_t* entries, int32_t cap,
+                    int32_t* n_entries);
+
+/* Diagnostics (no reference counterpart): one FastMCTS selection step on the device --
+   the UCB1 argmax (first max in child order) over n children with the given visits
+   (all > 0) and total rewards, parent visits N, with k_fastmcts's exact arithmetic and
+   pow corrections -- so tests can pin near-ties.  out_best: the chosen child index. */
+int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, const double* totals, uint32_t root_visits,
+                             const double* log_table, int32_t log_len, const int32_t* pow_fix_offsets,
+                             const int32_t* pow_fix_entries, int32_t pow_fix_len, double exploration,
+                             int32_t* out_best);
 
 /*
  * bk_mcts -- MCTSAgent.select_action searches (mcts/mcts_agent.py:304-582, MCTSNode
@@ -313,7 +346,7 @@ typedef struct bk_mcts_out {
     int32_t nodes_used;
     int32_t root_children;
     uint32_t status;         /* BK_MCTS_E* bits                                          */
-    int32_t reserved;
+    int32_t rollout_plies;   /* moves played by this search's rollouts (sum)             */
 } bk_mcts_out;
 
 int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const uint8_t* players,

@@ -742,7 +742,7 @@ uint64_t or_zobrist_hash(const or_board* b, const uint64_t* t) {
 
 /* ------------------------------------------------- CPU baseline batch driver ------- */
 typedef struct {
-    const bk_state* roots; int n_roots; int begin, end; uint64_t seed; int sem, max_plies;
+    const bk_state* roots; int n_roots; int begin, end; uint64_t seed; int sem, max_plies, order;
     bk_result* out;
 } batch_job;
 
@@ -754,10 +754,10 @@ static void* batch_worker(void* arg) {
         uint32_t seeds[4];
         for (int p = 0; p < 4; ++p) seeds[p] = (uint32_t)(j->seed * 2654435761u + (uint64_t)i * 4 + p);
         if (j->sem == BK_SEM_ARENA) {
-            or_playout_arena(b, seeds, BK_ORDER_FRONTIER, j->max_plies, &j->out[i], NULL, 0);
+            or_playout_arena(b, seeds, j->order, j->max_plies, &j->out[i], NULL, 0);
         } else {
             int32_t rw, pl, dr;
-            or_rollout_a(b, b->cur, seeds[0], BK_ORDER_FRONTIER, j->max_plies, &rw, &pl, &dr);
+            or_rollout_a(b, b->cur, seeds[0], j->order, j->max_plies, &rw, &pl, &dr);
             memset(&j->out[i], 0, sizeof(bk_result));
             j->out[i].reward = rw; j->out[i].plies = (uint16_t)pl;
         }
@@ -767,14 +767,14 @@ static void* batch_worker(void* arg) {
 }
 
 int or_batch_playouts(const bk_state* roots, int n_roots, int n_playouts, uint64_t seed,
-                      int semantics, int max_plies, int threads, bk_result* out) {
+                      int semantics, int max_plies, int threads, int order, bk_result* out) {
     or_init();
     if (threads < 1) threads = 1;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
     batch_job* jobs = (batch_job*)malloc(sizeof(batch_job) * (size_t)threads);
     for (int t = 0; t < threads; ++t) {
         jobs[t] = (batch_job){roots, n_roots, (int)((int64_t)n_playouts * t / threads),
-                              (int)((int64_t)n_playouts * (t + 1) / threads), seed, semantics, max_plies, out};
+                              (int)((int64_t)n_playouts * (t + 1) / threads), seed, semantics, max_plies, order, out};
         pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);

@@ -96,7 +96,7 @@ def lib():
             "or_zobrist_table": (None, [C.c_int64, P(C.c_uint64)]),
             "or_zobrist_hash": (C.c_uint64, [P(Board), P(C.c_uint64)]),
             "or_batch_playouts": (C.c_int, [P(State), C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
-                                            C.c_int, P(Result)]),
+                                            C.c_int, C.c_int, P(Result)]),
             "or_set_frontier_table": (C.c_int, [P(Board), C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
             "or_mcts": (C.c_int, [P(Board), C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int,
                                   C.c_void_p, P(MT), C.c_int, C.c_void_p, C.c_void_p, C.c_int,
@@ -242,9 +242,9 @@ def orient_table():
     return out
 
 
-def batch_playouts(states, n_playouts, seed, semantics=SEM_ARENA, max_plies=2500, threads=1):
+def batch_playouts(states, n_playouts, seed, semantics=SEM_ARENA, max_plies=2500, threads=1, order=ORDER_FRONTIER):
     out = (Result * n_playouts)()
-    lib().or_batch_playouts(states, len(states), n_playouts, seed, semantics, max_plies, threads, out)
+    lib().or_batch_playouts(states, len(states), n_playouts, seed, semantics, max_plies, threads, order, out)
     return out
 
 

@@ -30,7 +30,7 @@ EXPORTS = (
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
-    "bk_mcts", "bk_debug_sections",
+    "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select",
 )
 FSET_SLOTS = 256
 # bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
@@ -88,7 +88,7 @@ MCTS_NODE_DTYPE = np.dtype([("total", "<f8"), ("visits", "<u4"), ("child0", "<i4
 assert MCTS_NODE_DTYPE.itemsize == 24
 MCTS_OUT_DTYPE = np.dtype([("best_move", "<i4"), ("iterations_run", "<i4"), ("tt_hits", "<i4"),
                            ("rollouts", "<i4"), ("nodes_used", "<i4"), ("root_children", "<i4"),
-                           ("status", "<u4"), ("reserved", "<i4")])
+                           ("status", "<u4"), ("rollout_plies", "<i4")])
 assert MCTS_OUT_DTYPE.itemsize == 32
 MCTS_ZOBRIST_WORDS = 2088
 MCTS_MAX_DEPTH = 63
@@ -149,7 +149,11 @@ def load():
             "bk_has_moves": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int]),
             "bk_rollout": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
             "bk_advance": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
-            "bk_fastmcts": (C.c_int, [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32, C.c_double, vp, vp, C.c_int]),
+            "bk_fastmcts": (C.c_int, [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32, vp, vp, C.c_int32, C.c_double,
+                                      vp, vp, C.c_int]),
+            "bk_pow_half_fix": (C.c_int, [vp, C.c_int32, vp, vp, C.c_int32, P(C.c_int32)]),
+            "bk_debug_fastmcts_select": (C.c_int, [vp, C.c_int32, vp, vp, C.c_uint32, vp, C.c_int32, vp, vp,
+                                                   C.c_int32, C.c_double, P(C.c_int32)]),
             "bk_last_kernel_ms": (C.c_int, [vp, P(C.c_float)]),
             "bk_fset_init": (C.c_int, [vp]),
             "bk_fset_place": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32]),
@@ -179,6 +183,38 @@ def orient_table():
             raise NativeUnavailable("bk_orient_info failed")
         out.append((pid.value, o.value, [(offs[2 * k], offs[2 * k + 1]) for k in range(n.value)]))
     return out
+
+
+_POW_FIX = {}
+
+
+def pow_half_fix(log_table: np.ndarray):
+    """(offsets int32[len+1], entries int32[k]) of bk_pow_half_fix for this log table:
+    where CPython's (2*log(N)/v) ** 0.5 (libm pow) differs from sqrt by one ulp.  Host
+    only (no GPU); cached per table."""
+    lt = np.ascontiguousarray(log_table, dtype=np.float64)
+    key = lt.tobytes()
+    hit = _POW_FIX.get(key)
+    if hit is not None:
+        return hit
+    L = load()
+    off = np.zeros(len(lt) + 1, np.int32)
+    cap = max(64, len(lt) * 2)
+    while True:
+        ent = np.zeros(cap, np.int32)
+        k = C.c_int32()
+        rc = L.bk_pow_half_fix(lt.ctypes.data, len(lt), off.ctypes.data, ent.ctypes.data, cap, C.byref(k))
+        if rc == EOVERFLOW:
+            cap = int(k.value)
+            continue
+        if rc != OK:
+            raise RuntimeError(f"bk_pow_half_fix failed ({rc})")
+        break
+    res = (off, ent[: k.value].copy())
+    if len(_POW_FIX) > 8:
+        _POW_FIX.clear()
+    _POW_FIX[key] = res
+    return res
 
 
 def fset_new(n: int = 1) -> np.ndarray:
@@ -282,13 +318,24 @@ class Handle:
                                     n_playouts, C.byref(cfg), C.c_void_p(seeds_ptr or 0), C.c_void_p(out_ptr), mem)
         self.check(rc, "bk_rollout")
 
-    def fastmcts(self, n_games, offset_ptr, iters_ptr, base_ptr, mt_ptr, log_ptr, log_len, c, out_ptr, visits_ptr,
-                 mem):
+    def fastmcts(self, n_games, offset_ptr, iters_ptr, base_ptr, mt_ptr, log_ptr, log_len, fix_off_ptr, fix_ent_ptr,
+                 fix_len, c, out_ptr, visits_ptr, mem):
         with self._lock:
             rc = self._L.bk_fastmcts(self._h, n_games, C.c_void_p(offset_ptr), C.c_void_p(iters_ptr),
                                      C.c_void_p(base_ptr), C.c_void_p(mt_ptr), C.c_void_p(log_ptr), log_len,
+                                     C.c_void_p(fix_off_ptr), C.c_void_p(fix_ent_ptr or None), fix_len,
                                      float(c), C.c_void_p(out_ptr), C.c_void_p(visits_ptr or None), mem)
         self.check(rc, "bk_fastmcts")
+
+    def debug_fastmcts_select(self, n, visits_ptr, totals_ptr, root_visits, log_ptr, log_len, fix_off_ptr,
+                              fix_ent_ptr, fix_len, c) -> int:
+        best = C.c_int32(-1)
+        with self._lock:
+            rc = self._L.bk_debug_fastmcts_select(self._h, n, C.c_void_p(visits_ptr), C.c_void_p(totals_ptr),
+                                                  root_visits, C.c_void_p(log_ptr), log_len, C.c_void_p(fix_off_ptr),
+                                                  C.c_void_p(fix_ent_ptr or None), fix_len, float(c), C.byref(best))
+        self.check(rc, "bk_debug_fastmcts_select")
+        return best.value
 
     def rollout_frontier(self, roots_ptr, sets_ptr, n_roots, index_ptr, n_playouts, cfg: BkRolloutCfg, seeds_ptr,
                          out_ptr, states_ptr, osets_ptr, mem):

@@ -283,6 +283,13 @@ def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id:
                                               rng=N.RNG_NUMPY_MT, compat_seeds=seeds,
                                               max_plies=run_config.max_turns,
                                               root_index=np.zeros(n, dtype=np.int32), with_results=True)
+    # truncated = cut by max_turns while the game was not over (arena_runner.py:702):
+    # the kernel stops at the cap without looking ahead, so ask has_legal_moves of the
+    # final positions of the games that reached it
+    at_cap = np.flatnonzero(res["turns"].astype(np.int64) >= run_config.max_turns)
+    alive = np.zeros(n, dtype=bool)
+    if len(at_cap):
+        alive[at_cap] = gpu.has_moves(states[at_cap]) != 0
     dt = time.perf_counter() - t0
     out = []
     for i, gi in enumerate(idx):
@@ -304,7 +311,7 @@ def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id:
         out.append(_record(run_id=run_id, game_index=gi, game_seed=gseeds[i], run_config=run_config,
                            seats=seats[i], scores=scores, winner_ids=winners, is_tie=len(winners) > 1,
                            moves_made=int(states[i]["move_count"]), turn_count=turns, passes=int(r["passes"]),
-                           invalid=0, duration=dt / n, truncated=turns >= run_config.max_turns,
+                           invalid=0, duration=dt / n, truncated=bool(alive[i]),
                            per_agent=per_agent, error=None))
     return out
 

@@ -31,6 +31,7 @@
 //     and never returns to the host between plies.
 #include <hip/hip_runtime.h>
 
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -932,6 +933,11 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     return fs_place_pred(fs_ref(gfs, p, htab), fl->tmp, cells, n, addable);
 }
 
+// counter[2] of a handle: sticky error bits of device-path launches, reported (and
+// cleared) by bk_synchronize
+#define BK_STICKY_GUARD 1u  // a persistent kernel's iteration guard tripped: results incomplete
+#define BK_STICKY_ROOT 2u   // a root_index entry outside [0, n_roots)
+
 struct RolloutArgs {
     const bk_state* roots;
     int32_t n_roots;
@@ -1075,7 +1081,13 @@ __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const
 template <bool FR>
 __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot, int32_t pid,
                                            const uint64_t* htab) {
-    const int32_t ri = a.root_index ? a.root_index[pid] : (pid % a.n_roots);
+    int32_t ri = a.root_index ? a.root_index[pid] : (pid % a.n_roots);
+    bool bad_root = false;
+    if (ri < 0 || ri >= a.n_roots) {  // device-path input error: flagged, never read out of bounds
+        atomicOr(&a.counter[2], BK_STICKY_ROOT);
+        ri = 0;
+        bad_root = true;
+    }
     const bk_state* s = a.roots + ri;
     g.pid = pid;
     uint32_t occ[20];
@@ -1109,7 +1121,7 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
     g.root_score = board_score(g, g.cur);
     g.draws = 0;
     g.pcount = 0;
-    g.status = 0;
+    g.status = bad_root ? 4u : 0u;
     if constexpr (FR) {
         if (a.cfg.semantics == BK_SEM_ROLLOUT) {
             // MCTSAgent._rollout plays on sim = board.copy() (mcts/mcts_agent.py:470):
@@ -1215,7 +1227,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         }
         if (__ballot(!done) == 0ull) break;
         if (iter > a.max_iters) {  // safety valve: never spin forever
-            if (lane == 0) atomicOr(&a.counter[1], 1u);
+            if (lane == 0) { atomicOr(&a.counter[1], 1u); atomicOr(&a.counter[2], BK_STICKY_GUARD); }
             break;
         }
         SECT(1);
@@ -1369,20 +1381,6 @@ __device__ __forceinline__ double py_random(uint32_t* mt, int& idx, int lane) {
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
 }
 
-struct FastMctsArgs {
-    int32_t n_games;
-    const int32_t* offset;
-    const int32_t* iterations;
-    const double* base;
-    uint32_t* mt_state;
-    const double* log_table;
-    int32_t log_len;
-    double c;
-    bk_fastmcts_out* out;
-    int32_t* visits_out;  // optional: per legal index, flat by legal_offset
-    uint32_t* err;
-};
-
 // wave argmax of (value, index): larger value wins, ties -> smaller index
 __device__ __forceinline__ void wave_argmax(double& v, int& j) {
 #pragma unroll
@@ -1392,6 +1390,57 @@ __device__ __forceinline__ void wave_argmax(double& v, int& j) {
         if (ov > v || (ov == v && oj < j)) { v = ov; j = oj; }
     }
 }
+
+struct PowFix {  // bk_pow_half_fix tables: CPython's (2 log N / v) ** 0.5 vs sqrt
+    const int32_t* offsets;
+    const int32_t* entries;
+};
+
+// c * x ** 0.5 with x = L2 / v, L2 = 2 * math.log(N) (fast_mcts_agent.py:52): the IEEE
+// sqrt, moved one ulp where glibc's pow (what CPython calls) rounds the other way.  The
+// few corrections of this N are scanned by every lane (N is wave-uniform).
+__device__ __forceinline__ double fm_explore(double c, double L2, uint32_t v, uint32_t N, const PowFix& fx) {
+    double s = sqrt(L2 / (double)v);
+    const int32_t e0 = fx.offsets[N], e1 = fx.offsets[N + 1];
+    for (int32_t e = e0; e < e1; ++e) {
+        const int32_t w = fx.entries[e];
+        if ((uint32_t)(w >> 1) == v) {
+            const long long bits = __double_as_longlong(s);
+            s = __longlong_as_double((w & 1) ? bits + 1 : bits - 1);  // s > 0 here (v < N)
+        }
+    }
+    return c * s;
+}
+
+// UCB1 argmax over children [0, nch) (FastMCTSNode.select_child, fast_mcts_agent.py:55):
+// the first child with the largest total/visits + explore; one wave
+__device__ __forceinline__ int fm_select(const uint32_t* visits, const double* total, int nch, int lane,
+                                         double L2, uint32_t N, double c, const PowFix& fx) {
+    double best = -1.0 / 0.0;
+    int bj = 0x7fffffff;
+    for (int j = lane; j < nch; j += WAVE) {
+        const uint32_t vi = visits[j];
+        const double u = total[j] / (double)vi + fm_explore(c, L2, vi, N, fx);
+        if (u > best) { best = u; bj = j; }
+    }
+    wave_argmax(best, bj);
+    return bj;
+}
+
+struct FastMctsArgs {
+    int32_t n_games;
+    const int32_t* offset;
+    const int32_t* iterations;
+    const double* base;
+    uint32_t* mt_state;
+    const double* log_table;
+    int32_t log_len;
+    PowFix fix;
+    double c;
+    bk_fastmcts_out* out;
+    int32_t* visits_out;  // optional: per legal index, flat by legal_offset
+    uint32_t* err;
+};
 
 __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
     __shared__ uint32_t visits[BK_FASTMCTS_MAX_CHILDREN];
@@ -1420,16 +1469,7 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
         if (nch < n) {
             sel = nch++;  // expand: untried_moves.pop() -> child nch <-> legal[n - 1 - nch]
         } else {
-            const double L2 = 2.0 * a.log_table[root_visits];
-            double best = -1.0 / 0.0;
-            int bj = 0x7fffffff;
-            for (int j = lane; j < nch; j += WAVE) {
-                const double v = (double)visits[j];
-                const double u = total[j] / v + a.c * sqrt(L2 / v);
-                if (u > best) { best = u; bj = j; }
-            }
-            wave_argmax(best, bj);
-            sel = bj;
+            sel = fm_select(visits, total, nch, lane, 2.0 * a.log_table[root_visits], root_visits, a.c, a.fix);
         }
         // NaN base: the cached legal list was empty -> reward 0.0 and no draw
         // (fast_mcts_agent.py:255-257)
@@ -1479,6 +1519,13 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
         ++ntop;
     }
     if (lane == 0) o->n_top = ntop;
+}
+
+// bk_debug_fastmcts_select: one selection step of k_fastmcts on given child stats
+__global__ __launch_bounds__(WAVE) void k_fastmcts_select(const uint32_t* visits, const double* totals, int n,
+                                                          uint32_t N, double L2, double c, PowFix fx, int32_t* out) {
+    const int j = fm_select(visits, totals, n, threadIdx.x, L2, N, c, fx);
+    if (threadIdx.x == 0) *out = j;
 }
 
 // ------------------------------------------------------------------------------------
@@ -1537,7 +1584,7 @@ struct Mc {
     int32_t mode;
     int32_t depth;      // path[depth] = node being expanded / simulated
     int32_t node;
-    int32_t nodes_used, tt_cnt, hits, rollouts;
+    int32_t nodes_used, tt_cnt, hits, rollouts, rplies;
     int32_t root_player, root_cp;
     int32_t cur, player, plies, score0;
     uint32_t status, mt_pos, first, tt_slot;
@@ -1721,11 +1768,12 @@ __device__ __forceinline__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* 
         m.nodes_used = o.nodes_used;
         m.hits = o.tt_hits;
         m.rollouts = o.rollouts;
+        m.rplies = o.rollout_plies;
         m.status = o.status;
     } else {
         m.it = 0;
         m.nodes_used = 1;
-        m.hits = m.rollouts = 0;
+        m.hits = m.rollouts = m.rplies = 0;
         m.status = 0;
         bk_mcts_node* root = a.nodes + (size_t)g * a.cfg.node_cap;
         root->total = 0.0; root->visits = 0; root->child0 = -1;
@@ -1775,7 +1823,7 @@ __device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m) {
     o.nodes_used = m.nodes_used;
     o.root_children = root.n_exp;
     o.status = m.status;
-    o.reserved = 0;
+    o.rollout_plies = m.rplies;
     a.out[g] = o;
     a.mt[(size_t)g * (FM_N + 1) + FM_N] = m.mt_pos;
     if (a.cfg.use_tt) a.tt_count[g] = m.tt_cnt;
@@ -1935,7 +1983,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
         }
         if (__ballot(!done) == 0ull) break;
         if (step > a.max_steps) {  // safety valve: never spin forever
-            if (lane == 0) atomicOr(&a.counter[1], 1u);
+            if (lane == 0) { atomicOr(&a.counter[1], 1u); atomicOr(&a.counter[2], BK_STICKY_GUARD); }
             break;
         }
         SECT(8);
@@ -2045,6 +2093,7 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
         } else {
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             m.plies++;
+            m.rplies++;
             m.cur = (m.cur + 1) & 3;
             if (m.plies >= a.cfg.max_rollout_moves)
                 mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
@@ -2129,6 +2178,7 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
     if (e == hipSuccess) e = hipEventCreate(&h->ev0);
     if (e == hipSuccess) e = hipEventCreate(&h->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_counter, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(h->d_counter, 0, 4 * sizeof(uint32_t));
     hipDeviceProp_t prop;
     if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) {
@@ -2171,7 +2221,16 @@ int bk_set_stream(bk_handle h, void* stream) {
 
 int bk_synchronize(bk_handle h) {
     if (!h) return BK_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->cur));
+    uint32_t sticky = 0;
+    HIPCHK(h, hipMemcpy(&sticky, h->d_counter + 2, sizeof sticky, hipMemcpyDeviceToHost));
+    if (sticky) {
+        HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof sticky));
+        if (sticky & BK_STICKY_GUARD)
+            return set_err(h, BK_EOVERFLOW, "device-path launch: iteration guard tripped, results incomplete%s", "");
+        return set_err(h, BK_EINVAL, "device-path launch: root_index entry outside [0, n_roots)%s", "");
+    }
     return BK_OK;
 }
 
@@ -2317,6 +2376,10 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     int rc = stage_in(h, roots, sizeof(bk_state) * (size_t)n_roots, mem, &d_roots, &h->d_in, &h->d_in_cap);
     if (rc) return rc;
     if (root_index) {
+        if (mem == BK_MEM_HOST)
+            for (int32_t i = 0; i < n_playouts; ++i)
+                if (root_index[i] < 0 || root_index[i] >= n_roots)
+                    return set_err(h, BK_EINVAL, "bk_rollout: root_index entry outside [0, n_roots)%s", "");
         rc = stage_in(h, root_index, sizeof(int32_t) * (size_t)n_playouts, mem, &d_idx, &h->d_aux, &h->d_aux_cap);
         if (rc) return rc;
     }
@@ -2358,10 +2421,11 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         rc = grow(h, &h->d_fslab, &h->d_fslab_cap, sizeof(FsLane) * (size_t)nslots);
         if (rc) return rc;
     }
-    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
+    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
     const uint64_t per_lane = ((uint64_t)n_playouts + nslots - 1) / nslots + 1;
     const uint64_t per_game = (cfg->semantics == BK_SEM_ROLLOUT ? (uint64_t)cfg->max_plies + 2u : 100u);
-    const uint64_t iters = per_lane * per_game + 64u;
+    uint64_t iters = per_lane * per_game + 64u;
+    if (const char* dbg = getenv("BK_DEBUG_MAX_ITERS")) iters = strtoull(dbg, nullptr, 10);  // tests: force the guard
     RolloutArgs a{(const bk_state*)d_roots, n_roots, (const int32_t*)d_idx, n_playouts, *cfg,
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
@@ -2388,6 +2452,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         uint32_t ctr[4];
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipStreamSynchronize(h->cur));
+        if (ctr[2]) HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof(uint32_t)));  // reported here
         if (ctr[1]) return set_err(h, BK_EOVERFLOW, "bk_rollout: iteration guard tripped%s", "");
     }
     return BK_OK;
@@ -2474,22 +2539,87 @@ int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {
     return n;
 }
 
+int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, int32_t* entries, int32_t cap,
+                    int32_t* n_entries) {
+    if (!log_table || log_len < 1 || !offsets || cap < 0 || (cap > 0 && !entries) || !n_entries) return BK_EINVAL;
+    // through a volatile pointer: the call must reach libm's pow (what CPython's float
+    // ** calls), never a compiler rewrite of pow(x, 0.5) into sqrt(x)
+    double (*volatile powp)(double, double) = pow;
+    int32_t k = 0;
+    for (int32_t N = 0; N < log_len; ++N) {
+        offsets[N] = k;
+        const double L2 = 2.0 * log_table[N];
+        for (int32_t v = 1; v <= N; ++v) {
+            const double x = L2 / (double)v;
+            const double q = sqrt(x), p = powp(x, 0.5);
+            if (p == q) continue;
+            const double up = nextafter(q, INFINITY), dn = nextafter(q, -INFINITY);
+            if (p != up && p != dn) return BK_EINVAL;
+            if (k < cap) entries[k] = (v << 1) | (p > q ? 1 : 0);
+            ++k;
+        }
+    }
+    offsets[log_len] = k;
+    *n_entries = k;
+    return k > cap ? BK_EOVERFLOW : BK_OK;
+}
+
+int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, const double* totals,
+                             uint32_t root_visits, const double* log_table, int32_t log_len,
+                             const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_len,
+                             double exploration, int32_t* out_best) {
+    if (!h || n < 1 || !visits || !totals || !log_table || (int64_t)root_visits >= log_len || !pow_fix_offsets ||
+        pow_fix_len < 0 || (pow_fix_len > 0 && !pow_fix_entries) || !out_best ||
+        pow_fix_offsets[log_len] != pow_fix_len)
+        return set_err(h, BK_EINVAL, "bk_debug_fastmcts_select: invalid arguments%s", "");
+    for (int32_t j = 0; j < n; ++j)
+        if (visits[j] == 0) return set_err(h, BK_EINVAL, "bk_debug_fastmcts_select: visits must be > 0%s", "");
+    HIPCHK(h, hipSetDevice(h->device));
+    const size_t bv = sizeof(uint32_t) * n, bt = sizeof(double) * n, bo = sizeof(int32_t) * (size_t)(log_len + 1),
+                 be = sizeof(int32_t) * (size_t)(pow_fix_len + 1);
+    int rc = grow(h, &h->d_aux, &h->d_aux_cap, bt + bv + bo + be + 64);
+    if (rc) return rc;
+    char* p = (char*)h->d_aux;
+    double* d_t = (double*)p; p += bt;
+    uint32_t* d_v = (uint32_t*)p; p += bv;
+    int32_t* d_o = (int32_t*)p; p += bo;
+    int32_t* d_e = (int32_t*)p; p += be;
+    int32_t* d_out = (int32_t*)(((uintptr_t)p + 15) & ~(uintptr_t)15);
+    HIPCHK(h, hipMemcpyAsync(d_t, totals, bt, hipMemcpyHostToDevice, h->cur));
+    HIPCHK(h, hipMemcpyAsync(d_v, visits, bv, hipMemcpyHostToDevice, h->cur));
+    HIPCHK(h, hipMemcpyAsync(d_o, pow_fix_offsets, bo, hipMemcpyHostToDevice, h->cur));
+    if (pow_fix_len) HIPCHK(h, hipMemcpyAsync(d_e, pow_fix_entries, be - sizeof(int32_t), hipMemcpyHostToDevice, h->cur));
+    hipLaunchKernelGGL(k_fastmcts_select, dim3(1), dim3(WAVE), 0, h->cur, d_v, d_t, n, root_visits,
+                       2.0 * log_table[root_visits], exploration, PowFix{d_o, d_e}, d_out);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(out_best, d_out, sizeof(int32_t), hipMemcpyDeviceToHost, h->cur));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
+    return BK_OK;
+}
+
 int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,
                 const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
+                const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_len,
                 double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem) {
     if (!h || n_games < 0 || !legal_offset || !iterations || !base || !mt_state || !log_table || log_len <= 0 ||
+        !pow_fix_offsets || pow_fix_len < 0 || (pow_fix_len > 0 && !pow_fix_entries) ||
         !out || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
         return set_err(h, BK_EINVAL, "bk_fastmcts: invalid arguments%s", "");
+    if (mem == BK_MEM_HOST && pow_fix_offsets[log_len] != pow_fix_len)
+        return set_err(h, BK_EINVAL, "bk_fastmcts: pow_fix tables do not match log_len%s", "");
     if (n_games == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
     const size_t b_off = sizeof(int32_t) * (size_t)(n_games + 1), b_it = sizeof(int32_t) * (size_t)n_games,
                  b_base = sizeof(double) * (size_t)n_games, b_mt = sizeof(uint32_t) * 625 * (size_t)n_games,
-                 b_log = sizeof(double) * (size_t)log_len, b_out = sizeof(bk_fastmcts_out) * (size_t)n_games;
+                 b_log = sizeof(double) * (size_t)log_len, b_out = sizeof(bk_fastmcts_out) * (size_t)n_games,
+                 b_fo = sizeof(int32_t) * (size_t)(log_len + 1), b_fe = sizeof(int32_t) * (size_t)(pow_fix_len + 1);
     const int32_t* d_off = legal_offset;
     const int32_t* d_it = iterations;
     const double* d_base = base;
     uint32_t* d_mt = mt_state;
     const double* d_log = log_table;
+    const int32_t* d_fo = pow_fix_offsets;
+    const int32_t* d_fe = pow_fix_entries;
     bk_fastmcts_out* d_out = out;
     int32_t* d_vis = visits_out;
     int32_t n_legal_total = 0;
@@ -2503,7 +2633,7 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
     if (mem == BK_MEM_HOST) {
         // one staging buffer, 16-byte aligned sections
         auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-        const size_t tot = al(b_off) + al(b_it) + al(b_base) + al(b_mt) + al(b_log);
+        const size_t tot = al(b_off) + al(b_it) + al(b_base) + al(b_mt) + al(b_log) + al(b_fo) + al(b_fe);
         int rc = grow(h, &h->d_in, &h->d_in_cap, tot);
         if (rc) return rc;
         rc = grow(h, &h->d_out, &h->d_out_cap, b_out);
@@ -2513,7 +2643,11 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
         HIPCHK(h, hipMemcpyAsync(p, iterations, b_it, hipMemcpyHostToDevice, h->cur)); d_it = (const int32_t*)p; p += al(b_it);
         HIPCHK(h, hipMemcpyAsync(p, base, b_base, hipMemcpyHostToDevice, h->cur)); d_base = (const double*)p; p += al(b_base);
         HIPCHK(h, hipMemcpyAsync(p, mt_state, b_mt, hipMemcpyHostToDevice, h->cur)); d_mt = (uint32_t*)p; p += al(b_mt);
-        HIPCHK(h, hipMemcpyAsync(p, log_table, b_log, hipMemcpyHostToDevice, h->cur)); d_log = (const double*)p;
+        HIPCHK(h, hipMemcpyAsync(p, log_table, b_log, hipMemcpyHostToDevice, h->cur)); d_log = (const double*)p; p += al(b_log);
+        HIPCHK(h, hipMemcpyAsync(p, pow_fix_offsets, b_fo, hipMemcpyHostToDevice, h->cur)); d_fo = (const int32_t*)p; p += al(b_fo);
+        if (pow_fix_len)
+            HIPCHK(h, hipMemcpyAsync(p, pow_fix_entries, b_fe - sizeof(int32_t), hipMemcpyHostToDevice, h->cur));
+        d_fe = (const int32_t*)p;
         d_out = (bk_fastmcts_out*)h->d_out;
         if (visits_out) {
             rc = grow(h, &h->d_aux, &h->d_aux_cap, sizeof(int32_t) * (size_t)n_legal_total + 4);
@@ -2521,8 +2655,9 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
             d_vis = (int32_t*)h->d_aux;
         }
     }
-    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
-    FastMctsArgs a{n_games, d_off, d_it, d_base, d_mt, d_log, log_len, exploration, d_out, d_vis, h->d_counter + 1};
+    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
+    FastMctsArgs a{n_games, d_off, d_it, d_base, d_mt, d_log, log_len, PowFix{d_fo, d_fe}, exploration, d_out, d_vis,
+                   h->d_counter + 1};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     hipLaunchKernelGGL(k_fastmcts, dim3(n_games), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
@@ -2625,7 +2760,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     int khz = 0;
     HIPCHK(h, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
     if (khz <= 0) khz = 100000;
-    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->cur));
+    HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
     const uint64_t per_lane = ((uint64_t)n_games + nslots - 1) / nslots + 1;
     const uint64_t steps = per_lane * ((uint64_t)cfg->iterations + 1) * ((uint64_t)cfg->max_rollout_moves + 2) + 64;
     MctsArgs a{(const bk_state*)sec[0].dev, (const bk_fset*)sec[1].dev, (const uint8_t*)sec[2].dev,
@@ -2649,6 +2784,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     }
     HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
     HIPCHK(h, hipStreamSynchronize(h->cur));
+    if (ctr[2]) HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof(uint32_t)));  // reported here
     if (ctr[1]) return set_err(h, BK_EOVERFLOW, "bk_mcts: step guard tripped%s", "");
     return BK_OK;
 }

@@ -41,7 +41,30 @@ class BlokusGPU:
         return self.handle.last_kernel_ms()
 
     def synchronize(self):
+        """Wait for this handle's launches; raises if a device-path launch tripped its
+        iteration guard or read a bad root_index (bk_synchronize)."""
         self.handle.synchronize()
+
+    def _check_playout_tensors(self, roots, n_playouts, root_index, compat_seeds, out, rng):
+        import torch
+        _check_device_tensor(roots, "roots", torch.uint8, (roots.shape[0], 256), self.device)
+        if root_index is not None:
+            _check_device_tensor(root_index, "root_index", torch.int32, (root_index.shape[0],), self.device)
+            if root_index.shape[0] < n_playouts:
+                raise ValueError(f"root_index: {root_index.shape[0]} entries for {n_playouts} playouts")
+        if rng == N.RNG_NUMPY_MT:
+            if compat_seeds is None:
+                raise ValueError("compat rng needs compat_seeds")
+            if compat_seeds.dtype not in (torch.int32, torch.uint32):
+                raise ValueError(f"compat_seeds: expected int32/uint32, got {compat_seeds.dtype}")
+            _check_device_tensor(compat_seeds, "compat_seeds", compat_seeds.dtype, (compat_seeds.shape[0], 4),
+                                 self.device)
+            if compat_seeds.shape[0] < n_playouts:
+                raise ValueError("compat_seeds: fewer rows than playouts")
+        if out is not None:
+            _check_device_tensor(out, "out", torch.uint8, (out.shape[0], 32), self.device)
+            if out.shape[0] < n_playouts:
+                raise ValueError("out: fewer rows than playouts")
 
     # ------------------------------------------------------------------ movegen
     def movegen(self, states, players, rows: bool = True):
@@ -55,6 +78,8 @@ class BlokusGPU:
         if _is_torch(states):
             import torch
             n = states.shape[0]
+            _check_device_tensor(states, "states", torch.uint8, (n, 256), self.device)
+            _check_device_tensor(players, "players", torch.uint8, (n,), self.device)
             cnt = torch.empty(n, dtype=torch.int32, device=states.device)
             out = torch.empty((n, N.N_ORIENTS, 20), dtype=torch.int32, device=states.device) if rows else None
             self._stream_from_torch()
@@ -77,6 +102,7 @@ class BlokusGPU:
         if _is_torch(states):
             import torch
             n = states.shape[0]
+            _check_device_tensor(states, "states", torch.uint8, (n, 256), self.device)
             out = torch.empty(n, dtype=torch.uint8, device=states.device)
             self._stream_from_torch()
             self.handle.has_moves(states.data_ptr(), n, out.data_ptr(), N.MEM_DEVICE)
@@ -103,6 +129,7 @@ class BlokusGPU:
             dev = roots.device
             if out is None:
                 out = torch.empty((n_playouts, 32), dtype=torch.uint8, device=dev)
+            self._check_playout_tensors(roots, n_playouts, root_index, compat_seeds, out, rng)
             self._stream_from_torch()
             self.handle.rollout(roots.data_ptr(), roots.shape[0],
                                 root_index.data_ptr() if root_index is not None else 0, n_playouts, cfg,
@@ -111,7 +138,7 @@ class BlokusGPU:
             return out
         st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
         res = np.zeros(n_playouts, dtype=RESULT_DTYPE)
-        idx = np.ascontiguousarray(root_index, dtype=np.int32) if root_index is not None else None
+        idx = _host_root_index(root_index, n_playouts)
         seeds = np.ascontiguousarray(compat_seeds, dtype=np.uint32).reshape(-1, 4) if compat_seeds is not None else None
         if seeds is not None:
             assert seeds.shape[0] >= n_playouts
@@ -137,6 +164,9 @@ class BlokusGPU:
             assert semantics != N.SEM_ADVANCE, "device path: playout results only"
             if out is None:
                 out = torch.empty((n_playouts, 32), dtype=torch.uint8, device=roots.device)
+            self._check_playout_tensors(roots, n_playouts, root_index, compat_seeds, out, rng)
+            _check_device_tensor(root_sets, "root_sets", torch.uint8, (roots.shape[0], N.FSET_DTYPE.itemsize),
+                                 self.device)
             self._stream_from_torch()
             self.handle.rollout_frontier(roots.data_ptr(), root_sets.data_ptr(), roots.shape[0],
                                          root_index.data_ptr() if root_index is not None else 0, n_playouts, cfg,
@@ -146,7 +176,7 @@ class BlokusGPU:
         st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
         fs = np.ascontiguousarray(root_sets, dtype=N.FSET_DTYPE)
         assert fs.shape[0] == st.shape[0]
-        idx = np.ascontiguousarray(root_index, dtype=np.int32) if root_index is not None else None
+        idx = _host_root_index(root_index, n_playouts)
         seeds = np.ascontiguousarray(compat_seeds, dtype=np.uint32).reshape(-1, 4) if compat_seeds is not None else None
         if seeds is not None:
             assert seeds.shape[0] >= n_playouts
@@ -177,6 +207,7 @@ class BlokusGPU:
         if _is_torch(roots):
             import torch
             out = torch.empty((n, 256), dtype=torch.uint8, device=roots.device)
+            self._check_playout_tensors(roots, n, root_index, None, None, N.RNG_PHILOX)
             self._stream_from_torch()
             self.handle.advance(roots.data_ptr(), roots.shape[0],
                                 root_index.data_ptr() if root_index is not None else 0, n, cfg, 0,
@@ -184,7 +215,7 @@ class BlokusGPU:
             return out
         st = np.ascontiguousarray(roots).view(np.uint8).reshape(-1, 256)
         out = np.zeros(n, dtype=STATE_DTYPE)
-        idx = np.ascontiguousarray(root_index, dtype=np.int32) if root_index is not None else None
+        idx = _host_root_index(root_index, n)
         self.handle.set_stream(None)
         self.handle.advance(st.ctypes.data, st.shape[0], idx.ctypes.data if idx is not None else 0, n, cfg, 0,
                             out.ctypes.data, N.MEM_HOST)
@@ -207,13 +238,27 @@ class BlokusGPU:
         b = np.ascontiguousarray(base, dtype=np.float64)
         assert mt_state.dtype == np.uint32 and mt_state.shape == (n, 625) and mt_state.flags.c_contiguous
         lt = np.ascontiguousarray(log_table, dtype=np.float64)
+        fo, fe = N.pow_half_fix(lt)
         out = np.zeros(n, dtype=N.FASTMCTS_OUT_DTYPE)
         vis = np.zeros(max(int(off[-1]), 1), dtype=np.int32) if want_visits else None
         self.handle.set_stream(None)
         self.handle.fastmcts(n, off.ctypes.data, it.ctypes.data, b.ctypes.data, mt_state.ctypes.data,
-                             lt.ctypes.data, len(lt), exploration, out.ctypes.data,
-                             vis.ctypes.data if vis is not None else 0, N.MEM_HOST)
+                             lt.ctypes.data, len(lt), fo.ctypes.data, fe.ctypes.data if len(fe) else 0, len(fe),
+                             exploration, out.ctypes.data, vis.ctypes.data if vis is not None else 0, N.MEM_HOST)
         return (out, vis[: int(off[-1])]) if want_visits else out
+
+    def fastmcts_select(self, visits, totals, root_visits: int, log_table, exploration: float) -> int:
+        """Diagnostic: k_fastmcts's UCB1 argmax (FastMCTSNode.select_child,
+        fast_mcts_agent.py:45-56) over children with these visits / total rewards."""
+        v = np.ascontiguousarray(visits, dtype=np.uint32)
+        t = np.ascontiguousarray(totals, dtype=np.float64)
+        assert len(v) == len(t) and len(v) > 0
+        lt = np.ascontiguousarray(log_table, dtype=np.float64)
+        fo, fe = N.pow_half_fix(lt)
+        self.handle.set_stream(None)
+        return self.handle.debug_fastmcts_select(len(v), v.ctypes.data, t.ctypes.data, int(root_visits), lt.ctypes.data,
+                                                 len(lt), fo.ctypes.data, fe.ctypes.data if len(fe) else 0, len(fe),
+                                                 exploration)
 
     # ------------------------------------------------------------------ MCTSAgent
     def mcts(self, roots, root_sets, players, root_hash, *, iterations: int, zobrist, mt_state,
@@ -281,7 +326,7 @@ class BlokusGPU:
     def mcts_device(self, roots, root_sets, players, root_hash, zobrist, zobrist_index, mt_state, log_table, nodes,
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
                     hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
-                    on_chunk=None):
+                    on_chunk=None, stop_after: int | None = None):
         """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
@@ -291,7 +336,9 @@ class BlokusGPU:
         tt_vals float64 [n, tt_cap] (NaN = empty) + tt_count int32[n] (all or none),
         rewards float64 / hit_flags uint8 [n, iterations] (optional).  chunk > 0 splits
         the searches into launches of `chunk` iterations; on_chunk(done_iterations) is
-        called after each.  Raises if any search reports a nonzero status."""
+        called after each; stop_after: run only the first stop_after iterations (they
+        can be resumed by no caller here: a warm-up).  Raises if any search reports a
+        nonzero status."""
         import torch
         n = roots.shape[0]
         use_tt = tt_keys is not None
@@ -314,7 +361,10 @@ class BlokusGPU:
         _check_device_tensor(log_table, "log_table", torch.float64, (log_table.shape[0],), self.device)
         self._stream_from_torch()
         d = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
-        for j, stop in enumerate(mcts_chunks(iterations, chunk)):
+        stops = mcts_chunks(iterations, chunk)
+        if stop_after is not None and 0 < stop_after < iterations:
+            stops = [x for x in stops if 0 < x < stop_after] + [stop_after]
+        for j, stop in enumerate(stops):
             cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
                               tt_keys.shape[1] if use_tt else 0, 0, stop, int(j > 0))
             self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
@@ -327,6 +377,15 @@ class BlokusGPU:
         if bad:
             raise RuntimeError(f"bk_mcts: {bad} searches stopped early, status bits "
                                f"{sorted(set(st[st != 0].tolist()))[:8]}")
+
+
+def _host_root_index(root_index, n_playouts):
+    if root_index is None:
+        return None
+    idx = np.ascontiguousarray(root_index, dtype=np.int32)
+    if idx.ndim != 1 or idx.shape[0] < n_playouts:
+        raise ValueError(f"root_index: need {n_playouts} entries, got shape {idx.shape}")
+    return idx
 
 
 def _check_device_tensor(t, name, dtype, shape, device):

@@ -199,14 +199,17 @@ class MCTSAgent:
                 todo.append(i)
         if not todo:
             return out
-        groups = {}  # agents sharing (iterations, rollout cap, c, TT on/off) share a launch
+        groups = {}  # agents sharing (iterations, rollout cap, c, TT on/off, time limit) share a launch
         for i in todo:
             a = agents[i]
-            if a.time_limit:
-                raise ValueError("rollout_backend='search' runs a fixed iteration count (time_limit unsupported)")
-            key = (int(a.iterations), a.max_rollout_moves, float(a.exploration_constant), a.use_transposition_table)
+            # time_limit (seconds, mcts_agent.py:325-333): iterate until it runs out; the
+            # kernel stops each search at the first iteration boundary past it, with the
+            # iteration count bounded by `iterations` (the node pool / log table size)
+            tl_us = int(round(float(a.time_limit) * 1e6)) if a.time_limit else 0
+            key = (int(a.iterations), a.max_rollout_moves, float(a.exploration_constant), a.use_transposition_table,
+                   tl_us)
             groups.setdefault(key, []).append(i)
-        for (iters, max_roll, c, use_tt), idx in groups.items():
+        for (iters, max_roll, c, use_tt, tl_us), idx in groups.items():
             ags = [agents[i] for i in idx]
             gpu = ags[0]._gpu = ags[0]._gpu or BlokusGPU(ags[0].device)
             roots = np.concatenate([pack_state(boards[i]) for i in idx])
@@ -231,7 +234,7 @@ class MCTSAgent:
                         tt.load(j, *a._gpu_tt.items(0))
             t0 = time.time()
             r = gpu.mcts(roots, sets, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
-                         mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c)
+                         mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us)
             dt = time.time() - t0
             for j, (i, a) in enumerate(zip(idx, ags)):
                 o = r["out"][j]

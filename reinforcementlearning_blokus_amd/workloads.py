@@ -42,13 +42,14 @@ def numpy_mt_states(seeds) -> np.ndarray:
 class MctsBatch:
     """Device-resident inputs and outputs of one bk_mcts batch (config 5 layout).
 
-    Game g searches roots[g] for its player to move, with zobrist table g % n_tables
-    (ZobristHash(seed=table), mcts/zobrist.py:41-68) and a rollout RandomAgent seeded
-    seed0 + g.  Each game has its own TT of tt_cap slots (<= half full after
+    Game g (global index i = index[g]) searches roots[g] for its player to move, with
+    zobrist table i % n_tables (ZobristHash(seed=table), mcts/zobrist.py:41-68) and a
+    rollout RandomAgent seeded seed0 + i.  Each game has its own TT of tt_cap slots (<= half full after
     `iterations` inserts) and a node pool of 4 * iterations + 1 slots."""
 
     def __init__(self, gpu: BlokusGPU, roots: np.ndarray, sets: np.ndarray, *, iterations: int, seed0: int = 0,
-                 n_tables: int = 8, use_tt: bool = True, want_rewards: bool = False, max_rollout_moves: int = 50):
+                 n_tables: int = 8, use_tt: bool = True, want_rewards: bool = False, max_rollout_moves: int = 50,
+                 index=None):
         import torch
 
         from .mcts.zobrist import ZobristHash, flat_keys, hash_states
@@ -58,13 +59,16 @@ class MctsBatch:
         self.roots_np, self.sets_np = roots, sets
         self.players_np = np.asarray(roots["current_player"], np.uint8) & 3
         zob = np.stack([flat_keys(ZobristHash(seed=t)) for t in range(n_tables)])
-        zi = (np.arange(n) % n_tables).astype(np.int32)
+        # global game indices (a rank's shard of a multi-GPU job): seeds and tables follow them
+        self.index = np.arange(n) if index is None else np.asarray(index, dtype=np.int64)
+        assert len(self.index) == n
+        zi = (self.index % n_tables).astype(np.int32)
         rh = np.zeros(n, np.uint64)
         for t in range(n_tables):
             sel = zi == t
             rh[sel] = hash_states(roots[sel], zob[t])
         self.zobrist_np, self.zidx_np, self.hash_np = zob, zi, rh
-        self.mt0 = numpy_mt_states(seed0 + g for g in range(n))
+        self.mt0 = numpy_mt_states(seed0 + int(g) for g in self.index)
         u8 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)).to(dev)  # noqa: E731
         self.roots, self.sets = u8(roots), u8(sets)
         self.players = torch.from_numpy(self.players_np.copy()).to(dev)
@@ -98,12 +102,15 @@ class MctsBatch:
             self.tt_vals.fill_(float("nan"))
             self.tt_count.zero_()
 
-    def run(self, chunk: int = 0, on_chunk=None):
+    def run(self, chunk: int = 0, on_chunk=None, stop_after: int | None = None):
+        """Run the searches (launches of `chunk` iterations); stop_after: only the
+        first stop_after iterations (a warm-up)."""
         self.gpu.mcts_device(self.roots, self.sets, self.players, self.root_hash, self.zobrist, self.zidx, self.mt,
                              self.log_table, self.nodes, self.out, iterations=self.iterations,
                              tt_keys=self.tt_keys, tt_vals=self.tt_vals, tt_count=self.tt_count,
                              rewards=self.rewards, hit_flags=self.hit_flags,
-                             max_rollout_moves=self.max_rollout_moves, chunk=chunk, on_chunk=on_chunk)
+                             max_rollout_moves=self.max_rollout_moves, chunk=chunk, on_chunk=on_chunk,
+                             stop_after=stop_after)
 
     def results(self) -> np.ndarray:
         return self.out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(-1)

@@ -23,6 +23,20 @@ def test_gpu_arena_games_match_reference_records():
             assert got[k] == ref[k], (ref["game_index"], k)
 
 
+def test_gpu_arena_games_cut_by_max_turns():
+    """Games whose max_turns equals their natural length end by their own last move (not
+    truncated); with 5 turns fewer they are cut (truncated) -- arena_runner.py:653, :702
+    (tests/golden/arena_cap.json)."""
+    fx = load_golden("arena_cap.json")
+    base = load_golden("arena_runs.json")["config"]
+    for ref in fx:
+        cfg = RunConfig.from_dict(dict(base, max_turns=ref["max_turns"]))
+        got = run_games_gpu(cfg, [ref["game_index"]])[0]
+        for k in ("seat_assignment", "winner_ids", "final_scores", "moves_made", "turn_count", "passes", "is_tie",
+                  "truncated"):
+            assert got[k] == ref[k], (ref["game_index"], ref["max_turns"], k)
+
+
 def test_gpu_arena_round_robin_small():
     cfg = RunConfig.from_dict({"agents": [{"name": f"r{i}", "type": "random"} for i in range(4)], "num_games": 2,
                                "seed": 20260301, "seat_policy": "round_robin"})

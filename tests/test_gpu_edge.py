@@ -129,3 +129,47 @@ def test_device_pointer_path_equals_host_path(gpu):
     res_d = gpu.rollout(dst, 2000, root_index=torch.from_numpy(idx).cuda(), seed=5)
     torch.cuda.synchronize()
     assert np.array_equal(res_d.cpu().numpy().view(N.RESULT_DTYPE).reshape(-1), res_h)
+
+
+def test_root_index_is_validated(gpu):
+    """Host path: an index outside [0, n_roots) or a short index array is EINVAL /
+    ValueError before any launch.  Device path: int64 or short tensors are rejected in
+    Python; an out-of-range entry runs from root 0 with status bit 2 and is reported by
+    the next synchronize (bk_synchronize), never read out of bounds."""
+    import torch
+    roots = pack_many([replay(POS[8]), replay(POS[9])])
+    with pytest.raises(RuntimeError, match="root_index"):
+        gpu.rollout(roots, 3, root_index=np.array([0, 1, 2], np.int32))
+    with pytest.raises(ValueError):
+        gpu.rollout(roots, 3, root_index=np.array([0, 1], np.int32))
+    droots = torch.from_numpy(roots.view(np.uint8).reshape(-1, 256).copy()).cuda()
+    with pytest.raises(ValueError):  # int64 indices would be read as int32 pairs
+        gpu.rollout(droots, 3, root_index=torch.arange(3, device="cuda") % 2)
+    with pytest.raises(ValueError):
+        gpu.rollout(droots, 3, root_index=torch.zeros(2, dtype=torch.int32, device="cuda"))
+    with pytest.raises(ValueError):  # host tensor on the device path
+        gpu.rollout(droots, 3, root_index=torch.zeros(3, dtype=torch.int32))
+    bad = torch.tensor([0, 5, 1], dtype=torch.int32, device="cuda")
+    out = gpu.rollout(droots, 3, root_index=bad, seed=1)
+    with pytest.raises(RuntimeError, match="root_index"):
+        gpu.synchronize()
+    res = out.cpu().numpy().view(N.RESULT_DTYPE).reshape(-1)
+    assert res["status"].tolist() == [0, 4, 0]
+    gpu.synchronize()  # reported once, then cleared
+
+
+def test_device_iteration_guard_is_reported(gpu, monkeypatch):
+    """A persistent-kernel guard trip on the device path (forced with a tiny iteration
+    budget) is surfaced by synchronize() instead of leaving unplayed rows unreported."""
+    import torch
+    roots = pack_many([replay(POS[8])])
+    droots = torch.from_numpy(roots.view(np.uint8).reshape(-1, 256).copy()).cuda()
+    monkeypatch.setenv("BK_DEBUG_MAX_ITERS", "3")
+    gpu.rollout(droots, 512, seed=2)
+    with pytest.raises(RuntimeError, match="guard"):
+        gpu.synchronize()
+    with pytest.raises(RuntimeError, match="guard"):  # the host path reports it at once
+        gpu.rollout(roots, 512, seed=2)
+    monkeypatch.delenv("BK_DEBUG_MAX_ITERS")
+    gpu.rollout(droots, 512, seed=2)
+    gpu.synchronize()

@@ -200,3 +200,23 @@ def test_agent_search_batch_equals_sequential():
             kx, vx = x._gpu_tt.items(0)
             ky, vy = y._gpu_tt.items(0)
             assert dict(zip(kx.tolist(), vx.tolist())) == dict(zip(ky.tolist(), vy.tolist()))
+
+
+def test_agent_time_limit_runs_on_the_search_backend():
+    """MCTSAgent(time_limit=..., rollout_agent=RandomAgent) -- a valid reference
+    configuration (mcts_agent.py:327-333) -- searches on the GPU until the limit (bounded
+    by `iterations`) and returns one of the legal moves."""
+    from reinforcementlearning_blokus_amd.agents.random_agent import RandomAgent
+    from reinforcementlearning_blokus_amd.engine.board import Player
+    from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator, move_to_int
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
+    from tests.helpers import engine_board
+    rec = POS[20]
+    board = engine_board(rec)
+    cur = Player(rec["state"]["current_player"])
+    legal = get_shared_generator().get_legal_moves(board, cur)
+    agent = MCTSAgent(iterations=100000, time_limit=0.05, rollout_agent=RandomAgent(seed=3), seed=1)
+    assert agent.rollout_backend == "search"
+    mv = agent.select_action(board, cur, legal)
+    assert move_to_int(mv) in {move_to_int(m) for m in legal}
+    assert 1 <= agent.stats["iterations_run"] < 100000

@@ -28,6 +28,7 @@ What is recorded (all reference behaviour, nothing re-implemented here):
 * ``fastmcts.json``    -- FastMCTSAgent.think results (agents/fast_mcts_agent.py:112)
 * ``zobrist.json``     -- ZobristHash.hash_board values (mcts/zobrist.py:70)
 * ``arena_small.json`` -- run_single_game records for 4 random agents
+* ``arena_cap.json`` -- run_single_game records cut by (or ending exactly at) max_turns
 * ``mcts.json``        -- MCTSAgent (UCT + Zobrist transposition table) searches with
                           RandomAgent rollouts (mcts/mcts_agent.py:304-582): two
                           consecutive select_action calls per agent, the root children
@@ -333,6 +334,38 @@ def gen_arena_runs():
     return {"config": ARENA_RUN, "games": games, "summary_input": synth, "summary": summary}
 
 
+def _arena_cap_game(job):
+    """run_single_game of ARENA_RUN game gi with max_turns = cap (None: default)."""
+    gi, cap = job
+    _setup()
+    from analytics.tournament.arena_runner import (RunConfig, _seat_assignment_for_game, game_seed_from_run_seed,
+                                                   run_single_game)
+    d = dict(ARENA_RUN)
+    if cap is not None:
+        d["max_turns"] = cap
+    cfg = RunConfig.from_dict(d)
+    gs = game_seed_from_run_seed(cfg.seed, gi)
+    seats = _seat_assignment_for_game([a.name for a in cfg.agents], gi, gs, cfg.seat_policy)
+    rec, _ = run_single_game(run_id="fx4", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                             agent_configs={a.name: a for a in cfg.agents})
+    keep = ("game_index", "game_seed", "seat_assignment", "winner_ids", "final_scores", "moves_made", "turn_count",
+            "passes", "is_tie", "truncated")
+    out = {k: rec[k] for k in keep}
+    out["max_turns"] = cfg.max_turns
+    return out
+
+
+def gen_arena_cap():
+    """Games cut by max_turns (arena_runner.py:653, :702): for ARENA_RUN games 0..3 the
+    full game's turn count T, then the same game with max_turns = T (it ends by its own
+    last move exactly at the cap: NOT truncated) and max_turns = T - 5 (truncated)."""
+    with Pool(8) as pool:
+        full = pool.map(_arena_cap_game, [(gi, None) for gi in range(4)])
+        jobs = [(r["game_index"], r["turn_count"]) for r in full] + \
+               [(r["game_index"], r["turn_count"] - 5) for r in full]
+        return pool.map(_arena_cap_game, jobs)
+
+
 # (position index, iterations, max_rollout_moves, use_tt, rollout seed, zobrist seed)
 MCTS_CASES = [
     (8, 24, 50, True, 11, 3), (12, 40, 50, True, 12, 4), (16, 24, 50, False, 13, 5),
@@ -595,6 +628,8 @@ def main():
         dump("arena_small.json", gen_arena())
     if what in ("all", "arena_runs"):
         dump("arena_runs.json", gen_arena_runs())
+    if what in ("all", "arena_cap"):
+        dump("arena_cap.json", gen_arena_cap())
     if what in ("all", "mcts"):
         with Pool(8) as pool:
             dump("mcts.json", pool.map(gen_mcts_case, MCTS_CASES))
