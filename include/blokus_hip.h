@@ -100,7 +100,10 @@ typedef struct bk_result {
                                    ROLLOUT: Board.get_score (engine/board.py:562)             */
     uint8_t winner_mask;        /* bit p: p in GameResult.winner_ids (engine/game.py:216)    */
     uint8_t status;             /* 0 ok; bit0: rng stream overflow (compat mode); bit1:
-                                   frontier table overflow; bit2: bad root_index (device path) */
+                                   frontier table overflow; bit2: bad root_index (device path);
+                                   bit3: ARENA run stopped by the max_plies turn cap before
+                                   every player was known to be stuck (passes / turns are
+                                   then raw and reserved[0] = passes since the last move)  */
     uint16_t plies;             /* moves placed during the playout                          */
     uint16_t passes;            /* arena passes (arena_runner.py:660-664)                   */
     uint16_t turns;             /* arena turn_count                                         */
@@ -205,7 +208,8 @@ int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap);
  * bk_rollout / bk_advance in the reference's FRONTIER order (cfg->order ==
  * BK_ORDER_FRONTIER): root_sets[n_roots] carry the roots' frontier tables; with
  * BK_RNG_NUMPY_MT the playouts are the reference's default-config games move for move.
- * BK_SEM_ARENA / BK_SEM_ROLLOUT: out[n_playouts]; out_states and out_sets NULL.
+ * BK_SEM_ARENA / BK_SEM_ROLLOUT: out[n_playouts]; ARENA may also ask for the final
+ * states and tables (out_states and out_sets both set, else both NULL).
  * BK_SEM_ROLLOUT starts from set.copy() of the root tables, as MCTSAgent._rollout plays
  * on sim = board.copy() (mcts/mcts_agent.py:470).
  * BK_SEM_ADVANCE: out_states[n_playouts] and out_sets[n_playouts] (out may be NULL).
@@ -247,7 +251,7 @@ typedef struct bk_fastmcts_out {
 
 int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,
                 const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
-                const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_len,
+                const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_rows,
                 double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem);
 
 /*
@@ -256,14 +260,17 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
  * (N, v) it is one ulp off the correctly rounded sqrt() a GPU computes.  The kernel takes
  * sqrt and applies the listed corrections.  bk_pow_half_fix computes them on the host with
  * the process's own libm pow() (the function CPython calls):
- *   for N in [0, log_len), v in [1, N]: x = (2.0 * log_table[N]) / v; if pow(x, 0.5) !=
+ *   for N in [0, rows), v in [1, N]: x = (2.0 * log_table[N]) / v; if pow(x, 0.5) !=
  *   sqrt(x), entry (v << 1) | (pow > sqrt) in entries[offsets[N] .. offsets[N + 1]).
- * offsets: log_len + 1 ints.  Returns BK_OK; BK_EOVERFLOW with *n_entries = the count
- * needed when cap is too small; BK_EINVAL if pow and sqrt ever differ by more than 1 ulp.
- * bk_fastmcts reads offsets / entries as pow_fix_offsets / pow_fix_entries (pow_fix_len =
- * the entry count); the same log_table must be passed to both.
+ * offsets: rows + 1 ints.  Cost ~N^2/2 sqrt (pow only near rounding midpoints, where it
+ * can differ).  Returns BK_OK; BK_EOVERFLOW with *n_entries = the count needed when cap is
+ * too small; BK_EINVAL if pow and sqrt ever differ by more than 1 ulp.
+ * bk_fastmcts reads offsets / entries as pow_fix_offsets / pow_fix_entries with
+ * pow_fix_rows = rows (<= log_len, same log_table): selections at root visits N >= rows
+ * use the plain sqrt (the host builds rows up to 16,385: exact for searches of up to
+ * 16,384 iterations).
  */
-int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, int32_t* entries, int32_t cap,
+int bk_pow_half_fix(const double* log_table, int32_t rows, int32_t* offsets, int32_t* entries, int32_t cap,
                     int32_t* n_entries);
 
 /* Diagnostics (no reference counterpart): one FastMCTS selection step on the device --
@@ -272,7 +279,7 @@ int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, 
    pow corrections -- so tests can pin near-ties.  out_best: the chosen child index. */
 int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, const double* totals, uint32_t root_visits,
                              const double* log_table, int32_t log_len, const int32_t* pow_fix_offsets,
-                             const int32_t* pow_fix_entries, int32_t pow_fix_len, double exploration,
+                             const int32_t* pow_fix_entries, int32_t pow_fix_rows, double exploration,
                              int32_t* out_best);
 
 /*

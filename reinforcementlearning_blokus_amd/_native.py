@@ -185,36 +185,43 @@ def orient_table():
     return out
 
 
-_POW_FIX = {}
+POW_FIX_ROWS = 16385  # FastMCTS UCB bit-exact for searches of up to 16,384 iterations
+_POW_FIX = {"lt": np.zeros(0), "off": np.zeros(1, np.int32), "ent": np.zeros(0, np.int32)}
 
 
-def pow_half_fix(log_table: np.ndarray):
-    """(offsets int32[len+1], entries int32[k]) of bk_pow_half_fix for this log table:
-    where CPython's (2*log(N)/v) ** 0.5 (libm pow) differs from sqrt by one ulp.  Host
-    only (no GPU); cached per table."""
+def pow_half_fix(log_table: np.ndarray, rows: int | None = None, cached_only: bool = False):
+    """(offsets int32[rows+1], entries int32[k]) of bk_pow_half_fix: the (N, v), N < rows,
+    where CPython's (2*log(N)/v) ** 0.5 (libm pow) differs from sqrt by one ulp.
+    rows defaults to min(len(log_table), POW_FIX_ROWS).  Host only (no GPU).  The largest
+    table built so far is kept; a smaller request is its prefix.  cached_only: never
+    build, return at most what is cached (for wall-clock-bounded searches, whose
+    iteration count -- hence reference parity -- depends on timing anyway)."""
     lt = np.ascontiguousarray(log_table, dtype=np.float64)
-    key = lt.tobytes()
-    hit = _POW_FIX.get(key)
-    if hit is not None:
-        return hit
+    rows = min(len(lt), POW_FIX_ROWS) if rows is None else min(int(rows), len(lt), POW_FIX_ROWS)
+    c = _POW_FIX
+    have = len(c["off"]) - 1
+    if have < rows and cached_only:
+        rows = have
+    if have >= rows and np.array_equal(c["lt"][:rows], lt[:rows]):
+        off = c["off"][: rows + 1]
+        return off, c["ent"][: int(off[-1])]
     L = load()
-    off = np.zeros(len(lt) + 1, np.int32)
-    cap = max(64, len(lt) * 2)
+    off = np.zeros(rows + 1, np.int32)
+    cap = max(64, rows * 8)
     while True:
         ent = np.zeros(cap, np.int32)
         k = C.c_int32()
-        rc = L.bk_pow_half_fix(lt.ctypes.data, len(lt), off.ctypes.data, ent.ctypes.data, cap, C.byref(k))
+        rc = L.bk_pow_half_fix(lt.ctypes.data, rows, off.ctypes.data, ent.ctypes.data, cap, C.byref(k))
         if rc == EOVERFLOW:
             cap = int(k.value)
             continue
         if rc != OK:
             raise RuntimeError(f"bk_pow_half_fix failed ({rc})")
         break
-    res = (off, ent[: k.value].copy())
-    if len(_POW_FIX) > 8:
-        _POW_FIX.clear()
-    _POW_FIX[key] = res
-    return res
+    ent = ent[: k.value].copy()
+    if rows >= have:
+        c.update(lt=lt[:rows].copy(), off=off, ent=ent)
+    return off, ent
 
 
 def fset_new(n: int = 1) -> np.ndarray:

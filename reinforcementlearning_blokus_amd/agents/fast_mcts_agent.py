@@ -212,16 +212,20 @@ class FastMCTSAgent:
         mt[0] = self._rng_words()
         for k in range(1, len(todo)):
             mt[k] = _advance_words(mt[k - 1], 0 if math.isnan(bases[k - 1]) else 2 * iters)
-        out = self._launch([len(legal_lists[i]) for i in todo], [iters] * len(todo), bases, mt)
+        out = self._launch([len(legal_lists[i]) for i in todo], [iters] * len(todo), bases, mt,
+                           exact_ucb=iters >= self.iterations)
         self._set_rng_words(mt[-1])
         for k, i in enumerate(todo):
             results[i] = self._finish(out[k], boards[i], players[i], legal_lists[i], time_budget_ms, start)
         return results  # type: ignore[return-value]
 
-    def _launch(self, n_legal, counts, bases, mt, want_visits=False):
+    def _launch(self, n_legal, counts, bases, mt, want_visits=False, exact_ucb=True):
+        # exact_ucb=False: the time budget cut the iteration count (a wall-clock search,
+        # not reproducible by the reference either), so do not stall on building pow
+        # corrections for it (gpu.fastmcts)
         t0 = time.perf_counter()
         r = self._engine().fastmcts(n_legal, counts, bases, mt, _log_table(max(counts) + 1),
-                                    self.exploration_constant, want_visits=want_visits)
+                                    self.exploration_constant, want_visits=want_visits, exact_ucb=exact_ucb)
         work = max(counts)  # roots run side by side, one wave each
         if work >= 64:
             self._us_per_iter = 0.5 * self._us_per_iter + 0.5 * (time.perf_counter() - t0) * 1e6 / work

@@ -257,6 +257,9 @@ def _all_random(run_config: RunConfig) -> bool:
     return all(a.type.lower() == "random" for a in run_config.agents)
 
 
+STATUS_CAP = 8  # bk_result.status bit 3 (include/blokus_hip.h)
+
+
 def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
                   device: int = 0) -> List[Dict[str, Any]]:
     """All-random seatings: the games ``game_indices`` in one frontier-order playout launch.
@@ -279,17 +282,24 @@ def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id:
         seeds[i] = [agent_seed(run_config.seed, gi, st[str(p + 1)]) for p in range(4)]
     gpu = BlokusGPU(device)
     t0 = time.perf_counter()
-    states, _sets, res = gpu.rollout_frontier(empty_state(), N.fset_new(1), n, semantics=N.SEM_ADVANCE,
+    states, _sets, res = gpu.rollout_frontier(empty_state(), N.fset_new(1), n, semantics=N.SEM_ARENA,
                                               rng=N.RNG_NUMPY_MT, compat_seeds=seeds,
                                               max_plies=run_config.max_turns,
-                                              root_index=np.zeros(n, dtype=np.int32), with_results=True)
-    # truncated = cut by max_turns while the game was not over (arena_runner.py:702):
-    # the kernel stops at the cap without looking ahead, so ask has_legal_moves of the
-    # final positions of the games that reached it
-    at_cap = np.flatnonzero(res["turns"].astype(np.int64) >= run_config.max_turns)
+                                              root_index=np.zeros(n, dtype=np.int32), with_states=True)
+    # A game the kernel stopped at max_turns (status bit 3) may or may not be over: it
+    # stops without looking ahead.  has_legal_moves of its final position decides
+    # (arena_runner.py:653, :702): still alive -> truncated; over -> it ended with its
+    # last move, so the passes counted since then never happened in the reference.
+    at_cap = np.flatnonzero(res["status"] & STATUS_CAP)
     alive = np.zeros(n, dtype=bool)
     if len(at_cap):
         alive[at_cap] = gpu.has_moves(states[at_cap]) != 0
+    res = res.copy()
+    for i in at_cap[~alive[at_cap]]:
+        k = int(res["reserved"][i, 0])
+        res["passes"][i] -= k
+        res["turns"][i] -= k
+    res["status"] &= ~np.uint8(STATUS_CAP)
     dt = time.perf_counter() - t0
     out = []
     for i, gi in enumerate(idx):

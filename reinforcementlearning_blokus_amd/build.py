@@ -50,7 +50,7 @@ def build_native(force: bool = True, verbose: bool = True) -> str:
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wno-unused-command-line-argument", "-o", OUT + ".tmp", SRC]
+           "-pthread", "-Wno-unused-command-line-argument", "-o", OUT + ".tmp", SRC]
     if verbose:
         print("[build] " + " ".join(cmd), flush=True)
     digest = source_hash()

@@ -38,6 +38,7 @@
 #include <string.h>
 
 #include <mutex>
+#include <thread>
 #include <new>
 #include <vector>
 
@@ -935,6 +936,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 
 // counter[2] of a handle: sticky error bits of device-path launches, reported (and
 // cleared) by bk_synchronize
+#define BK_STATUS_CAP 8u     // bk_result.status: arena run stopped by the turn cap
 #define BK_STICKY_GUARD 1u  // a persistent kernel's iteration guard tripped: results incomplete
 #define BK_STICKY_ROOT 2u   // a root_index entry outside [0, n_roots)
 
@@ -1027,7 +1029,7 @@ __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
 
 template <bool FR>
 __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot) {
-    if (a.cfg.semantics == BK_SEM_ADVANCE) {
+    if (a.out_states != nullptr) {  // BK_SEM_ADVANCE, or an arena run that wants final states
         store_state(a, g, slab);
         if constexpr (FR) copy_fset(a.out_sets + g.pid, &a.fslab[slot].s);
         if (a.out == nullptr) { g.pid = -1; return; }
@@ -1057,10 +1059,22 @@ __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const
             wm |= (uint8_t)(((int)sc.get(p) == best) << p);
         }
         r.winner_mask = wm;
-        // passes detected lazily after the final move are not counted by the reference,
-        // whose game-over check runs right after each move (engine/game.py:182-214)
-        r.passes = (uint16_t)(g.passes - g.since_move);
-        r.turns = (uint16_t)(g.turns - g.since_move);
+        if (g.out == 0xFu || a.cfg.semantics != BK_SEM_ARENA) {
+            // passes detected lazily after the final move are not counted by the
+            // reference, whose game-over check runs right after each move
+            // (engine/game.py:182-214)
+            r.passes = (uint16_t)(g.passes - g.since_move);
+            r.turns = (uint16_t)(g.turns - g.since_move);
+        } else {
+            // stopped by the turn cap (arena max_turns) before every player was known
+            // to be stuck: the game may or may not be over.  Raw counts, the passes since
+            // the last move in reserved[0]; the host decides with has_moves on the final
+            // state (arena_runner.py:702), discounting them if the game is over.
+            r.passes = (uint16_t)g.passes;
+            r.turns = (uint16_t)g.turns;
+            r.reserved[0] = (uint32_t)g.since_move;
+            g.status |= BK_STATUS_CAP;
+        }
     } else {
         int best = -1000000;
 #pragma unroll
@@ -1211,7 +1225,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             }
             if (arena) {
 #pragma unroll 1
-                for (int s = 0; s < 4 && ((g.out >> g.cur) & 1u) && g.out != 0xFu; ++s) {
+                for (int s = 0; s < 4 && ((g.out >> g.cur) & 1u) && g.out != 0xFu && (advance || g.turns < cap); ++s) {
                     g.passes++; g.turns++; g.since_move++;
                     g.cur = (g.cur + 1) & 3;
                 }
@@ -1394,6 +1408,7 @@ __device__ __forceinline__ void wave_argmax(double& v, int& j) {
 struct PowFix {  // bk_pow_half_fix tables: CPython's (2 log N / v) ** 0.5 vs sqrt
     const int32_t* offsets;
     const int32_t* entries;
+    int32_t rows;     // the tables cover N < rows
 };
 
 // c * x ** 0.5 with x = L2 / v, L2 = 2 * math.log(N) (fast_mcts_agent.py:52): the IEEE
@@ -1401,6 +1416,7 @@ struct PowFix {  // bk_pow_half_fix tables: CPython's (2 log N / v) ** 0.5 vs sq
 // few corrections of this N are scanned by every lane (N is wave-uniform).
 __device__ __forceinline__ double fm_explore(double c, double L2, uint32_t v, uint32_t N, const PowFix& fx) {
     double s = sqrt(L2 / (double)v);
+    if ((int32_t)N >= fx.rows) return c * s;
     const int32_t e0 = fx.offsets[N], e1 = fx.offsets[N + 1];
     for (int32_t e = e0; e < e1; ++e) {
         const int32_t w = fx.entries[e];
@@ -2355,16 +2371,16 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         return set_err(h, BK_EINVAL, "bk_rollout: invalid arguments%s", "");
     if (cfg->semantics != BK_SEM_ARENA && cfg->semantics != BK_SEM_ROLLOUT && cfg->semantics != BK_SEM_ADVANCE)
         return set_err(h, BK_EINVAL, "bk_rollout: unknown semantics%s", "");
-    if ((cfg->semantics == BK_SEM_ADVANCE) != (out_states != nullptr))
-        return set_err(h, BK_EINVAL, "bk_rollout: out_states goes with BK_SEM_ADVANCE only%s", "");
+    if ((cfg->semantics == BK_SEM_ADVANCE && !out_states) || (cfg->semantics == BK_SEM_ROLLOUT && out_states))
+        return set_err(h, BK_EINVAL, "bk_rollout: out_states goes with BK_SEM_ADVANCE (or BK_SEM_ARENA)%s", "");
     if (!out && !out_states) return set_err(h, BK_EINVAL, "bk_rollout: no output%s", "");
     const bool fr = cfg->order == BK_ORDER_FRONTIER;
     if (cfg->order != BK_ORDER_NAIVE && !fr) return set_err(h, BK_EINVAL, "bk_rollout: unknown order%s", "");
     if (fr != (root_sets != nullptr))
         return set_err(h, BK_EINVAL, "bk_rollout: BK_ORDER_FRONTIER goes with root frontier sets "
                                      "(bk_rollout_frontier)%s", "");
-    if (fr && (cfg->semantics == BK_SEM_ADVANCE) != (out_sets != nullptr))
-        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_sets goes with BK_SEM_ADVANCE%s", "");
+    if (fr && (out_states != nullptr) != (out_sets != nullptr))
+        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_sets goes with out_states%s", "");
     if (cfg->rng != BK_RNG_PHILOX && cfg->rng != BK_RNG_NUMPY_MT)
         return set_err(h, BK_EINVAL, "bk_rollout: unknown rng%s", "");
     if (cfg->rng == BK_RNG_NUMPY_MT && !compat_seeds)
@@ -2478,8 +2494,8 @@ int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_
                         int mem) {
     if (!cfg || cfg->order != BK_ORDER_FRONTIER || !root_sets)
         return set_err(h, BK_EINVAL, "bk_rollout_frontier: needs BK_ORDER_FRONTIER and root_sets%s", "");
-    if ((cfg->semantics == BK_SEM_ADVANCE) != (out_states != nullptr))
-        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_states goes with BK_SEM_ADVANCE%s", "");
+    if ((cfg->semantics == BK_SEM_ADVANCE && !out_states) || (cfg->semantics == BK_SEM_ROLLOUT && out_states))
+        return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_states goes with BK_SEM_ADVANCE / BK_SEM_ARENA%s", "");
     if (cfg->semantics != BK_SEM_ADVANCE && !out)
         return set_err(h, BK_EINVAL, "bk_rollout_frontier: out is NULL%s", "");
     return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, out, out_states, mem,
@@ -2539,23 +2555,64 @@ int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {
     return n;
 }
 
+// Rows [N] of the pow corrections: v in [1, N] where libm pow(x, 0.5) != sqrt(x),
+// x = (2.0 * log_table[N]) / v.  false: pow and sqrt more than one ulp apart.
+static bool pow_fix_row(const double* log_table, int32_t N, double (*powp)(double, double), std::vector<int32_t>& out) {
+    const double L2 = 2.0 * log_table[N];
+    for (int32_t v = 1; v <= N; ++v) {
+        const double x = L2 / (double)v;
+        const double q = sqrt(x);
+        if (!(q > 0.0)) continue;
+        // sqrt is correctly rounded: |sqrt_exact - q| = d ulp with d <= 0.5.  glibc's pow is
+        // within 0.54 ulp of exact (the bound stated in its e_pow.c), so it can return the
+        // other neighbour only when d >= 0.46; pow is called for d >= 0.45 alone (~10 %).
+        // d from the residual q*q - x, q*q exact by Dekker's product (no fma needed).
+        const double c = 134217729.0 * q, qh = c - (c - q), ql = q - qh;
+        const double pq = q * q;
+        const double err = ((qh * qh - pq) + 2.0 * qh * ql) + ql * ql;
+        const double r = (pq - x) + err;  // pq - x is exact (Sterbenz)
+        uint64_t b;
+        memcpy(&b, &q, sizeof b);
+        b &= 0x7FF0000000000000ull;
+        double ulp;
+        memcpy(&ulp, &b, sizeof ulp);
+        ulp *= 2.220446049250313e-16;  // 2^-52: one ulp of q (q normal)
+        if (fabs(r) < 0.90 * q * ulp) continue;  // d = |r| / (2 q ulp) < 0.45
+        const double p = powp(x, 0.5);
+        if (p == q) continue;
+        if (p != nextafter(q, INFINITY) && p != nextafter(q, -INFINITY)) return false;
+        out.push_back((v << 1) | (p > q ? 1 : 0));
+    }
+    return true;
+}
+
 int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, int32_t* entries, int32_t cap,
                     int32_t* n_entries) {
     if (!log_table || log_len < 1 || !offsets || cap < 0 || (cap > 0 && !entries) || !n_entries) return BK_EINVAL;
     // through a volatile pointer: the call must reach libm's pow (what CPython's float
     // ** calls), never a compiler rewrite of pow(x, 0.5) into sqrt(x)
     double (*volatile powp)(double, double) = pow;
+    double (*const pw)(double, double) = powp;
+    std::vector<std::vector<int32_t>> rows((size_t)log_len);
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;  // the GPU box's CPU share is 16
+    if ((int64_t)log_len * log_len < 4000000) nt = 1;
+    std::vector<char> ok(nt, 1);
+    auto work = [&](unsigned t) {  // rows interleaved: row N costs N
+        for (int32_t N = (int32_t)t; N < log_len; N += (int32_t)nt)
+            if (!pow_fix_row(log_table, N, pw, rows[(size_t)N])) ok[t] = 0;
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (char o : ok)
+        if (!o) return BK_EINVAL;
     int32_t k = 0;
     for (int32_t N = 0; N < log_len; ++N) {
         offsets[N] = k;
-        const double L2 = 2.0 * log_table[N];
-        for (int32_t v = 1; v <= N; ++v) {
-            const double x = L2 / (double)v;
-            const double q = sqrt(x), p = powp(x, 0.5);
-            if (p == q) continue;
-            const double up = nextafter(q, INFINITY), dn = nextafter(q, -INFINITY);
-            if (p != up && p != dn) return BK_EINVAL;
-            if (k < cap) entries[k] = (v << 1) | (p > q ? 1 : 0);
+        for (int32_t w : rows[(size_t)N]) {
+            if (k < cap) entries[k] = w;
             ++k;
         }
     }
@@ -2566,16 +2623,17 @@ int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, 
 
 int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, const double* totals,
                              uint32_t root_visits, const double* log_table, int32_t log_len,
-                             const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_len,
+                             const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_rows,
                              double exploration, int32_t* out_best) {
     if (!h || n < 1 || !visits || !totals || !log_table || (int64_t)root_visits >= log_len || !pow_fix_offsets ||
-        pow_fix_len < 0 || (pow_fix_len > 0 && !pow_fix_entries) || !out_best ||
-        pow_fix_offsets[log_len] != pow_fix_len)
+        pow_fix_rows < 0 || pow_fix_rows > log_len || !out_best ||
+        (pow_fix_offsets[pow_fix_rows] > 0 && !pow_fix_entries))
         return set_err(h, BK_EINVAL, "bk_debug_fastmcts_select: invalid arguments%s", "");
+    const int32_t pow_fix_len = pow_fix_offsets[pow_fix_rows];
     for (int32_t j = 0; j < n; ++j)
         if (visits[j] == 0) return set_err(h, BK_EINVAL, "bk_debug_fastmcts_select: visits must be > 0%s", "");
     HIPCHK(h, hipSetDevice(h->device));
-    const size_t bv = sizeof(uint32_t) * n, bt = sizeof(double) * n, bo = sizeof(int32_t) * (size_t)(log_len + 1),
+    const size_t bv = sizeof(uint32_t) * n, bt = sizeof(double) * n, bo = sizeof(int32_t) * (size_t)(pow_fix_rows + 1),
                  be = sizeof(int32_t) * (size_t)(pow_fix_len + 1);
     int rc = grow(h, &h->d_aux, &h->d_aux_cap, bt + bv + bo + be + 64);
     if (rc) return rc;
@@ -2590,7 +2648,7 @@ int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, con
     HIPCHK(h, hipMemcpyAsync(d_o, pow_fix_offsets, bo, hipMemcpyHostToDevice, h->cur));
     if (pow_fix_len) HIPCHK(h, hipMemcpyAsync(d_e, pow_fix_entries, be - sizeof(int32_t), hipMemcpyHostToDevice, h->cur));
     hipLaunchKernelGGL(k_fastmcts_select, dim3(1), dim3(WAVE), 0, h->cur, d_v, d_t, n, root_visits,
-                       2.0 * log_table[root_visits], exploration, PowFix{d_o, d_e}, d_out);
+                       2.0 * log_table[root_visits], exploration, PowFix{d_o, d_e, pow_fix_rows}, d_out);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipMemcpyAsync(out_best, d_out, sizeof(int32_t), hipMemcpyDeviceToHost, h->cur));
     HIPCHK(h, hipStreamSynchronize(h->cur));
@@ -2599,20 +2657,21 @@ int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, con
 
 int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const int32_t* iterations,
                 const double* base, uint32_t* mt_state, const double* log_table, int32_t log_len,
-                const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_len,
+                const int32_t* pow_fix_offsets, const int32_t* pow_fix_entries, int32_t pow_fix_rows,
                 double exploration, bk_fastmcts_out* out, int32_t* visits_out, int mem) {
     if (!h || n_games < 0 || !legal_offset || !iterations || !base || !mt_state || !log_table || log_len <= 0 ||
-        !pow_fix_offsets || pow_fix_len < 0 || (pow_fix_len > 0 && !pow_fix_entries) ||
+        !pow_fix_offsets || pow_fix_rows < 0 || pow_fix_rows > log_len ||
         !out || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
         return set_err(h, BK_EINVAL, "bk_fastmcts: invalid arguments%s", "");
-    if (mem == BK_MEM_HOST && pow_fix_offsets[log_len] != pow_fix_len)
-        return set_err(h, BK_EINVAL, "bk_fastmcts: pow_fix tables do not match log_len%s", "");
+    const int32_t pow_fix_len = mem == BK_MEM_HOST ? pow_fix_offsets[pow_fix_rows] : 0;
+    if (pow_fix_len > 0 && !pow_fix_entries)
+        return set_err(h, BK_EINVAL, "bk_fastmcts: pow_fix_entries missing%s", "");
     if (n_games == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
     const size_t b_off = sizeof(int32_t) * (size_t)(n_games + 1), b_it = sizeof(int32_t) * (size_t)n_games,
                  b_base = sizeof(double) * (size_t)n_games, b_mt = sizeof(uint32_t) * 625 * (size_t)n_games,
                  b_log = sizeof(double) * (size_t)log_len, b_out = sizeof(bk_fastmcts_out) * (size_t)n_games,
-                 b_fo = sizeof(int32_t) * (size_t)(log_len + 1), b_fe = sizeof(int32_t) * (size_t)(pow_fix_len + 1);
+                 b_fo = sizeof(int32_t) * (size_t)(pow_fix_rows + 1), b_fe = sizeof(int32_t) * (size_t)(pow_fix_len + 1);
     const int32_t* d_off = legal_offset;
     const int32_t* d_it = iterations;
     const double* d_base = base;
@@ -2656,7 +2715,8 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
         }
     }
     HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
-    FastMctsArgs a{n_games, d_off, d_it, d_base, d_mt, d_log, log_len, PowFix{d_fo, d_fe}, exploration, d_out, d_vis,
+    FastMctsArgs a{n_games, d_off, d_it, d_base, d_mt, d_log, log_len, PowFix{d_fo, d_fe, pow_fix_rows}, exploration,
+                   d_out, d_vis,
                    h->d_counter + 1};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     hipLaunchKernelGGL(k_fastmcts, dim3(n_games), dim3(WAVE), 0, h->cur, a);

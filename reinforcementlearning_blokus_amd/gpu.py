@@ -151,10 +151,12 @@ class BlokusGPU:
     def rollout_frontier(self, roots, root_sets, n_playouts: int, *, semantics: int = N.SEM_ARENA,
                          rng: int = N.RNG_NUMPY_MT, seed: int = 0, max_plies: int | None = None,
                          compat_seeds=None, root_index=None, seats_share_stream: bool = False, out=None,
-                         with_results: bool = False):
+                         with_results: bool = False, with_states: bool = False):
         """Playouts in the reference's FRONTIER list order (bk_rollout_frontier): with the
         numpy-MT compat stream these are the reference's default-config games.
-        root_sets: FSET_DTYPE records (one per root).  Host numpy in/out."""
+        root_sets: FSET_DTYPE records (one per root).  Host numpy in/out.  SEM_ADVANCE
+        returns (states, tables[, results]); SEM_ARENA with with_states returns
+        (states, tables, results): the final positions as well."""
         if max_plies is None:
             max_plies = 2500 if semantics == N.SEM_ARENA else 50
         cfg = N.BkRolloutCfg(semantics, N.ORDER_FRONTIER, rng, max_plies, seed & (2**64 - 1),
@@ -181,7 +183,8 @@ class BlokusGPU:
         if seeds is not None:
             assert seeds.shape[0] >= n_playouts
         self.handle.set_stream(None)
-        if semantics == N.SEM_ADVANCE:  # (states, tables[, results])
+        if semantics == N.SEM_ADVANCE or (semantics == N.SEM_ARENA and with_states):  # (states, tables[, results])
+            with_results = with_results or semantics == N.SEM_ARENA
             out_st = np.zeros(n_playouts, dtype=STATE_DTYPE)
             out_fs = np.zeros(n_playouts, dtype=N.FSET_DTYPE)
             res = np.zeros(n_playouts, dtype=RESULT_DTYPE) if with_results else None
@@ -223,12 +226,14 @@ class BlokusGPU:
 
     # ------------------------------------------------------------------ FastMCTS
     def fastmcts(self, n_legal, iterations, base, mt_state, log_table, exploration: float,
-                 want_visits: bool = False):
+                 want_visits: bool = False, exact_ucb: bool = True):
         """Run FastMCTSAgent's bandit loop for a batch of roots (bk_fastmcts).
 
         n_legal[i]: root legal-move count; iterations[i]; base[i]: deterministic part of
         the rollout reward (NaN = empty cached list); mt_state: uint32[n,625] CPython
-        random states, advanced in place; log_table[k] = math.log(k).
+        random states, advanced in place; log_table[k] = math.log(k).  exact_ucb: build
+        the pow-correction rows the iteration counts need (bk_pow_half_fix), else use
+        whatever rows are cached (wall-clock-bounded searches).
         Returns a FASTMCTS_OUT_DTYPE record array (and, with want_visits, the flat int32
         visit counts per legal index)."""
         n = len(n_legal)
@@ -238,12 +243,12 @@ class BlokusGPU:
         b = np.ascontiguousarray(base, dtype=np.float64)
         assert mt_state.dtype == np.uint32 and mt_state.shape == (n, 625) and mt_state.flags.c_contiguous
         lt = np.ascontiguousarray(log_table, dtype=np.float64)
-        fo, fe = N.pow_half_fix(lt)
+        fo, fe = N.pow_half_fix(lt, rows=int(it.max(initial=0)), cached_only=not exact_ucb)
         out = np.zeros(n, dtype=N.FASTMCTS_OUT_DTYPE)
         vis = np.zeros(max(int(off[-1]), 1), dtype=np.int32) if want_visits else None
         self.handle.set_stream(None)
         self.handle.fastmcts(n, off.ctypes.data, it.ctypes.data, b.ctypes.data, mt_state.ctypes.data,
-                             lt.ctypes.data, len(lt), fo.ctypes.data, fe.ctypes.data if len(fe) else 0, len(fe),
+                             lt.ctypes.data, len(lt), fo.ctypes.data, fe.ctypes.data if len(fe) else 0, len(fo) - 1,
                              exploration, out.ctypes.data, vis.ctypes.data if vis is not None else 0, N.MEM_HOST)
         return (out, vis[: int(off[-1])]) if want_visits else out
 
@@ -257,8 +262,8 @@ class BlokusGPU:
         fo, fe = N.pow_half_fix(lt)
         self.handle.set_stream(None)
         return self.handle.debug_fastmcts_select(len(v), v.ctypes.data, t.ctypes.data, int(root_visits), lt.ctypes.data,
-                                                 len(lt), fo.ctypes.data, fe.ctypes.data if len(fe) else 0, len(fe),
-                                                 exploration)
+                                                 len(lt), fo.ctypes.data, fe.ctypes.data if len(fe) else 0,
+                                                 len(fo) - 1, exploration)
 
     # ------------------------------------------------------------------ MCTSAgent
     def mcts(self, roots, root_sets, players, root_hash, *, iterations: int, zobrist, mt_state,
