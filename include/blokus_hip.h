@@ -89,9 +89,12 @@ typedef struct bk_rollout_cfg {
     int32_t max_plies;  /* BK_SEM_ROLLOUT cap (MCTSAgent max_rollout_moves, default 50);
                            BK_SEM_ARENA: max turns (arena max_turns, default 2500)         */
     uint64_t seed;      /* BK_RNG_PHILOX key                                              */
-    int32_t seats_share_stream; /* compat: 1 = one RandomAgent for every seat (MCTSAgent
-                                   rollout_agent), 0 = one RandomAgent per seat (arena)   */
-    int32_t reserved;
+    int32_t seats_share_stream; /* compat: 1 = one agent stream for every seat (MCTSAgent
+                                   rollout_agent), 0 = one agent per seat (arena)         */
+    int32_t heuristic_seats;    /* bit p: seat p plays HeuristicAgent (agents/heuristic_agent.py
+                                   :39-244) instead of RandomAgent; BK_ORDER_FRONTIER only.
+                                   Its choice is certified exact (result status bit 4 set
+                                   otherwise)                               */
 } bk_rollout_cfg;
 
 /* One playout result: 32 bytes */
@@ -101,6 +104,8 @@ typedef struct bk_result {
     uint8_t winner_mask;        /* bit p: p in GameResult.winner_ids (engine/game.py:216)    */
     uint8_t status;             /* 0 ok; bit0: rng stream overflow (compat mode); bit1:
                                    frontier table overflow; bit2: bad root_index (device path);
+                                   bit4: a HeuristicAgent draw fell within 2^-36 of a
+                                   cumulative-probability boundary (choice not certified); 
                                    bit3: ARENA run stopped by the max_plies turn cap before
                                    every player was known to be stuck (passes / turns are
                                    then raw and reserved[0] = passes since the last move)  */
@@ -284,7 +289,7 @@ int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, con
 
 /*
  * bk_mcts -- MCTSAgent.select_action searches (mcts/mcts_agent.py:304-582, MCTSNode
- * :19-191) with RandomAgent rollouts (agents/random_agent.py:49) and the Zobrist
+ * :19-191) with RandomAgent or HeuristicAgent rollouts (cfg.rollout_policy) and the Zobrist
  * transposition table (mcts/zobrist.py:12-220), one search per game, all on the GPU.
  * Bit-exact with the reference for the same inputs: frontier-order legal lists
  * (root_sets = the Board's frontier tables, see bk_fset_*), untried.pop() expansion,
@@ -336,7 +341,13 @@ typedef struct bk_mcts_cfg {
                                   iter_stop iterations in total (chunked searches)      */
     int32_t resume;            /* 1: continue the searches left in nodes / out / tt /
                                   mt_state by an earlier launch (iter_stop chunks)      */
+    int32_t rollout_policy;    /* BK_MCTS_ROLLOUT_*: the rollout_agent                  */
+    int32_t reserved;
 } bk_mcts_cfg;
+#define BK_MCTS_ROLLOUT_RANDOM 0    /* RandomAgent (agents/random_agent.py:49)            */
+#define BK_MCTS_ROLLOUT_HEURISTIC 1 /* HeuristicAgent (agents/heuristic_agent.py:39-244),
+                                       MCTSAgent's default (mcts/mcts_agent.py:275-281);
+                                       choices certified exact, else BK_MCTS_EUNCERT    */
 
 #define BK_MCTS_EPOOL 1u   /* node pool full                    */
 #define BK_MCTS_EFSET 2u   /* frontier table overflow           */
@@ -344,6 +355,8 @@ typedef struct bk_mcts_cfg {
 #define BK_MCTS_EPATH 8u   /* tree deeper than BK_MCTS_MAX_DEPTH */
 #define BK_MCTS_ELOG 16u   /* log_table too short               */
 #define BK_MCTS_EINTERNAL 32u /* consistency check failed        */
+#define BK_MCTS_EUNCERT 64u   /* a HeuristicAgent draw fell within 2^-36 of a probability
+                                 boundary: that choice is not certified exact           */
 #define BK_MCTS_MAX_DEPTH 63
 typedef struct bk_mcts_out {
     int32_t best_move;       /* g*400+cell of the most visited root child (first on ties), -1 */

@@ -309,3 +309,113 @@ def mcts(b, player, iterations, exploration, max_rollout, ztab, rng, tt=None, ch
     n = min(nch.value, child_cap)
     return {"move": best.value, "hits": hits.value, "rewards": rewards, "hit_flags": flags,
             "children": list(zip(cm[:n].tolist(), cv[:n].tolist(), ct[:n].tolist()))}
+
+
+# ---------------------------------------------------------------------------------
+# HeuristicAgent (agents/heuristic_agent.py:39-244), restated move by move for test
+# use: _evaluate_move (:68-103) with _evaluate_corner_creation (:107-138),
+# _evaluate_edge_avoidance (:140-176), _evaluate_center_preference (:178-199), then
+# _softmax (:223-244) and rng.choice (:61-65) with numpy itself.  Legal lists come from
+# the C oracle in the reference's frontier order.  Pinned by tests/golden/heuristic.json
+# (tests/test_oracle_golden.py).
+# ---------------------------------------------------------------------------------
+_ORIENTS = None
+
+
+def _orients():
+    global _ORIENTS
+    if _ORIENTS is None:
+        _ORIENTS = orient_table()
+    return _ORIENTS
+
+
+def heuristic_score(b, player, move):
+    """_evaluate_move of move = g * 400 + anchor for player (0..3) on oracle board b."""
+    grid = b.grid
+    g, a = divmod(int(move), 400)
+    ar, ac = divmod(a, 20)
+    cells = [(ar + dr, ac + dc) for dr, dc in _orients()[g][2]]
+    pv = player + 1
+    score = 0.0
+    score += 1.0 * len(cells)
+    corners = 0
+    for r, c in cells:
+        for dr, dc in ((-1, -1), (-1, 1), (1, -1), (1, 1)):
+            nr, nc = r + dr, c + dc
+            if not (0 <= nr < 20 and 0 <= nc < 20) or grid[nr * 20 + nc] != 0:
+                continue
+            safe = True
+            for er, ec in ((-1, 0), (1, 0), (0, -1), (0, 1)):
+                rr, cc = nr + er, nc + ec
+                if 0 <= rr < 20 and 0 <= cc < 20 and grid[rr * 20 + cc] == pv:
+                    safe = False
+                    break
+            if safe:
+                corners += 1
+    score += 2.0 * corners
+    edge = sum(1 for r, c in cells if min(r, c, 19 - r, 19 - c) <= 2)
+    edge_score = edge if b.move_count / 100.0 < 0.3 else edge * 0.5
+    score += -1.5 * edge_score
+    distance = np.sqrt((ar - 9.5) ** 2 + (ac - 9.5) ** 2)
+    center = 1.0 - distance / np.sqrt(2 * (9.5 ** 2))
+    score += 0.5 * center
+    return score
+
+
+def heuristic_choice(b, player, rng):
+    """HeuristicAgent.select_action on b for player with numpy RandomState rng: the chosen
+    move int, or None with no legal move (no draw then)."""
+    moves = legal_moves(b, player, ORDER_FRONTIER)
+    if not moves:
+        return None
+    x = np.array([heuristic_score(b, player, m) for m in moves]) / 1.0
+    e = np.exp(x - np.max(x))
+    p = e / np.sum(e)
+    return moves[rng.choice(len(moves), p=p)]
+
+
+def mixed_playout_arena(b, seeds, heuristic_seats, max_turns=2500):
+    """Arena game loop (arena_runner.py:652-697, pass when stuck, terminal when nobody can
+    move) from b with one agent per seat: HeuristicAgent(seeds[p]) where bit p of
+    heuristic_seats is set, else RandomAgent(seeds[p]) (randint over the frontier-order
+    list).  Returns (scores, winner_mask, moves, passes, turns, trace)."""
+    rngs = [np.random.RandomState(int(s)) for s in seeds]
+    passes = turns = 0
+    trace = []
+    while turns < max_turns:
+        if all(not legal_moves(b, p, ORDER_FRONTIER) for p in range(4)):
+            break
+        p = b.cur
+        turns += 1
+        if (heuristic_seats >> p) & 1:
+            mv = heuristic_choice(b, p, rngs[p])
+        else:
+            lm = legal_moves(b, p, ORDER_FRONTIER)
+            mv = lm[rngs[p].randint(0, len(lm))] if lm else None
+        if mv is None:
+            passes += 1
+            trace.append(-1)
+            b.cur = (b.cur + 1) & 3
+            continue
+        trace.append(mv)
+        place_move(b, p, mv)
+        b.cur = (p + 1) & 3
+    scores, wm = game_scores(b)
+    return scores, wm, sum(1 for t in trace if t >= 0), passes, turns, trace
+
+
+def heuristic_rollout_a(b, player, rng, max_moves=50):
+    """MCTSAgent._rollout (mcts/mcts_agent.py:470-554) with a HeuristicAgent rollout agent
+    drawing from rng, on a copy of b: (reward, plies)."""
+    sim = copy_board(b)
+    start = board_score(sim, player)
+    cur = player
+    plies = 0
+    while plies < max_moves:
+        mv = heuristic_choice(sim, cur, rng)
+        if mv is None:
+            break
+        place_move(sim, cur, mv)
+        cur = (cur + 1) & 3
+        plies += 1
+    return board_score(sim, player) - start, plies

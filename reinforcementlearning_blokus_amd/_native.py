@@ -59,7 +59,7 @@ class BkResult(C.Structure):
 
 class BkRolloutCfg(C.Structure):
     _fields_ = [("semantics", C.c_int32), ("order", C.c_int32), ("rng", C.c_int32), ("max_plies", C.c_int32),
-                ("seed", C.c_uint64), ("seats_share_stream", C.c_int32), ("reserved", C.c_int32)]
+                ("seed", C.c_uint64), ("seats_share_stream", C.c_int32), ("heuristic_seats", C.c_int32)]
 
 
 class BkFastMctsOut(C.Structure):
@@ -79,10 +79,11 @@ assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRoll
 class BkMctsCfg(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("max_rollout_moves", C.c_int32), ("exploration", C.c_double),
                 ("use_tt", C.c_int32), ("node_cap", C.c_int32), ("tt_cap", C.c_int32),
-                ("time_limit_us", C.c_int32), ("iter_stop", C.c_int32), ("resume", C.c_int32)]
+                ("time_limit_us", C.c_int32), ("iter_stop", C.c_int32), ("resume", C.c_int32),
+                ("rollout_policy", C.c_int32), ("reserved", C.c_int32)]
 
 
-assert C.sizeof(BkMctsCfg) == 40
+assert C.sizeof(BkMctsCfg) == 48
 MCTS_NODE_DTYPE = np.dtype([("total", "<f8"), ("visits", "<u4"), ("child0", "<i4"), ("move", "<u2"),
                             ("n_exp", "<u2"), ("n_legal", "<u2"), ("flags", "<u2")])
 assert MCTS_NODE_DTYPE.itemsize == 24
@@ -92,7 +93,8 @@ MCTS_OUT_DTYPE = np.dtype([("best_move", "<i4"), ("iterations_run", "<i4"), ("tt
 assert MCTS_OUT_DTYPE.itemsize == 32
 MCTS_ZOBRIST_WORDS = 2088
 MCTS_MAX_DEPTH = 63
-MCTS_EPOOL, MCTS_EFSET, MCTS_ETT, MCTS_EPATH, MCTS_ELOG, MCTS_EINTERNAL = 1, 2, 4, 8, 16, 32
+MCTS_EPOOL, MCTS_EFSET, MCTS_ETT, MCTS_EPATH, MCTS_ELOG, MCTS_EINTERNAL, MCTS_EUNCERT = 1, 2, 4, 8, 16, 32, 64
+MCTS_ROLLOUT_RANDOM, MCTS_ROLLOUT_HEURISTIC = 0, 1
 
 # numpy views of the same records
 

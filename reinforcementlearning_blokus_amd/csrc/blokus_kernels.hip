@@ -934,6 +934,286 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     return fs_place_pred(fs_ref(gfs, p, htab), fl->tmp, cells, n, addable);
 }
 
+// ------------------------------------------------------------------------------------
+// HeuristicAgent policy (agents/heuristic_agent.py:39-244) on the device.
+//
+// Score of a legal move (_evaluate_move :68-103): size + 2 * corners - 1.5 * edge' +
+// 0.5 * centre, with corners = sum over the piece's cells of the in-bounds diagonal
+// neighbours that are empty and not orthogonally adjacent to the mover (board BEFORE the
+// move; a neighbour reached from two cells counts twice, :107-138), edge' = cells with
+// min(r, c, 19 - r, 19 - c) <= 2, halved once move_count / 100.0 >= 0.3 (:140-176), and
+// centre = 1 - |anchor - (9.5, 9.5)| / sqrt(2 * 9.5^2) (:178-199).  4 * score =
+// K4 + 2 * centre with the integer K4 = 4 n + 8 corners - w edge (w = 6 early, 3 late).
+// The move is rng.choice(n, p=softmax(scores)) (:61-65, :223-244): one random_sample()
+// u (genrand_res53 of the agent's numpy MT19937) and the first list index whose
+// cumulative probability exceeds u.
+//
+// Exactness.  numpy's exp is not reproducible across hosts (AVX-512 SIMD vs libm), so
+// the probabilities are not recomputed bit for bit; the CHOICE is.  Here e = exp(score)
+// = TK[K4] * TC[anchor] (exp(K4 / 4) and exp(centre / 2), tables per block) and the
+// cumulative sums run in double: every computed cumulative probability is within
+// ~1e-13 of the exact value, and so is the reference's.  The kernel takes the first move
+// whose cumulative e exceeds u * total and verifies that u * total lies more than
+// HEUR_MARGIN * total inside that move's interval; then the reference (any host) picks
+// the same index.  A draw closer than that to an interval end sets status bit 4 (never
+// observed; tests require it clear).
+// ------------------------------------------------------------------------------------
+#define HK_MIN (-10)  // K4 range: 4 n + 8 corners - 6 edge in [-10, 180]
+#define HK_N 191
+#define HEUR_MARGIN 1.4551915228366852e-11  // 2^-36 of the total
+#define BK_STATUS_UNCERT 16u
+
+struct HeurShared {           // per block (LDS), built at kernel start
+    double tk[HK_N];          // exp(K4 / 4)
+    double tc[BK_CELLS];      // exp(centre(anchor) / 2)
+    int32_t first[BK_PIECES + 1];  // first global orientation of each piece (+ 91)
+};
+
+__device__ void heur_shared_init(HeurShared* hs, int tid, int nthreads) {
+    for (int i = tid; i < HK_N; i += nthreads) hs->tk[i] = exp(0.25 * (double)(i + HK_MIN));
+    for (int a = tid; a < BK_CELLS; a += nthreads) {
+        const double dr = (double)(a / 20) - 9.5, dc = (double)(a % 20) - 9.5;
+        const double centre = 1.0 - sqrt(dr * dr + dc * dc) / sqrt(2.0 * (9.5 * 9.5));
+        hs->tc[a] = exp(0.5 * centre);
+    }
+    for (int g = tid; g < BK_NUM_ORIENTS; g += nthreads) {
+        const uint32_t pc = kInfo[g] & 0xFFu;
+        if (g == 0 || (kInfo[g - 1] & 0xFFu) != pc) hs->first[pc - 1] = g;
+    }
+    if (tid == 0) hs->first[BK_PIECES] = BK_NUM_ORIENTS;
+}
+
+// e = exp(score) of orientation (n cells at (cd, cc)) with its box corner at (r, x);
+// rows[R * WAVE].x = the mover's blocked row R before the move (empty and not
+// orthogonally adjacent to the mover = ~B)
+__device__ __forceinline__ double heur_e(int n, const uint32_t (&cd)[5], const uint32_t (&cc)[5], int r, int x,
+                                         const uint2* rows, const HeurShared* hs, int edge_w) {
+    int corners = 0, edge = 0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        if (k < n) {
+            const int R = r + (int)cd[k], c = x + (int)cc[k];
+            const uint32_t up = R > 0 ? (~rows[(R - 1) * WAVE].x & ROWMASK) : 0u;
+            const uint32_t dn = R < 19 ? (~rows[(R + 1) * WAVE].x & ROWMASK) : 0u;
+            // bits c - 1 and c + 1 of the rows above (bits 0, 2) and below (bits 1, 3)
+            corners += __builtin_popcount((((up << 1) >> c) & 5u) | ((((dn << 1) >> c) & 5u) << 1));
+            edge += (R <= 2 || R >= 17 || c <= 2 || c >= 17) ? 1 : 0;
+        }
+    }
+    return hs->tk[4 * n + 8 * corners - edge_w * edge - HK_MIN] * hs->tc[r * 20 + x];
+}
+
+__device__ __forceinline__ void orient_cells(int g, int& n, uint32_t (&cd)[5], uint32_t (&cc)[5]) {
+    n = (int)((kInfo[g] >> 8) & 0xFFu);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[g][k];
+        cd[k] = cell >> 8;
+        cc[k] = cell & 0xFFu;
+    }
+}
+
+// sum of e over orientation g's legal anchors (ok rows in rows[r * WAVE].y, r < nr);
+// g is wave-uniform (a stencil-class entry)
+__device__ __forceinline__ double heur_orient_sum(int g, int nr, const uint2* rows, const HeurShared* hs, int edge_w,
+                                                  uint32_t& count) {
+    int n;
+    uint32_t cd[5], cc[5];
+    orient_cells(g, n, cd, cc);
+    double sum = 0.0;
+#pragma unroll 1
+    for (int r = 0; r < nr; ++r) {
+        uint32_t ok = rows[r * WAVE].y;
+        count += __builtin_popcount(ok);
+        while (ok) {
+            const int x = __builtin_ctz(ok);
+            ok &= ok - 1u;
+            sum += heur_e(n, cd, cc, r, x, rows, hs, edge_w);
+        }
+    }
+    return sum;
+}
+
+// pass A over one stencil class: e sums per piece (psum[(piece - 1) * WAVE], doubles in
+// LDS) and the legal-move count, for lanes whose mover plays the heuristic (avail = 0
+// otherwise)
+template <int H, int... T>
+__device__ __forceinline__ void heur_class(int i0, int i1, const Planes& P, uint32_t avail, uint2* rows,
+                                           double* psum, const HeurShared* hs, int edge_w, uint32_t& count) {
+#pragma unroll 1
+    for (int i = i0; i < i1; ++i) {
+        const uint32_t w0 = kClass[i][0], w1 = kClass[i][1];
+        const uint32_t piece = w0 & 0xFFu;
+        const bool av = (avail >> (piece - 1u)) & 1u;
+        if (__builtin_amdgcn_ballot_w64(av) == 0ull) continue;
+        StencilClass<H, T...>::scan(P, w1, [&](int r, uint32_t ok) { rows[r * WAVE].y = av ? ok : 0u; });
+        uint32_t c = 0;
+        const double sg = heur_orient_sum((int)(w0 >> 8), 21 - H, rows, hs, edge_w, c);
+        if (av) {
+            psum[(piece - 1u) * WAVE] += sg;
+            count += c;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t heur_pass_a(const Planes& P, uint32_t avail, uint2* rows, double* psum,
+                                                const HeurShared* hs, int edge_w) {
+#pragma unroll
+    for (int p = 0; p < BK_PIECES; ++p) psum[p * WAVE] = 0.0;
+    uint32_t count = 0;
+    int tb0 = 0;  // opaque 0 (see movegen_counts)
+    asm volatile("" : "+s"(tb0));
+    tb0 = __builtin_amdgcn_readfirstlane(tb0);
+#define BK_HEUR_CLASS(i0, i1, H, ...) heur_class<H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, rows, psum, hs, edge_w, count);
+    BK_CLASS_LIST(BK_HEUR_CLASS)
+#undef BK_HEUR_CLASS
+    return count;
+}
+
+// legal anchor rows of orientation gs (per lane) from the {B, C} rows in LDS
+__device__ __forceinline__ void lane_ok_rows(int gs, const uint2* rows, uint32_t (&ok)[20]) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    const int rlim = 20 - (int)((info >> 16) & 0xFFu);
+    const uint2* base[5];
+    uint32_t sh[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        base[k] = rows + (cell >> 8) * WAVE;
+        sh[k] = cell & 0xFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        const int rr = r < rlim ? r : rlim;
+        uint2 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = base[k][rr * WAVE];
+        uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
+        uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
+        ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
+        ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
+        ok[r] = r <= rlim ? (ac & ~ab) : 0u;
+    }
+}
+
+__device__ __forceinline__ double lane_orient_sum(int gs, const uint32_t (&ok)[20], const uint2* rows,
+                                                  const HeurShared* hs, int edge_w) {
+    int n;
+    uint32_t cd[5], cc[5];
+    orient_cells(gs, n, cd, cc);
+    double sum = 0.0;
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        uint32_t w = ok[r];
+        while (w) {
+            const int x = __builtin_ctz(w);
+            w &= w - 1u;
+            sum += heur_e(n, cd, cc, r, x, rows, hs, edge_w);
+        }
+    }
+    return sum;
+}
+
+// The heuristic's choice after pass A (psum per piece): target = u * total; the piece,
+// then the orientation (list order: piece asc, orientation asc) whose cumulative e
+// crosses it.  rows: {B, C} in LDS.  Returns the orientation (its legal rows in ok) and
+// the cumulative e before it in R; uncertain when the crossing is not where the sums say
+// (rounding: the choice is then not certified).
+__device__ __forceinline__ int heur_pick_orient(const double* psum, const uint2* rows, const HeurShared* hs,
+                                                int edge_w, double target, double& R, uint32_t (&ok)[20],
+                                                bool& uncertain) {
+    int pstar = -1;
+    R = 0.0;
+#pragma unroll 1
+    for (int p = 0; p < BK_PIECES; ++p) {
+        const double sp = psum[p * WAVE];
+        if (pstar < 0 && sp > 0.0) {
+            if (R + sp > target) pstar = p;
+            else R += sp;
+        }
+    }
+    if (pstar < 0) {  // u * total rounded up to the total: take the last piece with moves
+        uncertain = true;
+        R = 0.0;
+        for (int p = 0; p < BK_PIECES; ++p)
+            if (psum[p * WAVE] > 0.0) pstar = p;
+#pragma unroll 1
+        for (int p = 0; p < pstar; ++p) R += psum[p * WAVE];
+    }
+    int gstar = -1, glast = -1;
+    double Rstar = R;
+    bool found = false;
+    const int g1 = hs->first[pstar + 1];
+#pragma unroll 1
+    for (int g = hs->first[pstar]; g < g1 && !found; ++g) {
+        lane_ok_rows(g, rows, ok);
+        glast = g;
+        const double sg = lane_orient_sum(g, ok, rows, hs, edge_w);
+        if (sg > 0.0) {
+            gstar = g;
+            Rstar = R;
+            found = R + sg > target;
+            R += sg;
+        }
+    }
+    if (!found) uncertain = true;  // rounding: the last orientation with moves, uncertified
+    if (gstar >= 0 && glast != gstar) lane_ok_rows(gstar, rows, ok);
+    R = Rstar;
+    return gstar;
+}
+
+// Walk orientation gs's anchors in the reference's frontier list order (pass 2 of
+// locate_move_frontier) accumulating e until the cumulative sum passes target.  ok =
+// gs's legal rows; rows[.].y is overwritten, rows[.].x (B) kept.
+__device__ __forceinline__ void heur_walk_frontier(int gs, const uint32_t (&ok)[20], uint2* rows, const int16_t* key,
+                                                   int mask, const HeurShared* hs, int edge_w, double target,
+                                                   double R, double total, int& out_r, int& out_c,
+                                                   bool& uncertain) {
+#pragma unroll
+    for (int r = 0; r < 20; ++r) rows[r * WAVE].y = ok[r];
+    int n;
+    uint32_t cd[5], cc[5];
+    orient_cells(gs, n, cd, cc);
+    int found_r = -1, found_c = 0, last_r = -1, last_c = 0;
+    double last_lo = R, last_e = 0.0;
+    const uint4* k4 = reinterpret_cast<const uint4*>(key);
+#pragma unroll 1
+    for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 16) {
+        const uint4 qa = k4[b0 >> 3], qb = k4[(b0 >> 3) + 1];
+        const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            if (found_r >= 0 || f < 0 || b0 + j > mask) continue;
+            const int fr = f / 20, fc = f - 20 * fr;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                if (k >= n || found_r >= 0) continue;
+                const int ar = fr - (int)cd[k], acl = fc - (int)cc[k];
+                if (ar < 0 || ar > 19 || acl < 0 || acl > 19) continue;
+                uint2* rp = rows + ar * WAVE;
+                const uint32_t okw = rp->y;
+                if (!((okw >> acl) & 1u)) continue;
+                rp->y = okw & ~(1u << acl);
+                const double e = heur_e(n, cd, cc, ar, acl, rows, hs, edge_w);
+                last_r = ar; last_c = acl; last_lo = R; last_e = e;
+                if (R + e > target) { found_r = ar; found_c = acl; continue; }
+                R += e;
+            }
+        }
+    }
+    if (found_r < 0) {  // rounding put the target past the last anchor: take it, uncertified
+        uncertain = true;
+        found_r = last_r; found_c = last_c;
+    }
+    // certification: target well inside [lo, lo + e) of the chosen move
+    if (!(target - last_lo > HEUR_MARGIN * total && last_lo + last_e - target > HEUR_MARGIN * total))
+        uncertain = true;
+    out_r = found_r;
+    out_c = found_c;
+}
+
 // counter[2] of a handle: sticky error bits of device-path launches, reported (and
 // cleared) by bk_synchronize
 #define BK_STATUS_CAP 8u     // bk_result.status: arena run stopped by the turn cap
@@ -1191,20 +1471,54 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
     return v;
 }
 
-template <bool FR>
+// RandomState.random_sample() of the current mover's stream (genrand_res53: two 32-bit
+// outputs), as rng.choice draws it (agents/heuristic_agent.py:65)
+__device__ __forceinline__ double draw_double(const RolloutArgs& a, Game& g, const Slab& slab) {
+    uint32_t x0, x1;
+    if (a.cfg.rng == BK_RNG_NUMPY_MT) {
+        const int q = a.cfg.seats_share_stream ? 0 : g.cur;
+        uint32_t* base = slab.base + SLAB_RNG_BASE + 4 * q;
+        MtCursor m;
+        m.i = base[0]; m.a = base[1]; m.b = base[2]; m.c = base[3];
+        bool ov = (g.status & 1u) != 0u;
+        x0 = mt_cursor_next(m, ov);
+        x1 = mt_cursor_next(m, ov);
+        if (ov) g.status |= 1u;
+        base[0] = m.i; base[1] = m.a; base[2] = m.b; base[3] = m.c;
+    } else {
+        x0 = philox_u32(g.pcount++, (uint32_t)g.pid, a.cfg.seed);
+        x1 = philox_u32(g.pcount++, (uint32_t)g.pid, a.cfg.seed);
+    }
+    g.draws += 2;
+    return ((double)(x0 >> 5) * 67108864.0 + (double)(x1 >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// heuristic-policy kernels: 128-lane blocks, per lane 84 LDS dwords ({B, C} rows, then
+// 21 per-piece e sums as doubles; the frontier-table staging reuses the area)
+#define HBLOCK 128
+#define HEUR_WORDS (84 * WAVE)
+#define HEUR_PSUM 40  // dword offset of the per-piece sums in a wave's area
+
+template <bool FR, bool HEUR = false>
 __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
-    constexpr int AREA = FR ? ROLL_WORDS_FR : ROLL_WORDS_PER_WAVE;
-    // FR: + the CPython cell hashes (shared by the block) for the frontier tables
-    __shared__ uint32_t lds[AREA * (BLOCK / WAVE) + (FR ? 2 * BK_CELLS : 0)];
+    constexpr int BLK = HEUR ? HBLOCK : BLOCK;
+    constexpr int AREA = HEUR ? HEUR_WORDS : FR ? ROLL_WORDS_FR : ROLL_WORDS_PER_WAVE;
+    constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
+    // FR: + the CPython cell hashes (shared by the block) for the frontier tables;
+    // HEUR: + the policy's exp tables
+    __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + (FR ? 2 * BK_CELLS : 0) + HS_WORDS];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint32_t* my = lds + wv * AREA;
     uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * AREA) + lane;  // + R * WAVE
-    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLOCK / WAVE));
+    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
+    HeurShared* hs = reinterpret_cast<HeurShared*>(lds + AREA * (BLK / WAVE) + (FR ? 2 * BK_CELLS : 0));
+    double* psum = reinterpret_cast<double*>(lds + wv * AREA + HEUR_PSUM * WAVE) + lane;  // + piece * WAVE
     if constexpr (FR) {
-        for (int i = threadIdx.x; i < BK_CELLS; i += BLOCK) htab[i] = kCellHash[i];
-        __syncthreads();
+        for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab[i] = kCellHash[i];
     }
-    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
+    if constexpr (FR || HEUR) __syncthreads();
+    const uint32_t slot = blockIdx.x * BLK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
     const bool advance = a.cfg.semantics == BK_SEM_ADVANCE;
@@ -1260,7 +1574,44 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         }
         make_pairs(P);
         const uint32_t avail = idle ? 0u : (~g.used.get(p) & 0x1FFFFFu);
-        const uint32_t total = movegen_counts<true>(P, avail, my, lane);
+        uint32_t total;
+        int gs = 0;
+        uint32_t kk = 0;
+        // heuristic policy (HEUR kernels): this lane's mover plays HeuristicAgent
+        const bool heur = HEUR && !idle && ((a.cfg.heuristic_seats >> p) & 1u);
+        double h_target = 0.0, h_R = 0.0, h_total = 0.0;
+        uint32_t h_ok[20];
+        bool h_unc = false;
+        if constexpr (HEUR) {
+            total = 0;
+            // uniform-random movers: counts, draw, orientation (before the area is reused)
+            if (__builtin_amdgcn_ballot_w64(!idle && !heur)) {
+                const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane);
+                if (!idle && !heur) {
+                    total = t;
+                    if (t > 0u) gs = pick_orient(my, lane, draw_index(a, g, slab, slot, t), kk);
+                }
+            }
+            if (__builtin_amdgcn_ballot_w64(heur)) {
+                const int edge_w = (g.move_count0 + g.plies) < 30 ? 6 : 3;  // move_count / 100.0 < 0.3
+#pragma unroll
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE].x = P.B[R];
+                const uint32_t t = heur_pass_a(P, heur ? avail : 0u, rows_lds, psum, hs, edge_w);
+#pragma unroll
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+                if (heur) {
+                    total = t;
+                    if (t > 0u) {
+#pragma unroll 1
+                        for (int q = 0; q < BK_PIECES; ++q) h_total += psum[q * WAVE];
+                        h_target = draw_double(a, g, slab) * h_total;
+                        gs = heur_pick_orient(psum, rows_lds, hs, edge_w, h_target, h_R, h_ok, h_unc);
+                    }
+                }
+            }
+        } else {
+            total = movegen_counts<true>(P, avail, my, lane);
+        }
         SECT(2);
         if (idle) continue;
         if (total == 0u) {
@@ -1273,9 +1624,10 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             }
             continue;
         }
-        const uint32_t k = draw_index(a, g, slab, slot, total);
-        uint32_t kk;
-        const int gs = pick_orient(my, lane, k, kk);
+        if constexpr (!HEUR) {
+            const uint32_t k = draw_index(a, g, slab, slot, total);
+            gs = pick_orient(my, lane, k, kk);
+        }
         // counts are consumed: the area now takes the mover's rows for locate
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
@@ -1283,9 +1635,24 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         int ar, ac;
         if constexpr (FR) {
             const bk_fset* fs = &a.fslab[slot].s;
-            locate_move_frontier(gs, kk, rows_lds, fs->key[p], fs->mask[p], ar, ac);
+            if (heur && gs < 0) {
+                ar = -1;
+                ac = 0;
+            } else if (heur) {
+                const int edge_w = (g.move_count0 + g.plies) < 30 ? 6 : 3;
+                heur_walk_frontier(gs, h_ok, rows_lds, fs->key[p], fs->mask[p], hs, edge_w, h_target, h_R, h_total,
+                                   ar, ac, h_unc);
+                if (h_unc) g.status |= BK_STATUS_UNCERT;
+            } else {
+                locate_move_frontier(gs, kk, rows_lds, fs->key[p], fs->mask[p], ar, ac);
+            }
         } else {
             locate_move_lds(gs, kk, rows_lds, ar, ac);
+        }
+        if (HEUR && ar < 0) {  // cannot happen (counts > 0 means e sums > 0); never write off the board
+            g.status |= BK_STATUS_UNCERT;
+            finish_game<FR>(a, g, slab, slot);
+            continue;
         }
         SECT(4);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
@@ -1347,6 +1714,8 @@ __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_rollout(RolloutAr
 __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_advance(RolloutArgs a) { rollout_body<false>(a); }
 // reference frontier order (compat parity mode)
 __global__ __launch_bounds__(BLOCK, 2) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
+// reference frontier order with HeuristicAgent seats (cfg.heuristic_seats)
+__global__ __launch_bounds__(HBLOCK, 3) void k_rollout_fr_h(RolloutArgs a) { rollout_body<true, true>(a); }
 
 // ------------------------------------------------------------------------------------
 // FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256): one wave per game
@@ -1960,17 +2329,35 @@ __device__ __forceinline__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& 
     }
 }
 
-__global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
-    // per wave: counts / B,C rows / the staged frontier table share ROLL_WORDS_FR
-    __shared__ uint32_t lds[ROLL_WORDS_FR * (BLOCK / WAVE) + 2 * BK_CELLS];
+// numpy RandomState.random_sample() (genrand_res53) from a per-game stream
+__device__ __forceinline__ double mc_random_sample(uint32_t* st, uint32_t& pos) {
+    if (pos >= FM_N) { mc_twist(st); pos = 0; }
+    const uint32_t a0 = mc_temper(st[pos++]);
+    if (pos >= FM_N) { mc_twist(st); pos = 0; }
+    const uint32_t a1 = mc_temper(st[pos++]);
+    return ((double)(a0 >> 5) * 67108864.0 + (double)(a1 >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// HEUR: rollouts play HeuristicAgent (MCTSAgent's default rollout_agent,
+// mcts/mcts_agent.py:275-281) instead of RandomAgent
+template <bool HEUR>
+__device__ __forceinline__ void mcts_body(const MctsArgs& a) {
+    constexpr int BLK = HEUR ? HBLOCK : BLOCK;
+    constexpr int AREA = HEUR ? HEUR_WORDS : ROLL_WORDS_FR;
+    constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
+    // per wave: counts / B,C rows (+ HEUR: per-piece e sums) / the staged frontier table
+    __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + 2 * BK_CELLS + HS_WORDS];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint32_t* my = lds + wv * ROLL_WORDS_FR;
+    uint32_t* my = lds + wv * AREA;
     uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
     int16_t* lk = reinterpret_cast<int16_t*>(my) + lane;
-    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + ROLL_WORDS_FR * (BLOCK / WAVE));
-    for (int i = threadIdx.x; i < BK_CELLS; i += BLOCK) htab[i] = kCellHash[i];
+    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
+    HeurShared* hs = reinterpret_cast<HeurShared*>(lds + AREA * (BLK / WAVE) + 2 * BK_CELLS);
+    double* psum = reinterpret_cast<double*>(my + HEUR_PSUM * WAVE) + lane;
+    for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab[i] = kCellHash[i];
+    if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
     __syncthreads();
-    const uint32_t slot = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t slot = blockIdx.x * BLK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     McLane* L = a.lanes + slot;
     Mc m;
@@ -2047,16 +2434,50 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
                 mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
                 continue;
             }
-            k = mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
+            k = HEUR ? 0u : mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
         }
         uint32_t kk;
-        const int gs = pick_orient(my, lane, k, kk);
+        int gs = pick_orient(my, lane, k, kk);
+        // HEUR: a rollout ply's move is HeuristicAgent.select_action's (heur_* above)
+        const bool hroll = HEUR && m.mode == MC_ROLLOUT;
+        double h_target = 0.0, h_R = 0.0, h_total = 0.0;
+        uint32_t h_ok[20];
+        bool h_unc = false;
+        int edge_w = 6;
+        if constexpr (HEUR) {
+            if (__builtin_amdgcn_ballot_w64(hroll)) {
+                // Board.move_count of the rollout board: placements on the way from the root
+                edge_w = (int)(a.roots[m.game].move_count + m.depth + m.plies) < 30 ? 6 : 3;
+#pragma unroll
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE].x = P.B[R];
+                heur_pass_a(P, hroll ? avail : 0u, rows_lds, psum, hs, edge_w);
+#pragma unroll
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+                if (hroll) {
+#pragma unroll 1
+                    for (int q = 0; q < BK_PIECES; ++q) h_total += psum[q * WAVE];
+                    h_target = mc_random_sample(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos) * h_total;
+                    gs = heur_pick_orient(psum, rows_lds, hs, edge_w, h_target, h_R, h_ok, h_unc);
+                }
+            }
+        }
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
         FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
         int ar, ac;
         SECT(10);
-        locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+        if (hroll) {
+            if (gs < 0) {
+                ar = -1;
+                ac = 0;
+            } else {
+                heur_walk_frontier(gs, h_ok, rows_lds, T->s.key[p], T->s.mask[p], hs, edge_w, h_target, h_R, h_total,
+                                   ar, ac, h_unc);
+            }
+            if (h_unc) m.status |= BK_MCTS_EUNCERT;
+        } else {
+            locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+        }
         SECT(11);
         if (ar < 0) {  // the table does not list the move: counts and tables disagree
             m.status |= BK_MCTS_EINTERNAL;
@@ -2118,6 +2539,9 @@ __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) {
     }
     SECT_FLUSH;
 }
+
+__global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
+__global__ __launch_bounds__(HBLOCK, 3) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
 
 // ------------------------------------------------------------------------------------
 // C ABI
@@ -2386,6 +2810,8 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     if (cfg->rng == BK_RNG_NUMPY_MT && !compat_seeds)
         return set_err(h, BK_EINVAL, "bk_rollout: compat rng needs compat_seeds%s", "");
     if (cfg->max_plies <= 0) return set_err(h, BK_EINVAL, "bk_rollout: max_plies must be > 0%s", "");
+    if ((cfg->heuristic_seats & ~0xF) || (cfg->heuristic_seats && !fr))
+        return set_err(h, BK_EINVAL, "bk_rollout: heuristic_seats (4 bits) needs BK_ORDER_FRONTIER%s", "");
     if (n_playouts == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
     void *d_roots, *d_idx = nullptr, *d_seeds = nullptr;
@@ -2426,11 +2852,13 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         }
     }
     // persistent grid: every resident slot pulls playouts from the counter
-    int blocks = h->num_cu * h->rollout_blocks_per_cu;
-    const int need = (n_playouts + BLOCK - 1) / BLOCK;
+    const bool heur = fr && (cfg->heuristic_seats & 0xF) != 0;
+    const int blk = heur ? HBLOCK : BLOCK;
+    int blocks = h->num_cu * (heur ? 3 : fr ? 2 : h->rollout_blocks_per_cu);
+    const int need = (n_playouts + blk - 1) / blk;
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    const uint32_t nslots = (uint32_t)blocks * BLOCK;
+    const uint32_t nslots = (uint32_t)blocks * blk;
     rc = grow(h, &h->d_slab, &h->d_slab_cap, sizeof(uint32_t) * SLAB_WORDS * (size_t)nslots);
     if (rc) return rc;
     if (fr) {
@@ -2447,7 +2875,9 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
                   (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    if (fr)
+    if (heur)
+        hipLaunchKernelGGL(k_rollout_fr_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
+    else if (fr)
         hipLaunchKernelGGL(k_rollout_fr, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     else if (cfg->semantics == BK_SEM_ADVANCE)
         hipLaunchKernelGGL(k_advance, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
@@ -2749,7 +3179,8 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         !mt_state || !log_table || log_len < 1 || !out || (rewards == nullptr) != (hit_flags == nullptr))
         return set_err(h, BK_EINVAL, "bk_mcts: missing buffer%s", "");
     if (cfg->iterations < 0 || cfg->max_rollout_moves <= 0 || cfg->node_cap < 1 || cfg->time_limit_us < 0 ||
-        cfg->iter_stop < 0 || (cfg->resume != 0 && cfg->resume != 1))
+        cfg->iter_stop < 0 || (cfg->resume != 0 && cfg->resume != 1) ||
+        (cfg->rollout_policy != BK_MCTS_ROLLOUT_RANDOM && cfg->rollout_policy != BK_MCTS_ROLLOUT_HEURISTIC))
         return set_err(h, BK_EINVAL, "bk_mcts: bad cfg (iterations/max_rollout_moves/node_cap/iter_stop/resume)%s", "");
     if (cfg->resume && !nodes)
         return set_err(h, BK_EINVAL, "bk_mcts: resume needs the caller's nodes buffer%s", "");
@@ -2808,11 +3239,13 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         p += al(sec[i].bytes);
     }
     // persistent grid: every resident slot pulls whole searches from the counter
-    int blocks = h->num_cu * 2;
-    const int need = (n_games + BLOCK - 1) / BLOCK;
+    const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;
+    const int blk = heur ? HBLOCK : BLOCK;
+    int blocks = h->num_cu * (heur ? 3 : 2);
+    const int need = (n_games + blk - 1) / blk;
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    const uint32_t nslots = (uint32_t)blocks * BLOCK;
+    const uint32_t nslots = (uint32_t)blocks * blk;
     rc = grow(h, &h->d_slab, &h->d_slab_cap, sizeof(uint32_t) * SLAB_WORDS * (size_t)nslots);
     if (rc) return rc;
     rc = grow(h, &h->d_mclane, &h->d_mclane_cap, sizeof(McLane) * (size_t)nslots);
@@ -2831,7 +3264,10 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
+    if (heur)
+        hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
+    else
+        hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;

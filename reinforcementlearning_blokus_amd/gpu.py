@@ -151,16 +151,17 @@ class BlokusGPU:
     def rollout_frontier(self, roots, root_sets, n_playouts: int, *, semantics: int = N.SEM_ARENA,
                          rng: int = N.RNG_NUMPY_MT, seed: int = 0, max_plies: int | None = None,
                          compat_seeds=None, root_index=None, seats_share_stream: bool = False, out=None,
-                         with_results: bool = False, with_states: bool = False):
+                         with_results: bool = False, with_states: bool = False, heuristic_seats: int = 0):
         """Playouts in the reference's FRONTIER list order (bk_rollout_frontier): with the
         numpy-MT compat stream these are the reference's default-config games.
         root_sets: FSET_DTYPE records (one per root).  Host numpy in/out.  SEM_ADVANCE
         returns (states, tables[, results]); SEM_ARENA with with_states returns
-        (states, tables, results): the final positions as well."""
+        (states, tables, results): the final positions as well.  heuristic_seats: bit p =
+        seat p plays HeuristicAgent (its draws from the seat's compat stream)."""
         if max_plies is None:
             max_plies = 2500 if semantics == N.SEM_ARENA else 50
         cfg = N.BkRolloutCfg(semantics, N.ORDER_FRONTIER, rng, max_plies, seed & (2**64 - 1),
-                             int(seats_share_stream), 0)
+                             int(seats_share_stream), int(heuristic_seats))
         if _is_torch(roots):  # device tensors: roots uint8 [n,256], root_sets uint8 [n,2080]
             import torch
             assert semantics != N.SEM_ADVANCE, "device path: playout results only"
@@ -269,7 +270,7 @@ class BlokusGPU:
     def mcts(self, roots, root_sets, players, root_hash, *, iterations: int, zobrist, mt_state,
              zobrist_index=None, tt: "MctsTT" = None, max_rollout_moves: int = 50, exploration: float = 1.414,
              log_table=None, node_cap: int = 0, time_limit_us: int = 0, want_rewards: bool = True,
-             want_nodes: bool = False, chunk: int = 0):
+             want_nodes: bool = False, chunk: int = 0, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM):
         """MCTSAgent.select_action searches for a batch of positions, whole on the GPU
         (bk_mcts; mcts/mcts_agent.py:304-582 with RandomAgent rollouts).
 
@@ -281,6 +282,8 @@ class BlokusGPU:
         node_cap: node slots per search (default 4 * iterations + 1, which the kernel's
         child-block growth never exceeds).  chunk > 0: run the searches in launches of
         `chunk` iterations (cfg.iter_stop / cfg.resume), same result as one launch.
+        rollout_policy: MCTS_ROLLOUT_RANDOM (RandomAgent) or MCTS_ROLLOUT_HEURISTIC
+        (HeuristicAgent, MCTSAgent's default); mt_state is that agent's stream.
         Returns dict(out=MCTS_OUT_DTYPE[n], rewards, hit_flags, nodes)."""
         n = len(roots)
         roots = np.ascontiguousarray(roots, dtype=STATE_DTYPE)
@@ -311,7 +314,8 @@ class BlokusGPU:
             self.handle.set_stream(None)
             for j, stop in enumerate(stops):
                 cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(tt is not None), cap,
-                                  tt.cap if tt is not None else 0, int(time_limit_us), stop, int(j > 0))
+                                  tt.cap if tt is not None else 0, int(time_limit_us), stop, int(j > 0),
+                                  int(rollout_policy), 0)
                 self.handle.mcts(roots.ctypes.data, root_sets.ctypes.data, pl.ctypes.data, rh.ctypes.data, n, cfg,
                                  zob.ctypes.data, len(zob), zi.ctypes.data, mt_state.ctypes.data,
                                  ptr(tt.keys) if tt is not None else 0, ptr(tt.vals) if tt is not None else 0,
@@ -331,7 +335,7 @@ class BlokusGPU:
     def mcts_device(self, roots, root_sets, players, root_hash, zobrist, zobrist_index, mt_state, log_table, nodes,
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
                     hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
-                    on_chunk=None, stop_after: int | None = None):
+                    on_chunk=None, stop_after: int | None = None, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM):
         """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
@@ -371,7 +375,7 @@ class BlokusGPU:
             stops = [x for x in stops if 0 < x < stop_after] + [stop_after]
         for j, stop in enumerate(stops):
             cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
-                              tt_keys.shape[1] if use_tt else 0, 0, stop, int(j > 0))
+                              tt_keys.shape[1] if use_tt else 0, 0, stop, int(j > 0), int(rollout_policy), 0)
             self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
                              d(zobrist_index), d(mt_state), d(tt_keys), d(tt_vals), d(tt_count), d(log_table),
                              log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)

@@ -8,18 +8,18 @@ Rollouts (mcts/mcts_agent.py:470-554, <= max_rollout_moves plies, stop at the fi
 player without a move, reward = final - initial Board.get_score of the root player)
 have three GPU backends:
 
-* ``rollout_backend="search"`` (default when the rollout_agent is a RandomAgent): the
-  WHOLE search -- selection, expansion, TT lookups, RandomAgent rollouts,
-  backpropagation -- runs in one bk_mcts launch (k_mcts), bit-identical to the
-  reference: frontier-order legal lists, the agent's numpy MT19937 stream (read from
-  and written back to ``rollout_agent.rng``), the Zobrist TT kept in device-layout
-  tables across calls.  ``search_batch`` runs many agents' searches in one launch.
+* ``rollout_backend="search"`` (the default, for the reference's default HeuristicAgent
+  rollout agent and for a RandomAgent): the WHOLE search -- selection, expansion, TT
+  lookups, rollouts, backpropagation -- runs in one bk_mcts launch (k_mcts / k_mcts_h),
+  bit-identical to the reference: frontier-order legal lists, the agent's numpy MT19937
+  stream (read from and written back to ``rollout_agent.rng``), HeuristicAgent choices
+  certified exact per draw, the Zobrist TT kept in device-layout tables across calls.
+  ``search_batch`` runs many agents' searches in one launch.
 * ``rollout_backend="exact"`` (a rollout_agent with ``select_action``): the tree and
   the ply loop run on the host, every legal-move list comes from the GPU in the
   reference's frontier order and the agent draws from its own stream -- bit-identical
   to the reference for RandomAgent, usable with any agent.
-  Without a rollout_agent the reference's default applies, HeuristicAgent(seed=seed)
-  (mcts/mcts_agent.py:278-281), on this backend.
+  Used for rollout agents the kernels do not implement (e.g. re-weighted heuristics).
 * ``rollout_backend="kernel"`` (opt-in): the whole playout runs inside the persistent
   HIP rollout kernel (bk_rollout, BK_SEM_ROLLOUT, Philox stream, naive move order) with
   UNIFORM random moves: statistically a random playout, not the reference's numbers,
@@ -37,6 +37,20 @@ from ..engine.board import Board, Player, Position, _PLAYERS, pack_state
 from ..engine.move_generator import Move, get_shared_generator, int_to_move
 from ..engine.pieces import PieceGenerator
 from .zobrist import TranspositionTable, ZobristHash
+
+
+def _search_policy(agent) -> Optional[int]:
+    """bk_mcts rollout policy replaying this rollout agent on the GPU, or None:
+    RandomAgent, or HeuristicAgent with the reference's default weights (the kernel's
+    scoring constants, agents/heuristic_agent.py:33-37)."""
+    from .. import _native as N
+    from ..agents.heuristic_agent import HeuristicAgent
+    from ..agents.random_agent import RandomAgent
+    if isinstance(agent, RandomAgent):
+        return N.MCTS_ROLLOUT_RANDOM
+    if isinstance(agent, HeuristicAgent) and agent._weights() == (1.0, 2.0, -1.5, 0.5):
+        return N.MCTS_ROLLOUT_HEURISTIC
+    return None
 
 
 def _positions(move: Move) -> List[Position]:
@@ -123,15 +137,15 @@ class MCTSAgent:
             rollout_agent = HeuristicAgent(seed=seed)  # the reference's default policy
         self.rollout_agent = rollout_agent
         if rollout_backend is None:
-            rollout_backend = "search" if isinstance(rollout_agent, RandomAgent) else "exact"
+            rollout_backend = "search" if _search_policy(rollout_agent) is not None else "exact"
         self.rollout_backend = rollout_backend
         if self.rollout_backend not in ("search", "exact", "kernel"):
             raise ValueError("rollout_backend must be 'search', 'exact' or 'kernel'")
         if self.rollout_backend == "exact" and rollout_agent is None:
             raise ValueError("rollout_backend='exact' needs a rollout_agent")
-        if self.rollout_backend == "search" and not isinstance(rollout_agent, RandomAgent):
-            raise ValueError("rollout_backend='search' needs a RandomAgent rollout_agent (its numpy stream "
-                             "is replayed on the GPU)")
+        if self.rollout_backend == "search" and _search_policy(rollout_agent) is None:
+            raise ValueError("rollout_backend='search' needs a RandomAgent or a default-weight HeuristicAgent "
+                             "rollout_agent (its numpy stream is replayed on the GPU)")
         self.seed = 0 if seed is None else int(seed)
         self._kernel_calls = 0
         self.device = device
@@ -206,10 +220,13 @@ class MCTSAgent:
             # kernel stops each search at the first iteration boundary past it, with the
             # iteration count bounded by `iterations` (the node pool / log table size)
             tl_us = int(round(float(a.time_limit) * 1e6)) if a.time_limit else 0
+            policy = _search_policy(a.rollout_agent)
+            if policy is None:
+                raise ValueError("search_batch: the rollout agent cannot be replayed on the GPU")
             key = (int(a.iterations), a.max_rollout_moves, float(a.exploration_constant), a.use_transposition_table,
-                   tl_us)
+                   tl_us, policy)
             groups.setdefault(key, []).append(i)
-        for (iters, max_roll, c, use_tt, tl_us), idx in groups.items():
+        for (iters, max_roll, c, use_tt, tl_us, policy), idx in groups.items():
             ags = [agents[i] for i in idx]
             gpu = ags[0]._gpu = ags[0]._gpu or BlokusGPU(ags[0].device)
             roots = np.concatenate([pack_state(boards[i]) for i in idx])
@@ -234,7 +251,8 @@ class MCTSAgent:
                         tt.load(j, *a._gpu_tt.items(0))
             t0 = time.time()
             r = gpu.mcts(roots, sets, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
-                         mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us)
+                         mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us,
+                         rollout_policy=policy)
             dt = time.time() - t0
             for j, (i, a) in enumerate(zip(idx, ags)):
                 o = r["out"][j]

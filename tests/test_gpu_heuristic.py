@@ -72,17 +72,20 @@ def test_full_heuristic_game_matches_reference(i):
     assert (passes, turns) == (g["passes"], g["turns"])
 
 
+@pytest.mark.parametrize("backend", ["search", "exact"])
 @pytest.mark.parametrize("i", range(len(H["mcts"])))
-def test_mcts_default_heuristic_rollouts_match_reference(i):
+def test_mcts_default_heuristic_rollouts_match_reference(i, backend):
     """MCTSAgent(seed=s) without a rollout agent = HeuristicAgent(seed=s) rollouts
-    (mcts/mcts_agent.py:278-281), host tree + GPU legal lists."""
+    (mcts/mcts_agent.py:278-281): the default "search" backend (the whole search in one
+    k_mcts_h launch) and the "exact" backend (host tree + GPU legal lists)."""
     from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
     c = H["mcts"][i]
     b = engine_board(POS[c["position"]])
     p = Player(c["player"])
+    kw = {} if backend == "search" else {"rollout_backend": "exact"}
     agent = MCTSAgent(iterations=c["iterations"], seed=c["seed"], use_transposition_table=c["use_tt"],
-                      max_rollout_moves=c["max_rollout_moves"])
-    assert agent.rollout_backend == "exact" and isinstance(agent.rollout_agent, HeuristicAgent)
+                      max_rollout_moves=c["max_rollout_moves"], **kw)
+    assert agent.rollout_backend == backend and isinstance(agent.rollout_agent, HeuristicAgent)
     legal = get_shared_generator().get_legal_moves(b, p)
     assert len(legal) == c["n_legal"]
     mv = agent.select_action(b, p, legal)

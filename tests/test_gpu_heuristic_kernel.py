@@ -1,0 +1,138 @@
+"""HeuristicAgent policy inside the GPU kernels (k_rollout_fr_h, k_mcts_h), against the
+reference's recorded games and searches (tests/golden/heuristic.json) and against the
+pinned oracle restatement (oracle/pyoracle.py heuristic_*, tests/test_oracle_heuristic.py)
+on synthetic positions.  Tolerance: exact -- same moves, scores, passes, turns, rewards,
+root statistics and RNG state; every heuristic choice must be certified (status bit 4 /
+BK_MCTS_EUNCERT clear)."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from reinforcementlearning_blokus_amd import _native as N
+from tests.conftest import load_golden
+from tests.helpers import POS, mt_array, oracle_fset, oracle_states, pack_many, replay, sha_ints
+
+pytestmark = pytest.mark.gpu
+H = load_golden("heuristic.json")
+UNCERT = 16
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    return BlokusGPU(0)
+
+
+def _roots(boards):
+    st = pack_many(boards)
+    sets = np.array([oracle_fset(b) for b in boards], dtype=N.FSET_DTYPE)
+    return st, sets
+
+
+def test_full_heuristic_games_match_reference(gpu):
+    """Two full 4-HeuristicAgent games from the empty board (arena loop) in one launch."""
+    from reinforcementlearning_blokus_amd.gpu import empty_state
+    seeds = np.array([[g["seed"] + p + 1 for p in range(4)] for g in H["games"]], np.uint32)
+    res = gpu.rollout_frontier(empty_state(), N.fset_new(1), len(seeds), semantics=N.SEM_ARENA, rng=N.RNG_NUMPY_MT,
+                               compat_seeds=seeds, root_index=np.zeros(len(seeds), np.int32), heuristic_seats=0xF)
+    for r, g in zip(res, H["games"]):
+        assert int(r["status"]) == 0
+        assert [int(x) for x in r["scores"]] == g["scores"]
+        assert [p + 1 for p in range(4) if int(r["winner_mask"]) >> p & 1] == g["winner_ids"]
+        assert (int(r["passes"]), int(r["turns"])) == (g["passes"], g["turns"])
+        assert int(r["plies"]) == sum(1 for t in g["trace"] if t >= 0)
+
+
+def test_selfplay_traces_match_reference(gpu):
+    """heuristic.json cases: 12 turns of heuristic self-play from 16 positions
+    (one agent per seat, seed * 10 + player): the advanced states equal the replayed
+    reference traces."""
+    cases = H["cases"]
+    boards = [replay(POS[c["position"]]) for c in cases]
+    st, sets = _roots(boards)
+    seeds = np.array([[c["seed"] * 10 + p + 1 for p in range(4)] for c in cases], np.uint32)
+    nmoves = [sum(1 for t in c["selfplay_trace"] if t >= 0) for c in cases]
+    for i, c in enumerate(cases):  # one launch per case: each stops after its own move count
+        out_st, out_fs, res = gpu.rollout_frontier(st[i:i + 1], sets[i:i + 1], 1, semantics=N.SEM_ADVANCE,
+                                                   rng=N.RNG_NUMPY_MT, compat_seeds=seeds[i:i + 1],
+                                                   max_plies=max(nmoves[i], 1), root_index=np.zeros(1, np.int32),
+                                                   heuristic_seats=0xF, with_results=True)
+        b = replay(POS[c["position"]])
+        for t in c["selfplay_trace"]:
+            if t < 0:
+                b.cur = (b.cur + 1) & 3
+            else:
+                O.place_move(b, b.cur, t)
+        if nmoves[i] == 0:
+            continue
+        want = pack_many([b])[0]
+        assert int(res[0]["status"]) & UNCERT == 0
+        assert np.array_equal(out_st[0]["planes"], want["planes"]), i
+        assert np.array_equal(out_st[0]["used"], want["used"]), i
+
+
+@pytest.mark.parametrize("mask", [0xF, 0x5, 0xA, 0x1])
+def test_mixed_arena_games_match_oracle(gpu, mask):
+    """Arena games from 24 synthetic mid-game positions with HeuristicAgent seats (bit p
+    of mask) and RandomAgent seats, per-seat numpy streams: scores, winners, passes,
+    turns, plies equal the oracle's game loop."""
+    boards = oracle_states(24, seed0=4000 + mask, lo=8, hi=40)
+    st, sets = _roots(boards)
+    seeds = (np.arange(24 * 4, dtype=np.uint32).reshape(24, 4) * 7919 + mask).astype(np.uint32)
+    res = gpu.rollout_frontier(st, sets, 24, semantics=N.SEM_ARENA, rng=N.RNG_NUMPY_MT, compat_seeds=seeds,
+                               root_index=np.arange(24, dtype=np.int32), heuristic_seats=mask)
+    for i in range(24):
+        # the game is played on the board itself (no Board.copy(): set.copy() would
+        # re-lay the frontier tables out and change the list order)
+        scores, wm, moves, passes, turns, _ = O.mixed_playout_arena(boards[i], seeds[i].tolist(), mask)
+        r = res[i]
+        assert int(r["status"]) == 0, i
+        assert [int(x) for x in r["scores"]] == list(scores), i
+        assert int(r["winner_mask"]) == wm, i
+        assert (int(r["plies"]), int(r["passes"]), int(r["turns"])) == (moves, passes, turns), i
+
+
+def test_heuristic_rollouts_match_oracle(gpu):
+    """MCTSAgent._rollout with its default HeuristicAgent rollout agent (one stream for
+    every seat, 50-ply cap, stop at the first stuck player): rewards and plies."""
+    boards = oracle_states(32, seed0=777, lo=12, hi=44)
+    st, sets = _roots(boards)
+    seeds = np.zeros((32, 4), np.uint32)
+    seeds[:, 0] = np.arange(32) + 90
+    res = gpu.rollout_frontier(st, sets, 32, semantics=N.SEM_ROLLOUT, rng=N.RNG_NUMPY_MT, compat_seeds=seeds,
+                               root_index=np.arange(32, dtype=np.int32), seats_share_stream=True,
+                               heuristic_seats=0xF, max_plies=50)
+    for i in range(32):
+        rw, plies = O.heuristic_rollout_a(boards[i], boards[i].cur, np.random.RandomState(int(seeds[i, 0])), 50)
+        assert int(res[i]["status"]) == 0, i
+        assert (int(res[i]["reward"]), int(res[i]["plies"])) == (rw, plies), i
+
+
+@pytest.mark.parametrize("case", range(len(H["mcts"])))
+def test_mcts_heuristic_rollouts_match_reference(gpu, case):
+    """MCTSAgent(iterations, seed) with its DEFAULT rollout policy (HeuristicAgent(seed))
+    as one bk_mcts launch: best move, root children, rollout rewards, TT hits and the
+    rollout agent's RNG state equal the reference's search."""
+    from reinforcementlearning_blokus_amd.gpu import MctsTT
+    from reinforcementlearning_blokus_amd.mcts.zobrist import ZobristHash, flat_keys, hash_states
+    c = H["mcts"][case]
+    b = replay(POS[c["position"]])
+    player = c["player"] - 1
+    st, sets = _roots([b])
+    st["current_player"] = player
+    keys = flat_keys(ZobristHash(seed=c["seed"]))
+    mt = mt_array(O.numpy_mt(c["seed"]))[None, :].copy()
+    tt = MctsTT(1) if c["use_tt"] else None
+    r = gpu.mcts(st, sets, np.array([player], np.uint8), hash_states(st, keys), iterations=c["iterations"],
+                 zobrist=keys[None], mt_state=mt, tt=tt, max_rollout_moves=c["max_rollout_moves"], want_nodes=True,
+                 rollout_policy=N.MCTS_ROLLOUT_HEURISTIC)
+    o = r["out"][0]
+    assert int(o["status"]) == 0
+    assert int(o["best_move"]) == c["move"]
+    root = r["nodes"][0, 0]
+    kids = r["nodes"][0, root["child0"]: root["child0"] + root["n_exp"]]
+    assert [[int(x["move"]), int(x["visits"]), float(x["total"])] for x in kids] == c["root_children"]
+    rew = [x for x, f in zip(r["rewards"][0].tolist(), r["hit_flags"][0].tolist()) if not f]
+    assert rew == c["rollout_rewards"]
+    assert int(o["tt_hits"]) == c["transposition_hits"]
+    assert int(mt[0, 624]) == c["rng_pos"] and sha_ints(mt[0, :624].tolist()) == c["rng_sha"]
