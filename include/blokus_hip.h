@@ -226,6 +226,28 @@ int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_
                         bk_fset* out_sets, int mem);
 
 /*
+ * Arena games with search seats (config 4, analytics/tournament/arena_runner.py:578-777):
+ * advance each of n games in place until the player to move is a STOP seat that has a
+ * legal move (its agent -- MCTSAgent / FastMCTSAgent -- is run by the caller, which then
+ * places the move and calls again), or the game is over, or it reached cfg->max_plies
+ * turns in total.  Other seats play RandomAgent (randint) or, where seat_masks[i] bit p is
+ * set, HeuristicAgent, each from its own numpy stream carried in rng_state[i][16] (seat p:
+ * MT19937 cursor {pos, mt[pos], mt[pos + 1], mt[pos + 397]} of the first 227 outputs of its
+ * seed; bk_mt_cursor_init makes fresh ones).  seat_masks[i]: bits 0-3 heuristic seats,
+ * bits 4-7 stop seats.  states[i] / sets[i] (the position and its frontier tables) are
+ * read and rewritten; states[i].reserved[0] / [1] carry the game's turn_count / passes
+ * across calls (0 at the start).  out[i]: status BK_STATUS_STOP (32) = stopped at a stop
+ * seat (current_player of states[i]), else the finished game's result (status bit 3: cut
+ * by max_plies; passes / turns in out count this call only).  cfg: BK_SEM_ARENA,
+ * BK_ORDER_FRONTIER, BK_RNG_NUMPY_MT, seats_share_stream 0.
+ */
+#define BK_STATUS_STOP 32
+int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const bk_rollout_cfg* cfg,
+                     const uint8_t* seat_masks, uint32_t* rng_state, bk_result* out, int mem);
+/* numpy RandomState(seed) cursor for rng_state (host, no GPU) */
+int bk_mt_cursor_init(uint32_t seed, uint32_t* out4);
+
+/*
  * FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256) for n_games independent
  * roots, one wave per game.  Game i's root children are legal[legal_offset[i] ..
  * legal_offset[i+1]) (any int payload; only the count and order matter: expansion pops

@@ -17,6 +17,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BK_LIB_PATH") or os.path.join(_HERE, "_lib", "libblokus_hip.so")
 
 OK, EINVAL, EHIP, ENOMEM, EOVERFLOW = 0, -1, -2, -3, -4
+STATUS_CAP, STATUS_UNCERT, STATUS_STOP = 8, 16, 32  # bk_result.status bits
 MEM_HOST, MEM_DEVICE = 0, 1
 SEM_ARENA, SEM_ROLLOUT, SEM_ADVANCE = 0, 1, 2
 ORDER_NAIVE, ORDER_FRONTIER = 0, 1
@@ -30,7 +31,8 @@ EXPORTS = (
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
-    "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select",
+    "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
+    "bk_mt_cursor_init",
 )
 FSET_SLOTS = 256
 # bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
@@ -154,6 +156,8 @@ def load():
             "bk_fastmcts": (C.c_int, [vp, C.c_int32, vp, vp, vp, vp, vp, C.c_int32, vp, vp, C.c_int32, C.c_double,
                                       vp, vp, C.c_int]),
             "bk_pow_half_fix": (C.c_int, [vp, C.c_int32, vp, vp, C.c_int32, P(C.c_int32)]),
+            "bk_arena_advance": (C.c_int, [vp, vp, vp, C.c_int32, P(BkRolloutCfg), vp, vp, vp, C.c_int]),
+            "bk_mt_cursor_init": (C.c_int, [C.c_uint32, vp]),
             "bk_debug_fastmcts_select": (C.c_int, [vp, C.c_int32, vp, vp, C.c_uint32, vp, C.c_int32, vp, vp,
                                                    C.c_int32, C.c_double, P(C.c_int32)]),
             "bk_last_kernel_ms": (C.c_int, [vp, P(C.c_float)]),
@@ -224,6 +228,16 @@ def pow_half_fix(log_table: np.ndarray, rows: int | None = None, cached_only: bo
     if rows >= have:
         c.update(lt=lt[:rows].copy(), off=off, ent=ent)
     return off, ent
+
+
+def mt_cursors(seeds) -> np.ndarray:
+    """uint32[len(seeds), 4]: bk_mt_cursor_init of each numpy RandomState seed."""
+    L = load()
+    seeds = np.asarray(seeds, dtype=np.uint32).reshape(-1)
+    out = np.zeros((len(seeds), 4), np.uint32)
+    for i, sd in enumerate(seeds.tolist()):
+        L.bk_mt_cursor_init(sd, out[i].ctypes.data)
+    return out
 
 
 def fset_new(n: int = 1) -> np.ndarray:
@@ -364,6 +378,12 @@ class Handle:
                                  v(ttc_ptr), v(log_ptr), log_len, v(nodes_ptr), v(rewards_ptr), v(flags_ptr),
                                  v(out_ptr), mem)
         self.check(rc, "bk_mcts")
+
+    def arena_advance(self, states_ptr, sets_ptr, n, cfg: BkRolloutCfg, masks_ptr, rng_ptr, out_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_arena_advance(self._h, C.c_void_p(states_ptr), C.c_void_p(sets_ptr), n, C.byref(cfg),
+                                          C.c_void_p(masks_ptr), C.c_void_p(rng_ptr), C.c_void_p(out_ptr), mem)
+        self.check(rc, "bk_arena_advance")
 
     def advance(self, roots_ptr, n_roots, index_ptr, n, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
         with self._lock:

@@ -219,6 +219,51 @@ class FastMCTSAgent:
             results[i] = self._finish(out[k], boards[i], players[i], legal_lists[i], time_budget_ms, start)
         return results  # type: ignore[return-value]
 
+    @staticmethod
+    def think_many(agents: Sequence["FastMCTSAgent"], players: Sequence[Player], legal_lists: Sequence[List[Move]],
+                   move_counts: Sequence[int], iterations: Sequence[int]) -> List[Optional[Move]]:
+        """think(board, player, legal, budget >= 10^7 ms) of several agents, each on its
+        own root, in ONE bk_fastmcts launch: agent k runs iterations[k] iterations from its
+        own random stream, exactly as its think() would (the arena's deterministic budget,
+        arena_runner.py:352-369).  move_counts[k] = board.move_count (key of the
+        reference's cached legal list, :304-312).  Returns each agent's move."""
+        assert len({id(a) for a in agents}) == len(agents), "one search per agent per launch"
+        moves: List[Optional[Move]] = [None] * len(agents)
+        todo = []
+        for k, (a, p, legal) in enumerate(zip(agents, players, legal_lists)):
+            if len(legal) == 1:
+                moves[k] = legal[0]
+            elif len(legal) > 1:
+                if len(legal) > _MAX_CHILDREN:
+                    raise ValueError(f"{len(legal)} legal moves exceed the kernel's {_MAX_CHILDREN}")
+                todo.append(k)
+        if not todo:
+            return moves
+        bases = []
+        for k in todo:
+            a, p, legal = agents[k], players[k], legal_lists[k]
+            cache = a._legal_moves_cache.setdefault(f"{p.name}_{int(move_counts[k])}", legal)
+            q = a._quick_move_evaluation(cache) if cache else None
+            bases.append(math.nan if q is None else
+                         q.piece_id * 0.1 + (20 - (abs(q.anchor_row - 9.5) + abs(q.anchor_col - 9.5))) * 0.05)
+        base_of = dict(zip(todo, bases))
+        groups: Dict[float, List[int]] = {}  # one launch per exploration constant
+        for k in todo:
+            groups.setdefault(float(agents[k].exploration_constant), []).append(k)
+        for c, ks in groups.items():
+            mt = np.stack([agents[k]._rng_words() for k in ks])
+            counts = [max(1, int(iterations[k])) for k in ks]
+            out = agents[ks[0]]._engine().fastmcts([len(legal_lists[k]) for k in ks], counts, [base_of[k] for k in ks],
+                                                   mt, _log_table(max(counts) + 1), c)
+            for j, k in enumerate(ks):
+                agents[k]._set_rng_words(mt[j])
+                res, legal = out[j], legal_lists[k]
+                if int(res["iterations"]) < 5:
+                    moves[k] = agents[k]._quick_heuristic_selection(None, players[k], legal)
+                else:
+                    moves[k] = legal[int(res["best_index"])] if int(res["n_children"]) > 0 else legal[0]
+        return moves
+
     def _launch(self, n_legal, counts, bases, mt, want_visits=False, exact_ucb=True):
         # exact_ucb=False: the time budget cut the iteration count (a wall-clock search,
         # not reproducible by the reference either), so do not stall on building pow

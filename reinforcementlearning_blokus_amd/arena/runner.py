@@ -326,6 +326,187 @@ def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id:
     return out
 
 
+_SEARCH_KINDS = ("mcts", "fast_mcts", "gameplay_fast_mcts", "gameplay_mcts")
+
+
+def _batchable(run_config: RunConfig, seats: Mapping[str, str]) -> bool:
+    """run_games_batched can play this seating: random / default-weight heuristic seats
+    each with their own agent (a stream per seat), search seats of the supported kinds."""
+    cfgs = {a.name: a for a in run_config.agents}
+    names = list(seats.values())
+    for name in set(names):
+        c = cfgs[name]
+        kind = c.type.lower()
+        if kind in ("random", "heuristic"):
+            if names.count(name) > 1 or (kind == "heuristic" and c.params.get("weights")):
+                return False
+        elif kind not in _SEARCH_KINDS:
+            return False
+    return True
+
+
+def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
+                      device: int = 0) -> List[Dict[str, Any]]:
+    """Mixed seatings (Random / Heuristic / MCTS / FastMCTS, config 4) in lockstep batches:
+    every game's random and heuristic turns run inside bk_arena_advance (one launch
+    advances all games to their next search-seat turn, each seat drawing from its own
+    agent stream), then all MCTS seats to move search in one bk_mcts launch
+    (MCTSAgent.search_packed) and all FastMCTS seats in one bk_fastmcts launch
+    (FastMCTSAgent.think_many), their moves are placed, and the loop repeats.  Records
+    equal run_single_game's (arena_runner.py:578-777): same agents, seeds, streams and
+    move order.  Per-move times are launch shares."""
+    from .. import _native as N
+    from ..engine.move_generator import order_moves
+    from ..engine.pieces import ORIENT_CELLS, ORIENT_LIST
+    from ..gpu import BlokusGPU, empty_state
+    idx = list(game_indices)
+    n = len(idx)
+    if n == 0:
+        return []
+    cfgs = {a.name: a for a in run_config.agents}
+    gpu = BlokusGPU(device)
+    t0 = time.perf_counter()
+    states = np.repeat(empty_state(), n)
+    sets = N.fset_new(n)
+    masks = np.zeros(n, np.uint8)
+    rng = np.zeros((n, 16), np.uint32)
+    seats, gseeds, agents, per_agent = [], [], [], []
+    for i, gi in enumerate(idx):
+        gs = game_seed_from_run_seed(run_config.seed, gi)
+        st = seat_assignment_for_game(run_config.agent_names, gi, gs, run_config.seat_policy)
+        if not _batchable(run_config, st):
+            raise ValueError(f"game {gi}: seating {st} cannot be batched; use run_single_game")
+        seats.append(st)
+        gseeds.append(gs)
+        built = {}
+        for p in range(4):
+            name = st[str(p + 1)]
+            c = cfgs[name]
+            kind = c.type.lower()
+            seed = agent_seed(run_config.seed, gi, name)
+            if kind in ("random", "heuristic"):
+                rng[i, 4 * p:4 * p + 4] = N.mt_cursors([seed])[0]
+                if kind == "heuristic":
+                    masks[i] |= 1 << p
+            else:
+                masks[i] |= 16 << p
+                if name not in built:
+                    built[name] = build_agent(c, seed)
+        agents.append(built)
+        per_agent.append({name: {"moves": 0.0, "total_time_ms": 0.0, "total_simulations": 0.0,
+                                 "moves_with_simulations": 0.0, "move_times_ms": []} for name in set(st.values())})
+    results: List[Optional[Dict[str, Any]]] = [None] * n
+    active = np.arange(n)
+    while len(active):
+        sub_st, sub_fs, sub_rng = states[active].copy(), sets[active].copy(), rng[active].copy()
+        before = sub_st["reserved"].copy()
+        res = gpu.arena_advance(sub_st, sub_fs, masks[active], sub_rng, max_turns=run_config.max_turns)
+        states[active], sets[active], rng[active] = sub_st, sub_fs, sub_rng
+        stopped = []
+        for j, i in enumerate(active):
+            r = res[j]
+            if int(r["status"]) & N.STATUS_STOP:
+                stopped.append(i)
+                continue
+            if int(r["status"]) & ~(N.STATUS_CAP | N.STATUS_STOP):
+                raise RuntimeError(f"game {idx[i]}: kernel status {int(r['status'])}")
+            turns = int(before[j, 0]) + int(r["turns"])
+            passes = int(before[j, 1]) + int(r["passes"])
+            truncated = False
+            if int(r["status"]) & N.STATUS_CAP:  # cut by max_turns: over or not (arena_runner.py:702)
+                if int(gpu.has_moves(states[i:i + 1])[0]) != 0:
+                    truncated = True
+                else:
+                    turns -= int(r["reserved"][0])
+                    passes -= int(r["reserved"][0])
+            results[i] = (r.copy(), turns, passes, truncated)
+        if stopped:
+            stopped = np.array(stopped)
+            pl = (states["current_player"][stopped] & 3).astype(np.uint8)
+            _, rows = gpu.movegen(states[stopped], pl)
+            chosen: Dict[int, Optional[int]] = {}
+            by_kind: Dict[str, List[Tuple[int, Any, int, list]]] = {"mcts": [], "fast": []}
+            for k, i in enumerate(stopped):
+                p = int(pl[k])
+                adapter = agents[i][seats[i][str(p + 1)]]
+                fr = [divmod(c, 20) for c in N.fset_list(sets[i:i + 1], p)]
+                g, rr, cc = order_moves(rows[k], fr)
+                legal = [int(a) * 400 + int(b) * 20 + int(c) for a, b, c in zip(g, rr, cc)]
+                kind = "mcts" if isinstance(getattr(adapter, "agent", None), MCTSAgent) else "fast"
+                by_kind[kind].append((i, adapter, p, legal))
+            if by_kind["mcts"]:
+                todo = [(i, a, p, lg) for i, a, p, lg in by_kind["mcts"] if len(lg) > 1]
+                for i, a, p, lg in by_kind["mcts"]:
+                    if len(lg) == 1:
+                        chosen[i] = lg[0]
+                if todo:
+                    ti = np.array([t[0] for t in todo])
+                    mv = MCTSAgent.search_packed([t[1].agent for t in todo], states[ti], sets[ti], [t[2] for t in todo])
+                    for (i, a, p, lg), m in zip(todo, mv):
+                        chosen[i] = m
+                        e = per_agent[i][seats[i][str(p + 1)]]
+                        e["total_simulations"] += a.agent.stats["iterations_run"]
+                        e["moves_with_simulations"] += 1
+            if by_kind["fast"]:
+                from ..engine.move_generator import int_to_move, move_to_int
+                ags, players, lists, mcs, iters = [], [], [], [], []
+                for i, a, p, lg in by_kind["fast"]:
+                    fa = a.agent if isinstance(a, _FastMCTSAdapter) else a.agent._agent
+                    budget = (int(cfgs[seats[i][str(p + 1)]].thinking_time_ms or max(int(fa.time_limit * 1000), 1))
+                              if isinstance(a, _FastMCTSAdapter)
+                              else int(cfgs[seats[i][str(p + 1)]].thinking_time_ms or 1))
+                    if not a.deterministic_time_budget:
+                        raise ValueError("run_games_batched: FastMCTS seats need deterministic_time_budget")
+                    ags.append(fa)
+                    players.append(Player(p + 1))
+                    lists.append([int_to_move(x) for x in lg])
+                    mcs.append(int(states["move_count"][i]))
+                    iters.append(max(1, int(round(a.iterations_per_ms * budget))))
+                mv = FastMCTSAgent.think_many(ags, players, lists, mcs, iters)
+                for (i, a, p, lg), m, it in zip(by_kind["fast"], mv, iters):
+                    chosen[i] = move_to_int(m) if m is not None else None
+                    e = per_agent[i][seats[i][str(p + 1)]]
+                    if len(lg) > 1:
+                        e["total_simulations"] += it
+                        e["moves_with_simulations"] += 1
+            for i in stopped:  # place the search moves (Board.place_piece, engine/board.py:515-555)
+                p = int(states["current_player"][i]) & 3
+                m = chosen.get(i)
+                states["reserved"][i, 0] += 1  # turn_count
+                if m is None:  # agent returned no move: the reference passes (arena_runner.py:683-687)
+                    states["reserved"][i, 1] += 1
+                    states["current_player"][i] = (p + 1) & 3
+                    continue
+                g, a = divmod(int(m), 400)
+                cells = [(a // 20 + dr) * 20 + a % 20 + dc for dr, dc in ORIENT_CELLS[g]]
+                for c in cells:
+                    states["planes"][i, p, c // 64] |= np.uint64(1) << np.uint64(c % 64)
+                states["used"][i, p] |= np.uint32(1 << (ORIENT_LIST[g][0] - 1))
+                states["first_move"][i] &= np.uint8(~(1 << p) & 0xFF)
+                states["move_count"][i] += 1
+                states["current_player"][i] = (p + 1) & 3
+                N.fset_place(sets[i:i + 1], states[i:i + 1], p, cells)
+        active = np.array([i for i in active if results[i] is None], dtype=np.int64)
+    dt = time.perf_counter() - t0
+    out = []
+    for i, gi in enumerate(idx):
+        r, turns, passes, truncated = results[i]
+        scores = {p + 1: int(r["scores"][p]) for p in range(4)}
+        winners = [p for p, sc in scores.items() if sc == max(scores.values())]
+        pa = per_agent[i]
+        for p in range(4):
+            pa[seats[i][str(p + 1)]]["moves"] += float(bin(int(states["used"][i, p])).count("1"))
+        total_moves = max(sum(e["moves"] for e in pa.values()), 1.0)
+        for e in pa.values():
+            e["total_time_ms"] = dt / n * (e["moves"] / total_moves) * 1000.0
+        _finish_stats(pa)
+        out.append(_record(run_id=run_id, game_index=gi, game_seed=gseeds[i], run_config=run_config, seats=seats[i],
+                           scores=scores, winner_ids=winners, is_tie=len(winners) > 1,
+                           moves_made=int(states["move_count"][i]), turn_count=turns, passes=passes, invalid=0,
+                           duration=dt / n, truncated=truncated, per_agent=pa, error=None))
+    return out
+
+
 def _write_json(path: Path, payload: Mapping[str, Any]) -> None:
     with path.open("w", encoding="utf-8") as fh:
         json.dump(payload, fh, indent=2, sort_keys=True)
@@ -333,7 +514,7 @@ def _write_json(path: Path, payload: Mapping[str, Any]) -> None:
 
 
 def run_experiment(run_config: RunConfig, *, verbose: bool = False, device: int = 0, rank: int = 0,
-                   world: int = 1, dist=None) -> Dict[str, Any]:
+                   world: int = 1, dist=None, batched: bool = True) -> Dict[str, Any]:
     """run_config.json + games.jsonl + summary.json (:914-996).  With ``world`` > 1 each
     rank plays games index == rank (mod world) on its GPU and rank 0 gathers the records
     and writes the run (one gather of JSON records, games are independent)."""
@@ -341,6 +522,10 @@ def run_experiment(run_config: RunConfig, *, verbose: bool = False, device: int 
     mine = shard_indices(run_config.num_games, rank, world).tolist()
     if _all_random(run_config):
         records = run_games_gpu(run_config, mine, run_id="pending", device=device)
+    elif batched and all(_batchable(run_config, seat_assignment_for_game(
+            run_config.agent_names, gi, game_seed_from_run_seed(run_config.seed, gi), run_config.seat_policy))
+            for gi in mine):
+        records = run_games_batched(run_config, mine, run_id="pending", device=device)
     else:
         agent_configs = {a.name: a for a in run_config.agents}
         records = []

@@ -1217,6 +1217,7 @@ __device__ __forceinline__ void heur_walk_frontier(int gs, const uint32_t (&ok)[
 // counter[2] of a handle: sticky error bits of device-path launches, reported (and
 // cleared) by bk_synchronize
 #define BK_STATUS_CAP 8u     // bk_result.status: arena run stopped by the turn cap
+// BK_STATUS_STOP (32, include/blokus_hip.h): bk_arena_advance stopped at a stop seat
 #define BK_STICKY_GUARD 1u  // a persistent kernel's iteration guard tripped: results incomplete
 #define BK_STICKY_ROOT 2u   // a root_index entry outside [0, n_roots)
 
@@ -1236,6 +1237,8 @@ struct RolloutArgs {
     const bk_fset* root_sets;  // frontier order: roots' tables
     bk_fset* out_sets;         // frontier order + BK_SEM_ADVANCE
     FsLane* fslab;             // frontier order: one record per slot
+    const uint8_t* seat_masks; // bk_arena_advance: per game, bits 0-3 heuristic seats, 4-7 stop seats
+    uint32_t* rng_io;          // bk_arena_advance: per game 4 seats x MT cursor, in/out
 };
 
 // four per-player scalars (kept as separate SSA values: an array indexed by a
@@ -1263,6 +1266,10 @@ struct Game {
     uint32_t pcount;    // philox counter
     uint32_t move_count0;
     uint32_t status;    // bk_result.status bits: 1 rng stream overflow, 2 frontier table overflow
+    uint32_t hmask;     // seats playing HeuristicAgent
+    uint32_t smask;     // stop seats (bk_arena_advance)
+    int32_t cap;        // turn / ply budget of this game in this launch
+    uint32_t turns0, passes0;  // bk_arena_advance: the game's counts before this launch
 };
 
 __device__ __forceinline__ int board_score_q(const Game& g, int q) {  // q static
@@ -1296,7 +1303,9 @@ __device__ __forceinline__ void store_state(const RolloutArgs& a, const Game& g,
     o->flags = 0;
     o->move_count = (uint16_t)(g.move_count0 + g.plies);
     o->reserved16 = 0;
-    o->reserved[0] = o->reserved[1] = 0;
+    // bk_arena_advance: the game's arena turn_count / passes so far (raw, see finish_game)
+    o->reserved[0] = a.seat_masks ? g.turns0 + (uint32_t)g.turns : 0u;
+    o->reserved[1] = a.seat_masks ? g.passes0 + (uint32_t)g.passes : 0u;
 }
 
 __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
@@ -1309,6 +1318,10 @@ __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
 
 template <bool FR>
 __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot) {
+    if (a.rng_io) {  // the seats' streams go on in the next call
+#pragma unroll
+        for (int w = 0; w < 16; ++w) a.rng_io[(size_t)g.pid * 16 + w] = slab.word(SLAB_RNG_BASE + w);
+    }
     if (a.out_states != nullptr) {  // BK_SEM_ADVANCE, or an arena run that wants final states
         store_state(a, g, slab);
         if constexpr (FR) copy_fset(a.out_sets + g.pid, &a.fslab[slot].s);
@@ -1349,11 +1362,12 @@ __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const
             // stopped by the turn cap (arena max_turns) before every player was known
             // to be stuck: the game may or may not be over.  Raw counts, the passes since
             // the last move in reserved[0]; the host decides with has_moves on the final
-            // state (arena_runner.py:702), discounting them if the game is over.
+            // state (arena_runner.py:702), discounting them if the game is over.  (Or
+            // stopped at a stop seat, BK_STATUS_STOP: the game goes on, counts are real.)
             r.passes = (uint16_t)g.passes;
             r.turns = (uint16_t)g.turns;
             r.reserved[0] = (uint32_t)g.since_move;
-            g.status |= BK_STATUS_CAP;
+            if (!(g.status & BK_STATUS_STOP)) g.status |= BK_STATUS_CAP;
         }
     } else {
         int best = -1000000;
@@ -1430,7 +1444,15 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
             copy_fset(&a.fslab[slot].s, a.root_sets + ri);
         }
     }
-    if (a.cfg.rng == BK_RNG_NUMPY_MT) {
+    g.hmask = a.seat_masks ? (a.seat_masks[pid] & 0xFu) : (uint32_t)a.cfg.heuristic_seats;
+    g.smask = a.seat_masks ? ((a.seat_masks[pid] >> 4) & 0xFu) : 0u;
+    g.turns0 = a.seat_masks ? s->reserved[0] : 0u;
+    g.passes0 = a.seat_masks ? s->reserved[1] : 0u;
+    g.cap = a.cfg.max_plies - (int32_t)g.turns0;  // arena_runner max_turns over the whole game
+    if (a.rng_io) {  // seats' streams carried over from the previous call
+#pragma unroll
+        for (int w = 0; w < 16; ++w) slab.word(SLAB_RNG_BASE + w) = a.rng_io[(size_t)pid * 16 + w];
+    } else if (a.cfg.rng == BK_RNG_NUMPY_MT) {
         const int nstreams = a.cfg.seats_share_stream ? 1 : 4;
         for (int q = 0; q < nstreams; ++q) {
             const MtCursor m = mt_cursor_init(a.compat_seeds[(size_t)pid * 4 + q]);
@@ -1522,7 +1544,6 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
     const bool advance = a.cfg.semantics == BK_SEM_ADVANCE;
-    const int32_t cap = a.cfg.max_plies;
 
     Game g;
     g.pid = -1;
@@ -1539,15 +1560,15 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             }
             if (arena) {
 #pragma unroll 1
-                for (int s = 0; s < 4 && ((g.out >> g.cur) & 1u) && g.out != 0xFu && (advance || g.turns < cap); ++s) {
+                for (int s = 0; s < 4 && ((g.out >> g.cur) & 1u) && g.out != 0xFu && (advance || g.turns < g.cap); ++s) {
                     g.passes++; g.turns++; g.since_move++;
                     g.cur = (g.cur + 1) & 3;
                 }
-                if (g.out == 0xFu || (advance ? g.plies : g.turns) >= cap) {
+                if (g.out == 0xFu || (advance ? g.plies : g.turns) >= g.cap) {
                     finish_game<FR>(a, g, slab, slot);
                     continue;
                 }
-            } else if (g.plies >= cap) {
+            } else if (g.plies >= g.cap) {
                 finish_game<FR>(a, g, slab, slot);
                 continue;
             }
@@ -1578,7 +1599,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         int gs = 0;
         uint32_t kk = 0;
         // heuristic policy (HEUR kernels): this lane's mover plays HeuristicAgent
-        const bool heur = HEUR && !idle && ((a.cfg.heuristic_seats >> p) & 1u);
+        const bool heur = HEUR && !idle && ((g.hmask >> p) & 1u);
         double h_target = 0.0, h_R = 0.0, h_total = 0.0;
         uint32_t h_ok[20];
         bool h_unc = false;
@@ -1589,7 +1610,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane);
                 if (!idle && !heur) {
                     total = t;
-                    if (t > 0u) gs = pick_orient(my, lane, draw_index(a, g, slab, slot, t), kk);
+                    // (a stop seat draws nothing: bk_arena_advance hands its turn back)
+                    if (t > 0u && !((g.smask >> p) & 1u)) gs = pick_orient(my, lane, draw_index(a, g, slab, slot, t), kk);
                 }
             }
             if (__builtin_amdgcn_ballot_w64(heur)) {
@@ -1614,6 +1636,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         }
         SECT(2);
         if (idle) continue;
+        if (FR && total > 0u && ((g.smask >> p) & 1u)) {  // a search seat is to move: hand the game back
+            g.status |= BK_STATUS_STOP;
+            finish_game<FR>(a, g, slab, slot);
+            continue;
+        }
         if (total == 0u) {
             if (arena) {
                 g.out |= 1u << p;
@@ -1715,7 +1742,7 @@ __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_advance(RolloutAr
 // reference frontier order (compat parity mode)
 __global__ __launch_bounds__(BLOCK, 2) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
 // reference frontier order with HeuristicAgent seats (cfg.heuristic_seats)
-__global__ __launch_bounds__(HBLOCK, 3) void k_rollout_fr_h(RolloutArgs a) { rollout_body<true, true>(a); }
+__global__ __launch_bounds__(HBLOCK, 2) void k_rollout_fr_h(RolloutArgs a) { rollout_body<true, true>(a); }
 
 // ------------------------------------------------------------------------------------
 // FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256): one wave per game
@@ -2541,7 +2568,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
 }
 
 __global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
-__global__ __launch_bounds__(HBLOCK, 3) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
+__global__ __launch_bounds__(HBLOCK, 2) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
 
 // ------------------------------------------------------------------------------------
 // C ABI
@@ -2790,7 +2817,8 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
 static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_t* root_index,
                            int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
                            bk_result* out, bk_state* out_states, int mem, const bk_fset* root_sets = nullptr,
-                           bk_fset* out_sets = nullptr) {
+                           bk_fset* out_sets = nullptr, const uint8_t* seat_masks = nullptr,
+                           uint32_t* rng_io = nullptr) {
     if (!h || !roots || !cfg || n_roots <= 0 || n_playouts < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
         return set_err(h, BK_EINVAL, "bk_rollout: invalid arguments%s", "");
     if (cfg->semantics != BK_SEM_ARENA && cfg->semantics != BK_SEM_ROLLOUT && cfg->semantics != BK_SEM_ADVANCE)
@@ -2807,7 +2835,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         return set_err(h, BK_EINVAL, "bk_rollout_frontier: out_sets goes with out_states%s", "");
     if (cfg->rng != BK_RNG_PHILOX && cfg->rng != BK_RNG_NUMPY_MT)
         return set_err(h, BK_EINVAL, "bk_rollout: unknown rng%s", "");
-    if (cfg->rng == BK_RNG_NUMPY_MT && !compat_seeds)
+    if (cfg->rng == BK_RNG_NUMPY_MT && !compat_seeds && !rng_io)
         return set_err(h, BK_EINVAL, "bk_rollout: compat rng needs compat_seeds%s", "");
     if (cfg->max_plies <= 0) return set_err(h, BK_EINVAL, "bk_rollout: max_plies must be > 0%s", "");
     if ((cfg->heuristic_seats & ~0xF) || (cfg->heuristic_seats && !fr))
@@ -2825,7 +2853,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         rc = stage_in(h, root_index, sizeof(int32_t) * (size_t)n_playouts, mem, &d_idx, &h->d_aux, &h->d_aux_cap);
         if (rc) return rc;
     }
-    if (cfg->rng == BK_RNG_NUMPY_MT) {
+    if (cfg->rng == BK_RNG_NUMPY_MT && compat_seeds) {  // (bk_arena_advance carries cursors instead)
         rc = stage_in(h, compat_seeds, sizeof(uint32_t) * 4 * (size_t)n_playouts, mem, &d_seeds, &h->d_aux2,
                       &h->d_aux2_cap);
         if (rc) return rc;
@@ -2833,6 +2861,13 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     void* d_rsets = nullptr;
     if (fr) {
         rc = stage_in(h, root_sets, sizeof(bk_fset) * (size_t)n_roots, mem, &d_rsets, &h->d_fin, &h->d_fin_cap);
+        if (rc) return rc;
+    }
+    void *d_masks = nullptr, *d_rng = nullptr;
+    if (seat_masks) {  // bk_arena_advance
+        rc = stage_in(h, seat_masks, (size_t)n_playouts, mem, &d_masks, &h->d_aux, &h->d_aux_cap);
+        if (rc) return rc;
+        rc = stage_in(h, rng_io, sizeof(uint32_t) * 16 * (size_t)n_playouts, mem, &d_rng, &h->d_aux2, &h->d_aux2_cap);
         if (rc) return rc;
     }
     bk_result* d_out = out;
@@ -2852,7 +2887,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         }
     }
     // persistent grid: every resident slot pulls playouts from the counter
-    const bool heur = fr && (cfg->heuristic_seats & 0xF) != 0;
+    const bool heur = fr && ((cfg->heuristic_seats & 0xF) != 0 || seat_masks != nullptr);
     const int blk = heur ? HBLOCK : BLOCK;
     int blocks = h->num_cu * (heur ? 3 : fr ? 2 : h->rollout_blocks_per_cu);
     const int need = (n_playouts + blk - 1) / blk;
@@ -2873,7 +2908,8 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     RolloutArgs a{(const bk_state*)d_roots, n_roots, (const int32_t*)d_idx, n_playouts, *cfg,
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
-                  (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr};
+                  (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr,
+                  (const uint8_t*)d_masks, (uint32_t*)d_rng};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (heur)
         hipLaunchKernelGGL(k_rollout_fr_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
@@ -2894,6 +2930,9 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                                      hipMemcpyDeviceToHost, h->cur));
         if (out_sets)
             HIPCHK(h, hipMemcpyAsync(out_sets, d_osets, sizeof(bk_fset) * (size_t)n_playouts,
+                                     hipMemcpyDeviceToHost, h->cur));
+        if (rng_io)
+            HIPCHK(h, hipMemcpyAsync(rng_io, d_rng, sizeof(uint32_t) * 16 * (size_t)n_playouts,
                                      hipMemcpyDeviceToHost, h->cur));
         uint32_t ctr[4];
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
@@ -2916,6 +2955,29 @@ int bk_advance(bk_handle h, const bk_state* roots, int32_t n_roots, const int32_
     if (!out_states || !cfg || cfg->semantics != BK_SEM_ADVANCE)
         return set_err(h, BK_EINVAL, "bk_advance: needs out_states and BK_SEM_ADVANCE%s", "");
     return launch_playouts(h, roots, n_roots, root_index, n_playouts, cfg, compat_seeds, nullptr, out_states, mem);
+}
+
+int bk_mt_cursor_init(uint32_t seed, uint32_t* out4) {
+    if (!out4) return BK_EINVAL;
+    uint32_t x = seed, b = 0;
+    for (uint32_t j = 1; j <= 397; ++j) {
+        x = 1812433253u * (x ^ (x >> 30)) + j;
+        if (j == 1) b = x;
+    }
+    out4[0] = 0; out4[1] = seed; out4[2] = b; out4[3] = x;
+    return BK_OK;
+}
+
+int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const bk_rollout_cfg* cfg,
+                     const uint8_t* seat_masks, uint32_t* rng_state, bk_result* out, int mem) {
+    if (!h || !states || !sets || !cfg || !seat_masks || !rng_state || !out || n < 0)
+        return set_err(h, BK_EINVAL, "bk_arena_advance: invalid arguments%s", "");
+    if (cfg->semantics != BK_SEM_ARENA || cfg->order != BK_ORDER_FRONTIER || cfg->rng != BK_RNG_NUMPY_MT ||
+        cfg->seats_share_stream)
+        return set_err(h, BK_EINVAL, "bk_arena_advance: needs ARENA, FRONTIER order, NUMPY_MT per-seat streams%s", "");
+    if (n == 0) return BK_OK;
+    return launch_playouts(h, states, n, nullptr, n, cfg, nullptr, out, states, mem, sets, sets, seat_masks,
+                           rng_state);
 }
 
 int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_sets, int32_t n_roots,

@@ -202,6 +202,26 @@ class BlokusGPU:
                                      N.MEM_HOST)
         return res
 
+    # ------------------------------------------------------------------ arena with search seats
+    def arena_advance(self, states, sets, seat_masks, rng_state, *, max_turns: int = 2500):
+        """bk_arena_advance on host arrays, in place: states (STATE_DTYPE[n]), sets
+        (FSET_DTYPE[n]), rng_state uint32[n, 16]; seat_masks uint8[n] (bits 0-3 heuristic
+        seats, 4-7 stop seats).  Returns RESULT_DTYPE[n]."""
+        n = len(states)
+        assert states.dtype == STATE_DTYPE and sets.dtype == N.FSET_DTYPE and len(sets) == n
+        assert states.flags.c_contiguous and sets.flags.c_contiguous
+        masks = np.ascontiguousarray(seat_masks, dtype=np.uint8)
+        assert masks.shape == (n,) and rng_state.dtype == np.uint32 and rng_state.shape == (n, 16)
+        assert rng_state.flags.c_contiguous
+        cfg = N.BkRolloutCfg(N.SEM_ARENA, N.ORDER_FRONTIER, N.RNG_NUMPY_MT, int(max_turns), 0, 0, 0)
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+        if n == 0:
+            return out
+        self.handle.set_stream(None)
+        self.handle.arena_advance(states.ctypes.data, sets.ctypes.data, n, cfg, masks.ctypes.data,
+                                  rng_state.ctypes.data, out.ctypes.data, N.MEM_HOST)
+        return out
+
     # ------------------------------------------------------------------ positions
     def advance(self, roots, n: int, plies: int, *, seed: int = 0, root_index=None):
         """Play `plies` uniformly random moves (naive order, Philox stream) from each root

@@ -195,27 +195,35 @@ class MCTSAgent:
         reference's select_action (mcts/mcts_agent.py:304-341) does.  Positions with
         < 2 legal moves are answered without a search (:313-318); ``legal_moves[i]`` is
         the caller's legal list for position i (generated here when omitted)."""
+        assert len(agents) == len(boards) == len(players)
+        gen = get_shared_generator()
+        legal = [legal_moves[i] if legal_moves is not None else gen.get_legal_moves(b, p)
+                 for i, (b, p) in enumerate(zip(boards, players))]
+        todo = [i for i in range(len(agents)) if len(legal[i]) > 1]
+        out: List[Optional[Move]] = [lm[0] if len(lm) == 1 else None for lm in legal]
+        if todo:
+            roots = np.concatenate([pack_state(boards[i]) for i in todo])
+            sets = np.concatenate([boards[i].frontier_tables for i in todo])
+            moves = MCTSAgent.search_packed([agents[i] for i in todo], roots, sets,
+                                            [players[i].value - 1 for i in todo])
+            for i, mv in zip(todo, moves):
+                out[i] = int_to_move(mv) if mv is not None else None
+        return out
+
+    @staticmethod
+    def search_packed(agents: List["MCTSAgent"], roots: np.ndarray, sets: np.ndarray, players) -> List[Optional[int]]:
+        """The searches of search_batch on packed positions (STATE_DTYPE roots, their
+        FSET_DTYPE frontier tables, players 0..3), each with >= 2 legal moves; one
+        bk_mcts launch per parameter group.  Returns move ints (g * 400 + cell)."""
         from .. import _native as N
         from ..gpu import BlokusGPU, MctsTT
         from .zobrist import flat_keys, hash_states
-        assert len(agents) == len(boards) == len(players)
         assert len({id(a) for a in agents}) == len(agents), "one search per agent per launch"
-        out: List[Optional[Move]] = [None] * len(agents)
-        todo = []
-        gen = get_shared_generator()
-        for i, (a, b, p) in enumerate(zip(agents, boards, players)):
+        out: List[Optional[int]] = [None] * len(agents)
+        groups = {}  # agents sharing (iterations, rollout cap, c, TT on/off, time limit) share a launch
+        for i, a in enumerate(agents):
             if a.rollout_backend != "search":
                 raise ValueError("search_batch needs rollout_backend='search' agents")
-            legal = legal_moves[i] if legal_moves is not None else gen.get_legal_moves(b, p)
-            if len(legal) <= 1:
-                out[i] = legal[0] if legal else None
-            else:
-                todo.append(i)
-        if not todo:
-            return out
-        groups = {}  # agents sharing (iterations, rollout cap, c, TT on/off, time limit) share a launch
-        for i in todo:
-            a = agents[i]
             # time_limit (seconds, mcts_agent.py:325-333): iterate until it runs out; the
             # kernel stops each search at the first iteration boundary past it, with the
             # iteration count bounded by `iterations` (the node pool / log table size)
@@ -229,15 +237,16 @@ class MCTSAgent:
         for (iters, max_roll, c, use_tt, tl_us, policy), idx in groups.items():
             ags = [agents[i] for i in idx]
             gpu = ags[0]._gpu = ags[0]._gpu or BlokusGPU(ags[0].device)
-            roots = np.concatenate([pack_state(boards[i]) for i in idx])
-            sets = np.concatenate([boards[i].frontier_tables for i in idx])
-            pl = np.array([players[i].value - 1 for i in idx], np.uint8)
+            rts = np.ascontiguousarray(roots[idx])
+            sts = np.ascontiguousarray(sets[idx])
+            pl = np.array([players[i] for i in idx], np.uint8)
+            rts["current_player"] = pl
             tabs, zidx = [], []
             for a in ags:
                 tabs.append(flat_keys(a.zobrist_hash))
                 zidx.append(len(tabs) - 1)
             zob = np.stack(tabs)
-            rh = np.array([hash_states(roots[j:j + 1], zob[j])[0] for j in range(len(idx))], np.uint64)
+            rh = np.array([hash_states(rts[j:j + 1], zob[j])[0] for j in range(len(idx))], np.uint64)
             mt = np.zeros((len(idx), 625), np.uint32)
             rng_states = [a.rollout_agent.rng.get_state() for a in ags]
             for j, st in enumerate(rng_states):
@@ -250,7 +259,7 @@ class MCTSAgent:
                     if a._gpu_tt is not None and a._gpu_tt.count[0]:
                         tt.load(j, *a._gpu_tt.items(0))
             t0 = time.time()
-            r = gpu.mcts(roots, sets, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
+            r = gpu.mcts(rts, sts, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
                          mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us,
                          rollout_policy=policy)
             dt = time.time() - t0
@@ -274,7 +283,7 @@ class MCTSAgent:
                     if t.gpu_size > 500000:  # mcts_agent.py:338-339
                         t.clear()
                         a._gpu_tt = None
-                out[i] = int_to_move(int(o["best_move"])) if o["best_move"] >= 0 else None
+                out[i] = int(o["best_move"]) if o["best_move"] >= 0 else None
         return out
 
     def _get_move_positions(self, move: Move) -> List[Position]:

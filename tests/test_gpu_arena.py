@@ -76,3 +76,77 @@ def test_host_loop_single_game_matches_reference():
                           agent_configs={a.name: a for a in cfg.agents})
     for k in FIELDS:
         assert got[k] == ref[k], k
+
+
+RECORD_FIELDS = ("seat_assignment", "winner_ids", "winner_agents", "is_tie", "final_scores", "final_ranks",
+                 "moves_made", "turn_count", "passes", "invalid_actions", "truncated")
+
+
+def test_batched_mixed_arena_matches_reference_records():
+    """Config-4 path: Random / Heuristic / MCTS (default heuristic rollouts) / FastMCTS
+    seats in lockstep batches (bk_arena_advance + one bk_mcts and one bk_fastmcts launch
+    per round) reproduce the reference's run_single_game records
+    (tests/golden/heuristic.json "arena", arena_runner.py:578-777)."""
+    from reinforcementlearning_blokus_amd.arena.runner import run_games_batched
+    h = load_golden("heuristic.json")
+    cfg = RunConfig.from_dict(h["arena_config"])
+    recs = run_games_batched(cfg, [r["game_index"] for r in h["arena"]])
+    for got, ref in zip(recs, h["arena"]):
+        for k in ("seat_assignment", "winner_ids", "final_scores", "moves_made", "turn_count", "passes",
+                  "invalid_actions", "is_tie"):
+            assert got[k] == ref[k], (ref["game_index"], k)
+
+
+def test_batched_all_random_matches_reference_records():
+    from reinforcementlearning_blokus_amd.arena.runner import run_games_batched
+    fx = load_golden("arena_runs.json")
+    cfg = RunConfig.from_dict(fx["config"])
+    recs = run_games_batched(cfg, range(cfg.num_games))
+    for got, ref in zip(recs, fx["games"]):
+        for k in FIELDS:
+            assert got[k] == ref[k], (ref["game_index"], k)
+
+
+def test_batched_equals_host_loop_randomized_seats():
+    """16 randomized-seat mixed games (two MCTS configurations, FastMCTS, heuristic,
+    random): the batched driver's records equal the host game loop's (run_single_game,
+    the reference loop over the GPU-backed engine), game by game."""
+    from reinforcementlearning_blokus_amd.arena.config import game_seed_from_run_seed, seat_assignment_for_game
+    from reinforcementlearning_blokus_amd.arena.runner import run_games_batched, run_single_game
+    cfg = RunConfig.from_dict({
+        "agents": [{"name": "r", "type": "random"}, {"name": "h", "type": "heuristic"},
+                   {"name": "m", "type": "mcts", "params": {"iterations": 6, "max_rollout_moves": 3}},
+                   {"name": "f", "type": "fast_mcts", "params": {"time_limit": 0.005}}],
+        "num_games": 16, "seed": 99173, "seat_policy": "randomized"})
+    batched = run_games_batched(cfg, range(16))
+    agents = {a.name: a for a in cfg.agents}
+    for gi, got in enumerate(batched):
+        gs = game_seed_from_run_seed(cfg.seed, gi)
+        seats = seat_assignment_for_game(cfg.agent_names, gi, gs, cfg.seat_policy)
+        ref = run_single_game(run_id="h", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                              agent_configs=agents)
+        assert ref["error"] is None, ref["error"]
+        for k in RECORD_FIELDS:
+            assert got[k] == ref[k], (gi, k)
+
+
+def test_batched_cap_at_max_turns():
+    """max_turns reached in the middle of a batched mixed game: truncated records equal
+    the host loop's."""
+    from reinforcementlearning_blokus_amd.arena.config import game_seed_from_run_seed, seat_assignment_for_game
+    from reinforcementlearning_blokus_amd.arena.runner import run_games_batched, run_single_game
+    cfg = RunConfig.from_dict({
+        "agents": [{"name": "r", "type": "random"}, {"name": "h", "type": "heuristic"},
+                   {"name": "m", "type": "mcts", "params": {"iterations": 4, "max_rollout_moves": 2}},
+                   {"name": "f", "type": "fast_mcts", "params": {"time_limit": 0.002}}],
+        "num_games": 4, "seed": 5151, "seat_policy": "round_robin", "max_turns": 37})
+    batched = run_games_batched(cfg, range(4))
+    agents = {a.name: a for a in cfg.agents}
+    for gi, got in enumerate(batched):
+        gs = game_seed_from_run_seed(cfg.seed, gi)
+        seats = seat_assignment_for_game(cfg.agent_names, gi, gs, cfg.seat_policy)
+        ref = run_single_game(run_id="h", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                              agent_configs=agents)
+        assert got["truncated"] and ref["truncated"]
+        for k in RECORD_FIELDS:
+            assert got[k] == ref[k], (gi, k)

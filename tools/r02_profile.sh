@@ -16,6 +16,7 @@ ARGS[config3]="--steps 5 --warmup 1 --no-cpu-baseline"
 ARGS[config2]="--workload config2 --steps 50 --warmup 2 --no-cpu-baseline"
 ARGS[config5]="--workload config5 --iterations 256 --chunk 64 --steps 1 --warmup 0 --no-cpu-baseline"
 for W in config3 config2 config5; do
+  mkdir -p $OUT/$W
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$W/trace -o run --output-format csv -- python3 $R/bench.py ${ARGS[$W]} > $OUT/$W/trace.log 2>&1; step $? "trace $W"
   i=0
   for counters in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS"; do
