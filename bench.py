@@ -59,8 +59,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 20; config5: 1)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; config5: 1, "
                                                               "a 64-iteration chunk)")
-    ap.add_argument("--workload", choices=("config3", "config5", "config2"), default="config3")
-    ap.add_argument("--games", type=int, default=None, help="config3: 256; config5: 65536 (whole job)")
+    ap.add_argument("--workload", choices=("config3", "config5", "config2", "config4"), default="config3")
+    ap.add_argument("--games", type=int, default=None, help="config3: 256; config5: 65536; config4: 8192 (whole job)")
     ap.add_argument("--rollouts", type=int, default=1024)
     ap.add_argument("--iterations", type=int, default=4096, help="config5 MCTS iterations per search")
     ap.add_argument("--chunk", type=int, default=512, help="config5 iterations per launch")
@@ -75,9 +75,9 @@ def parse():
                          "(CPython set tables carried per game)")
     a = ap.parse_args()
     if a.steps is None:
-        a.steps = 1 if a.workload == "config5" else (200 if a.workload == "config2" else 20)
+        a.steps = 1 if a.workload in ("config5", "config4") else (200 if a.workload == "config2" else 20)
     if a.warmup is None:
-        a.warmup = 1 if a.workload == "config5" else 3
+        a.warmup = 1 if a.workload in ("config5", "config4") else 3
     return a
 
 
@@ -400,6 +400,69 @@ def cpu_baseline_mcts(roots, sets, batch, seconds):
                       f"or_mcts), {threads} threads (one per usable core), {dt:.1f} s"}
 
 
+# ------------------------------------------------------------------ config 4
+CONFIG4_AGENTS = [
+    {"name": "random", "type": "random"},
+    {"name": "heuristic", "type": "heuristic"},
+    {"name": "mcts", "type": "mcts", "params": {"iterations": 64, "max_rollout_moves": 50}},
+    {"name": "fast_mcts", "type": "fast_mcts", "thinking_time_ms": 50,
+     "params": {"deterministic_time_budget": True, "iterations_per_ms": 20.0}},
+]
+
+
+def run_config4(args, world, rank, local, dist):
+    """Mixed-agent arena (BASELINE.json configs[3]): round-robin seats of RandomAgent,
+    HeuristicAgent, MCTSAgent (default heuristic rollouts, 64 iterations/move) and
+    FastMCTSAgent (1,000 iterations/move), reference-exact records; games sharded over
+    ranks (r mod W), records all-gathered after the timed region."""
+    import torch
+
+    from reinforcementlearning_blokus_amd.arena.config import RunConfig
+    from reinforcementlearning_blokus_amd.arena.runner import run_games_batched
+    from reinforcementlearning_blokus_amd.shard import shard_indices
+
+    total = args.games or 8192
+    cfg = RunConfig.from_dict({"agents": CONFIG4_AGENTS, "num_games": total, "seed": args.seed,
+                               "seat_policy": "round_robin"})
+    mine = shard_indices(total, rank, world).tolist()
+    dev = torch.device("cuda", local)
+    for _ in range(args.warmup):
+        run_games_batched(cfg, mine[:64], device=local)
+    barrier_sync(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        recs = run_games_batched(cfg, mine, device=local)
+    barrier_sync(dist)
+    elapsed = time.perf_counter() - t0
+    from reinforcementlearning_blokus_amd.arena.runner import LAST_BATCH_PROFILE
+    phases = dict(LAST_BATCH_PROFILE)
+    sims = sum(int(r["agent_move_stats"]["mcts"]["total_simulations"] or 0) for r in recs)
+    moves = sum(r["moves_made"] for r in recs)
+    elapsed, (games, all_sims, all_moves) = reduce_max_sum(dist, dev, elapsed,
+                                                           [len(recs) * args.steps, sims * args.steps,
+                                                            moves * args.steps])
+    if dist:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, [(r["game_index"], r["final_scores"]) for r in recs])
+    if rank != 0:
+        return None
+    return {
+        "metric": "arena games/sec (Random/Heuristic/MCTS/FastMCTS round-robin, reference-exact records)",
+        "value": games / elapsed, "unit": "games/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "u32+f64", "data": "synthetic",
+        "config": {"workload": f"config4: {total} arena games, seats {[a['name'] for a in CONFIG4_AGENTS]} "
+                               "round-robin, MCTS 64 iterations/move (heuristic rollouts), FastMCTS 1,000 "
+                               "iterations/move, lockstep batches (bk_arena_advance + bk_mcts + bk_fastmcts)",
+                   "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
+                   "rank0_phase_seconds": phases,
+                   "parallelism": f"dp{world} (games sharded r mod {world})"},
+        "reference_python": {"value": 1.0 / 20.3, "unit": "games/s/core",
+                             "what": "a 4-random-agent game with the reference's default telemetry (20.3 s), "
+                                     "measured in the build container (SURVEY.md 6); MCTS seats are slower"},
+    }
+
+
 # ------------------------------------------------------------------ config 2
 def run_config2(args, world, rank, local, dist):
     import numpy as np
@@ -507,7 +570,8 @@ def cpu_baseline_movegen(st, pl, seconds, value):
 def main():
     args = parse()
     world, rank, local, dist = setup()
-    run = {"config3": run_config3, "config5": run_config5, "config2": run_config2}[args.workload]
+    run = {"config3": run_config3, "config5": run_config5, "config2": run_config2,
+           "config4": run_config4}[args.workload]
     line = run(args, world, rank, local, dist)
     if line is not None:
         print(json.dumps(line), flush=True)

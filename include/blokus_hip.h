@@ -104,8 +104,9 @@ typedef struct bk_result {
     uint8_t winner_mask;        /* bit p: p in GameResult.winner_ids (engine/game.py:216)    */
     uint8_t status;             /* 0 ok; bit0: rng stream overflow (compat mode); bit1:
                                    frontier table overflow; bit2: bad root_index (device path);
-                                   bit4: a HeuristicAgent draw fell within 2^-36 of a
-                                   cumulative-probability boundary (choice not certified); 
+                                   bit4 (informational): a HeuristicAgent draw fell within
+                                   2^-40 of a cumulative-probability boundary (that choice
+                                   is not certified equal to the reference's);             
                                    bit3: ARENA run stopped by the max_plies turn cap before
                                    every player was known to be stuck (passes / turns are
                                    then raw and reserved[0] = passes since the last move)  */
@@ -377,8 +378,9 @@ typedef struct bk_mcts_cfg {
 #define BK_MCTS_EPATH 8u   /* tree deeper than BK_MCTS_MAX_DEPTH */
 #define BK_MCTS_ELOG 16u   /* log_table too short               */
 #define BK_MCTS_EINTERNAL 32u /* consistency check failed        */
-#define BK_MCTS_EUNCERT 64u   /* a HeuristicAgent draw fell within 2^-36 of a probability
-                                 boundary: that choice is not certified exact           */
+#define BK_MCTS_EUNCERT 64u   /* informational (the search goes on): a HeuristicAgent draw
+                                 fell within 2^-40 of a probability boundary, so that
+                                 choice is not certified equal to the reference's        */
 #define BK_MCTS_MAX_DEPTH 63
 typedef struct bk_mcts_out {
     int32_t best_move;       /* g*400+cell of the most visited root child (first on ties), -1 */

@@ -264,6 +264,53 @@ class FastMCTSAgent:
                     moves[k] = legal[int(res["best_index"])] if int(res["n_children"]) > 0 else legal[0]
         return moves
 
+    @staticmethod
+    def think_arrays(agents: Sequence["FastMCTSAgent"], legal_arrays, iterations: Sequence[int]) -> List[int]:
+        """think_many on legal lists given as arrays: legal_arrays[k] = (g, r, c) int arrays
+        in the reference's list order (order_moves), no Move objects.  For callers whose
+        agents never see one (player, move_count) twice (one agent per game, as in the
+        arena), where the reference's cached legal list is always the current one.
+        Returns the index of each agent's move in its list (-1: no legal move)."""
+        from ..engine.pieces import ORIENT_LIST
+        pid_of = np.array([p for p, _ in ORIENT_LIST], dtype=np.int64)
+        out = [-1] * len(agents)
+        todo, bases = [], []
+        for k, (g, r, c) in enumerate(legal_arrays):
+            n = len(g)
+            if n == 1:
+                out[k] = 0
+            elif n > 1:
+                if n > _MAX_CHILDREN:
+                    raise ValueError(f"{n} legal moves exceed the kernel's {_MAX_CHILDREN}")
+                todo.append(k)
+                # _quick_move_evaluation (:283-296): stable sort by piece id desc, top 3,
+                # stable sort by centre distance
+                top = np.argsort(-pid_of[g], kind="stable")[:3]
+                dist = [abs(int(r[j]) - 9.5) + abs(int(c[j]) - 9.5) for j in top]
+                q = int(top[min(range(len(top)), key=lambda t: dist[t])])
+                reward = int(pid_of[g[q]]) * 0.1
+                reward += (20 - (abs(int(r[q]) - 9.5) + abs(int(c[q]) - 9.5))) * 0.05
+                bases.append(reward)
+        groups: Dict[float, List[int]] = {}
+        for k in todo:
+            groups.setdefault(float(agents[k].exploration_constant), []).append(k)
+        base_of = dict(zip(todo, bases))
+        for ce, ks in groups.items():
+            mt = np.stack([agents[k]._rng_words() for k in ks])
+            counts = [max(1, int(iterations[k])) for k in ks]
+            res = agents[ks[0]]._engine().fastmcts([len(legal_arrays[k][0]) for k in ks], counts,
+                                                   [base_of[k] for k in ks], mt, _log_table(max(counts) + 1), ce)
+            for j, k in enumerate(ks):
+                agents[k]._set_rng_words(mt[j])
+                g, r, c = legal_arrays[k]
+                if int(res[j]["iterations"]) < 5:  # _quick_heuristic_selection
+                    top = np.argsort(-pid_of[g], kind="stable")[:3]
+                    dist = [abs(int(r[t]) - 9.5) + abs(int(c[t]) - 9.5) for t in top]
+                    out[k] = int(top[min(range(len(top)), key=lambda t: dist[t])])
+                else:
+                    out[k] = int(res[j]["best_index"]) if int(res[j]["n_children"]) > 0 else 0
+        return out
+
     def _launch(self, n_legal, counts, bases, mt, want_visits=False, exact_ucb=True):
         # exact_ucb=False: the time budget cut the iteration count (a wall-clock search,
         # not reproducible by the reference either), so do not stall on building pow

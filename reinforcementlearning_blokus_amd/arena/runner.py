@@ -345,6 +345,9 @@ def _batchable(run_config: RunConfig, seats: Mapping[str, str]) -> bool:
     return True
 
 
+LAST_BATCH_PROFILE: Dict[str, float] = {}  # phase times of the last run_games_batched call
+
+
 def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
                       device: int = 0) -> List[Dict[str, Any]]:
     """Mixed seatings (Random / Heuristic / MCTS / FastMCTS, config 4) in lockstep batches:
@@ -397,10 +400,16 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                                  "moves_with_simulations": 0.0, "move_times_ms": []} for name in set(st.values())})
     results: List[Optional[Dict[str, Any]]] = [None] * n
     active = np.arange(n)
+    prof = LAST_BATCH_PROFILE
+    prof.clear()
+    prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0)
     while len(active):
+        prof["rounds"] += 1
+        ta = time.perf_counter()
         sub_st, sub_fs, sub_rng = states[active].copy(), sets[active].copy(), rng[active].copy()
         before = sub_st["reserved"].copy()
         res = gpu.arena_advance(sub_st, sub_fs, masks[active], sub_rng, max_turns=run_config.max_turns)
+        prof["advance_s"] += time.perf_counter() - ta
         states[active], sets[active], rng[active] = sub_st, sub_fs, sub_rng
         stopped = []
         for j, i in enumerate(active):
@@ -408,7 +417,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
             if int(r["status"]) & N.STATUS_STOP:
                 stopped.append(i)
                 continue
-            if int(r["status"]) & ~(N.STATUS_CAP | N.STATUS_STOP):
+            if int(r["status"]) & ~(N.STATUS_CAP | N.STATUS_STOP | N.STATUS_UNCERT):
                 raise RuntimeError(f"game {idx[i]}: kernel status {int(r['status'])}")
             turns = int(before[j, 0]) + int(r["turns"])
             passes = int(before[j, 1]) + int(r["passes"])
@@ -423,16 +432,22 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
         if stopped:
             stopped = np.array(stopped)
             pl = (states["current_player"][stopped] & 3).astype(np.uint8)
-            _, rows = gpu.movegen(states[stopped], pl)
+            cnt, rows = gpu.movegen(states[stopped], pl)
             chosen: Dict[int, Optional[int]] = {}
             by_kind: Dict[str, List[Tuple[int, Any, int, list]]] = {"mcts": [], "fast": []}
             for k, i in enumerate(stopped):
                 p = int(pl[k])
                 adapter = agents[i][seats[i][str(p + 1)]]
-                fr = [divmod(c, 20) for c in N.fset_list(sets[i:i + 1], p)]
-                g, rr, cc = order_moves(rows[k], fr)
-                legal = [int(a) * 400 + int(b) * 20 + int(c) for a, b, c in zip(g, rr, cc)]
                 kind = "mcts" if isinstance(getattr(adapter, "agent", None), MCTSAgent) else "fast"
+                if kind == "mcts":  # the search needs the count only (and the move if it is the only one)
+                    if int(cnt[k]) == 1:
+                        g, rr, cc = order_moves(rows[k], None)
+                        legal = [int(g[0]) * 400 + int(rr[0]) * 20 + int(cc[0])]
+                    else:
+                        legal = [None] * int(cnt[k])
+                else:  # FastMCTS: the reference's list order (frontier sets)
+                    fr = [divmod(c, 20) for c in N.fset_list(sets[i:i + 1], p)]
+                    legal = order_moves(rows[k], fr)
                 by_kind[kind].append((i, adapter, p, legal))
             if by_kind["mcts"]:
                 todo = [(i, a, p, lg) for i, a, p, lg in by_kind["mcts"] if len(lg) > 1]
@@ -441,15 +456,16 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                         chosen[i] = lg[0]
                 if todo:
                     ti = np.array([t[0] for t in todo])
+                    tm = time.perf_counter()
                     mv = MCTSAgent.search_packed([t[1].agent for t in todo], states[ti], sets[ti], [t[2] for t in todo])
+                    prof["mcts_s"] += time.perf_counter() - tm
                     for (i, a, p, lg), m in zip(todo, mv):
                         chosen[i] = m
                         e = per_agent[i][seats[i][str(p + 1)]]
                         e["total_simulations"] += a.agent.stats["iterations_run"]
                         e["moves_with_simulations"] += 1
             if by_kind["fast"]:
-                from ..engine.move_generator import int_to_move, move_to_int
-                ags, players, lists, mcs, iters = [], [], [], [], []
+                ags, lists, iters = [], [], []
                 for i, a, p, lg in by_kind["fast"]:
                     fa = a.agent if isinstance(a, _FastMCTSAdapter) else a.agent._agent
                     budget = (int(cfgs[seats[i][str(p + 1)]].thinking_time_ms or max(int(fa.time_limit * 1000), 1))
@@ -458,15 +474,16 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                     if not a.deterministic_time_budget:
                         raise ValueError("run_games_batched: FastMCTS seats need deterministic_time_budget")
                     ags.append(fa)
-                    players.append(Player(p + 1))
-                    lists.append([int_to_move(x) for x in lg])
-                    mcs.append(int(states["move_count"][i]))
+                    lists.append(lg)
                     iters.append(max(1, int(round(a.iterations_per_ms * budget))))
-                mv = FastMCTSAgent.think_many(ags, players, lists, mcs, iters)
-                for (i, a, p, lg), m, it in zip(by_kind["fast"], mv, iters):
-                    chosen[i] = move_to_int(m) if m is not None else None
+                tf = time.perf_counter()
+                picks = FastMCTSAgent.think_arrays(ags, lists, iters)
+                prof["fast_s"] += time.perf_counter() - tf
+                for (i, a, p, lg), j, it in zip(by_kind["fast"], picks, iters):
+                    g, rr, cc = lg
+                    chosen[i] = int(g[j]) * 400 + int(rr[j]) * 20 + int(cc[j]) if j >= 0 else None
                     e = per_agent[i][seats[i][str(p + 1)]]
-                    if len(lg) > 1:
+                    if len(g) > 1:
                         e["total_simulations"] += it
                         e["moves_with_simulations"] += 1
             for i in stopped:  # place the search moves (Board.place_piece, engine/board.py:515-555)
@@ -488,6 +505,8 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                 N.fset_place(sets[i:i + 1], states[i:i + 1], p, cells)
         active = np.array([i for i in active if results[i] is None], dtype=np.int64)
     dt = time.perf_counter() - t0
+    prof["total_s"] = dt
+    prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"]
     out = []
     for i, gi in enumerate(idx):
         r, turns, passes, truncated = results[i]

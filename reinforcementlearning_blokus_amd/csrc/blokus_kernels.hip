@@ -600,13 +600,34 @@ __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&ow
         }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
-    const int lane = threadIdx.x & (WAVE - 1);
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
+// Dense rows of the class's table entries i0 <= i < i1 with i % G == grp (k_movegen_g)
+template <int H, int... T, typename F>
+__device__ __forceinline__ void rows_class_group(int i0, int i1, int grp, int G, const Planes& P, F&& f) {
+    int first = i0 + ((grp - i0 % G) + G) % G;
+#pragma unroll 1
+    for (int i = first; i < i1; i += G) {
+        const uint32_t w0 = kClass[i][0], w1 = kClass[i][1];
+        uint32_t ok[20];
+#pragma unroll
+        for (int r = 0; r < 20; ++r) ok[r] = 0u;
+        StencilClass<H, T...>::scan(P, w1, [&](int r, uint32_t v) { ok[r] = v; });
+        f((int)(w0 >> 8), w0 & 0xFFu, ok);
+    }
+}
+
+// Batched movegen with the 91 orientations of each board-player split over MG_GROUPS
+// wave-uniform groups (every MG_GROUPS-th stencil-table entry): block b = one 64-lane
+// wave for board-players 64 * (b / MG_GROUPS) .. + 63 and group b % MG_GROUPS, so 4,096
+// board-players run as 1,024 waves instead of 64 (config 2 fills the chip).  Counts are
+// summed with one atomicAdd per (board-player, group) into the zeroed out_count.
+#define MG_GROUPS 16
+__global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
+    const int grp = blockIdx.x % MG_GROUPS;
+    const int i = (blockIdx.x / MG_GROUPS) * WAVE + threadIdx.x;
     const bool live = i < a.n;
     const int idx = live ? i : 0;
     const bk_state* s = a.states + idx;
-    const int p = a.players ? (a.players[idx] & 3) : 0;
+    const int p = a.players[idx] & 3;
     uint32_t own[20], occ[20];
 #pragma unroll
     for (int R = 0; R < 20; ++R) { occ[R] = 0; own[R] = 0; }
@@ -622,15 +643,11 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
     derive_rows(own, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
     make_pairs(P);
     const uint32_t avail = live ? (~s->used[p] & 0x1FFFFFu) : 0u;
-    if (a.out_rows == nullptr) {
-        const uint32_t total = movegen_counts<false>(P, avail, nullptr, lane);
-        if (live && a.out_count) a.out_count[i] = total;
-        return;
-    }
     uint32_t total = 0;
     auto emit = [&](int g, uint32_t piece, const uint32_t (&ok)[20]) {
         const bool av = (avail >> (piece - 1u)) & 1u;
-        uint4* dst = reinterpret_cast<uint4*>(a.out_rows + ((size_t)idx * BK_NUM_ORIENTS + g) * 20);
+        uint4* dst = a.out_rows ? reinterpret_cast<uint4*>(a.out_rows + ((size_t)idx * BK_NUM_ORIENTS + g) * 20)
+                                : nullptr;
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
             uint4 v;
@@ -640,11 +657,13 @@ __global__ __launch_bounds__(BLOCK) void k_movegen(MovegenArgs a) {
             v.w = av ? ok[4 * q + 3] : 0u;
             total += __builtin_popcount(v.x) + __builtin_popcount(v.y) + __builtin_popcount(v.z) +
                      __builtin_popcount(v.w);
-            if (live) dst[q] = v;
+            if (live && dst) dst[q] = v;
         }
     };
-    all_rows(P, emit);
-    if (live && a.out_count) a.out_count[i] = total;
+#define BK_ROWS_GROUP(i0, i1, H, ...) rows_class_group<H, __VA_ARGS__>(i0, i1, grp, MG_GROUPS, P, emit);
+    BK_CLASS_LIST(BK_ROWS_GROUP)
+#undef BK_ROWS_GROUP
+    if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
@@ -652,21 +671,22 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     const bool live = i < a.n;
     const bk_state* s = a.states + (live ? i : 0);
-    uint32_t own[4][20], occ[20];
-    load_state_rows(s, own, occ);
+    uint32_t occ[20];
+#pragma unroll
+    for (int R = 0; R < 20; ++R) occ[R] = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int R = 0; R < 20; ++R) occ[R] |= plane_row(s->planes[q], R);
     uint8_t mask = 0;
 #pragma unroll 1
     for (int p = 0; p < 4; ++p) {
+        // the mover's rows re-read from the state (L1/L2) each time: a [4][20] register
+        // array indexed by the runtime player would be demoted to scratch memory
         uint32_t ow[20];
         Planes P;
 #pragma unroll
-        for (int R = 0; R < 20; ++R) {
-            uint32_t v = own[0][R];
-            v = p == 1 ? own[1][R] : v;
-            v = p == 2 ? own[2][R] : v;
-            v = p == 3 ? own[3][R] : v;
-            ow[R] = v;
-        }
+        for (int R = 0; R < 20; ++R) ow[R] = plane_row(s->planes[p], R);
         derive_rows(ow, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
         make_pairs(P);
         const uint32_t total = movegen_counts<false>(P, live ? (~s->used[p] & 0x1FFFFFu) : 0u, nullptr, lane);
@@ -791,8 +811,10 @@ __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool a
 __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) { return fs_op(t, tmp, k, true); }
 __host__ __device__ inline void fs_discard(FsetRef t, int16_t k) { fs_op(t, nullptr, k, false); }
 
+// an empty table of 8 slots (set_clear / make_new_set).  Slots beyond mask are never
+// read (every walk stops at mask; growing a table clears its new slots first)
 __host__ __device__ inline void fs_clear(FsetRef t) {
-    for (uint32_t i = 0; i < t.cap; ++i) t.at(i) = FS_UNUSED;
+    for (uint32_t i = 0; i < 8; ++i) t.at(i) = FS_UNUSED;
     *t.mask = 7;
     *t.fill = 0;
     *t.used = 0;
@@ -850,6 +872,7 @@ __host__ __device__ inline bool fs_copy(FsetRef d, const int16_t* skey, uint32_t
         uint32_t newsize = 8;
         while (newsize <= sused * 2) newsize <<= 1;
         if (newsize > d.cap) return false;
+        for (uint32_t i = 8; i < newsize; ++i) d.at(i) = FS_UNUSED;
         *d.mask = (uint16_t)(newsize - 1);
     }
     if (*d.mask == smask && sfill == sused) {
@@ -955,12 +978,13 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 // ~1e-13 of the exact value, and so is the reference's.  The kernel takes the first move
 // whose cumulative e exceeds u * total and verifies that u * total lies more than
 // HEUR_MARGIN * total inside that move's interval; then the reference (any host) picks
-// the same index.  A draw closer than that to an interval end sets status bit 4 (never
-// observed; tests require it clear).
+// the same index.  A draw closer than that to an interval end (probability ~1e-9 per draw
+// with ~500 moves) sets status bit 4: the choice is then still the exact-arithmetic one,
+// but the reference's rounding could pick a neighbour.  Informational: nothing stops.
 // ------------------------------------------------------------------------------------
 #define HK_MIN (-10)  // K4 range: 4 n + 8 corners - 6 edge in [-10, 180]
 #define HK_N 191
-#define HEUR_MARGIN 1.4551915228366852e-11  // 2^-36 of the total
+#define HEUR_MARGIN 9.094947017729282e-13  // 2^-40 of the total (error bound ~1e-13)
 #define BK_STATUS_UNCERT 16u
 
 struct HeurShared {           // per block (LDS), built at kernel start
@@ -1308,12 +1332,24 @@ __device__ __forceinline__ void store_state(const RolloutArgs& a, const Game& g,
     o->reserved[1] = a.seat_masks ? g.passes0 + (uint32_t)g.passes : 0u;
 }
 
+// a plain copy of the four tables: slots 0..mask of each (the rest is never read) and
+// the counters, as uint4
 __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
-    static_assert(sizeof(bk_fset) % 16 == 0, "bk_fset is copied as uint4");
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    static_assert(sizeof(bk_fset) % 16 == 0 && BK_FSET_SLOTS % 8 == 0, "bk_fset is copied as uint4");
+    const uint4* tail_s = reinterpret_cast<const uint4*>(&src->mask[0]);
+    uint4* tail_d = reinterpret_cast<uint4*>(&dst->mask[0]);
+    const uint4 t0 = tail_s[0], t1 = tail_s[1];  // mask[4] fill[4] used[4] reserved[4]
+    tail_d[0] = t0;
+    tail_d[1] = t1;
+    const uint32_t masks[4] = {t0.x & 0xFFFFu, t0.x >> 16, t0.y & 0xFFFFu, t0.y >> 16};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint4* s4 = reinterpret_cast<const uint4*>(src->key[q]);
+        uint4* d4 = reinterpret_cast<uint4*>(dst->key[q]);
+        const int nv = (int)(masks[q] + 1u) / 8;  // 8 slots per uint4
 #pragma unroll 2
-    for (int i = 0; i < (int)(sizeof(bk_fset) / 16); ++i) d4[i] = s4[i];
+        for (int i = 0; i < nv; ++i) d4[i] = s4[i];
+    }
 }
 
 template <bool FR>
@@ -1950,6 +1986,7 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts_select(const uint32_t* visits
 // movegen for each busy lane -- the expansion of its selected leaf or one rollout ply --
 // and the divergent tree work (selection, replay, TT, backpropagation) in between.
 // ------------------------------------------------------------------------------------
+#define MC_FATAL(st) ((st) & ~BK_MCTS_EUNCERT)  // status bits that end a search
 #define MC_SELECT 0
 #define MC_EXPAND 1
 #define MC_ROLLOUT 2
@@ -2404,10 +2441,10 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             const bool timed_out = a.cfg.time_limit_us > 0 &&
                                    wall_clock64() - m.t0 >= a.limit_ticks;
             const bool chunk_end = a.cfg.iter_stop > 0 && m.it >= a.cfg.iter_stop;
-            if (m.it >= a.cfg.iterations || chunk_end || timed_out || m.status) { mc_finish_game(a, m); continue; }
+            if (m.it >= a.cfg.iterations || chunk_end || timed_out || MC_FATAL(m.status)) { mc_finish_game(a, m); continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
-            if (m.status) continue;
+            if (MC_FATAL(m.status)) continue;
             mc_replay(a, m, slab, L, htab);
             m.mode = MC_EXPAND;
         }
@@ -2773,9 +2810,10 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
         return set_err(h, BK_EINVAL, "bk_movegen: out_rows must be 16-byte aligned%s", "");
     }
     MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr};
-    const int grid = (n + BLOCK - 1) / BLOCK;
+    if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
+    const int grid = ((n + WAVE - 1) / WAVE) * MG_GROUPS;
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    hipLaunchKernelGGL(k_movegen, dim3(grid), dim3(BLOCK), 0, h->cur, a);
+    hipLaunchKernelGGL(k_movegen_g, dim3(grid), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;

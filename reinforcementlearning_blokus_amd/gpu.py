@@ -348,9 +348,11 @@ class BlokusGPU:
                     tt.restore(tt0)
                 cap = cap * 2 + 1
                 continue
-            if st.any():
+            fatal = st & ~np.uint32(N.MCTS_EUNCERT)
+            if fatal.any():
                 raise RuntimeError(f"bk_mcts: search stopped early, status bits {sorted(set(st[st != 0].tolist()))}")
-            return {"out": out, "rewards": rewards, "hit_flags": flags, "nodes": nodes, "node_cap": cap}
+            return {"out": out, "rewards": rewards, "hit_flags": flags, "nodes": nodes, "node_cap": cap,
+                    "uncertified": int((st & np.uint32(N.MCTS_EUNCERT) != 0).sum())}
 
     def mcts_device(self, roots, root_sets, players, root_hash, zobrist, zobrist_index, mt_state, log_table, nodes,
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
@@ -401,7 +403,7 @@ class BlokusGPU:
                              log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)
             if on_chunk is not None:
                 on_chunk(stop or iterations)
-        st = out.view(torch.int32)[:, 6]
+        st = out.view(torch.int32)[:, 6] & ~N.MCTS_EUNCERT
         bad = int((st != 0).sum().item())
         if bad:
             raise RuntimeError(f"bk_mcts: {bad} searches stopped early, status bits "
