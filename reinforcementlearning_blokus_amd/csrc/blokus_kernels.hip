@@ -1352,6 +1352,46 @@ __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
     }
 }
 
+// fs_copy of table q on the device, as uint4 rows (8 slots each): the same-shape case
+// (set_merge's pointer copy) is a plain uint4 copy, the clean re-insert reads 8 keys per
+// load.  Equal to fs_copy slot for slot.
+__device__ __forceinline__ bool fs_copy_dev(bk_fset* d, int q, const bk_fset* s, const uint64_t* htab) {
+    const uint32_t smask = s->mask[q], sfill = s->fill[q], sused = s->used[q];
+    uint32_t newsize = 8;
+    if (sused * 5 >= 7u * 3u)
+        while (newsize <= sused * 2) newsize <<= 1;
+    uint4* d4 = reinterpret_cast<uint4*>(d->key[q]);
+    const uint4* s4 = reinterpret_cast<const uint4*>(s->key[q]);
+    if (newsize > BK_FSET_SLOTS) {
+        fs_clear(fs_ref(d, q, htab));
+        return false;
+    }
+    d->mask[q] = (uint16_t)(newsize - 1);
+    d->fill[q] = (uint16_t)sused;
+    d->used[q] = (uint16_t)sused;
+    if (newsize - 1 == smask && sfill == sused) {
+#pragma unroll 2
+        for (uint32_t i = 0; i < newsize / 8; ++i) d4[i] = s4[i];
+        return true;
+    }
+    const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);  // FS_UNUSED pairs
+#pragma unroll 2
+    for (uint32_t i = 0; i < newsize / 8; ++i) d4[i] = unused;
+    if (sused == 0) return true;
+    const FsetRef t = fs_ref(d, q, htab);
+#pragma unroll 1
+    for (uint32_t i = 0; i <= smask / 8; ++i) {
+        const uint4 v = s4[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int16_t k = (int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            if (k >= 0) fs_insert_clean(t, newsize - 1, k);
+        }
+    }
+    return true;
+}
+
 template <bool FR>
 __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot) {
     if (a.rng_io) {  // the seats' streams go on in the next call
@@ -1474,8 +1514,7 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
             const bk_fset* src = a.root_sets + ri;
 #pragma unroll 1
             for (int q = 0; q < 4; ++q)
-                if (!fs_copy(fs_ref(d, q, htab), src->key[q], src->mask[q], src->fill[q], src->used[q]))
-                    g.status |= 2u;
+                if (!fs_copy_dev(d, q, src, htab)) g.status |= 2u;
         } else {
             copy_fset(&a.fslab[slot].s, a.root_sets + ri);
         }
@@ -1992,6 +2031,7 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts_select(const uint32_t* visits
 #define MC_ROLLOUT 2
 #define MC_PATH (BK_MCTS_MAX_DEPTH + 1)
 #define MC_ZOB 2088
+#define MC_TREE_BATCH WAVE
 
 struct McLane {          // per-lane scratch record in HBM
     FsLane A;            // node.board tables of the node being worked on
@@ -2025,6 +2065,7 @@ struct MctsArgs {
     uint32_t* counter;  // [0] next game, [1] step guard tripped
     uint64_t max_steps;
     uint64_t limit_ticks;  // cfg.time_limit_us in wall-clock (s_memrealtime) ticks
+    int32_t tree_batch;    // tree phase once this many lanes of a wave wait for it (or no lane is busy)
 };
 
 struct Mc {
@@ -2085,7 +2126,7 @@ __device__ __forceinline__ int mc_score(const Mc& m, int p) {  // Board.get_scor
 __device__ __forceinline__ bool mc_copy_tables(bk_fset* d, const bk_fset* s, const uint64_t* htab) {
     bool ok = true;
 #pragma unroll 1
-    for (int q = 0; q < 4; ++q) ok &= fs_copy(fs_ref(d, q, htab), s->key[q], s->mask[q], s->fill[q], s->used[q]);
+    for (int q = 0; q < 4; ++q) ok &= fs_copy_dev(d, q, s, htab);
     return ok;
 }
 
@@ -2379,18 +2420,25 @@ __device__ __forceinline__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, c
 }
 
 // node.board of path[depth] into the lane (slab rows + table A): root, then per edge
-// new_board = board.copy(); place; MCTSNode(new_board) copies again (mcts_agent.py:113-145)
+// new_board = board.copy(); place; MCTSNode(new_board) copies again (mcts_agent.py:113-145).
+// Every node board is a copy, and a copy of a copy is slot-for-slot the same table
+// (set_merge's same-size path), so the first copy is skipped: place on the node table
+// itself and copy into the other record, alternating A and B.
 __device__ __forceinline__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L, const uint64_t* htab) {
     mc_load_root(a, m, slab, L);
     const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+    FsLane* X = &L->A;
+    FsLane* Y = &L->B;
+    bool ok = true;
     for (int d = 1; d <= m.depth; ++d) {
         int gs, ar, ac;
         mc_move_split(pool[L->path[d]].move, gs, ar, ac);
-        bool ok = mc_copy_tables(&L->B.s, &L->A.s, htab);
-        ok &= mc_place(m, slab, (m.root_player + d - 1) & 3, gs, ar, ac, &L->B, htab);
-        ok &= mc_copy_tables(&L->A.s, &L->B.s, htab);
-        if (!ok) m.status |= BK_MCTS_EFSET;
+        ok &= mc_place(m, slab, (m.root_player + d - 1) & 3, gs, ar, ac, X, htab);
+        ok &= mc_copy_tables(&Y->s, &X->s, htab);
+        FsLane* t = X; X = Y; Y = t;
     }
+    if (X != &L->A) ok &= mc_copy_tables(&L->A.s, &X->s, htab);  // same-shape copy
+    if (!ok) m.status |= BK_MCTS_EFSET;
 }
 
 // numpy RandomState.random_sample() (genrand_res53) from a per-game stream
@@ -2431,8 +2479,14 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     SECT_DECL
     for (uint64_t step = 0;; ++step) {
         SECT(13);
-        // ---- tree work until this lane needs a movegen (divergent)
-        while (!done && m.mode == MC_SELECT) {
+        // ---- tree work until this lane needs a movegen (divergent).  The wave runs it
+        // once a.tree_batch lanes wait for it (or none is mid-simulation): selection,
+        // replay and backpropagation of one lane cost the whole wave about one ply, so
+        // batching them beats letting every finished rollout stall the other 63 lanes.
+        // Lanes play independent searches: the order changes no result.
+        const uint64_t waiting = __ballot(!done && m.mode == MC_SELECT);
+        const bool tree_now = __popcll(waiting) >= a.tree_batch || __ballot(!done && m.mode != MC_SELECT) == 0ull;
+        while (tree_now && !done && m.mode == MC_SELECT) {
             if (m.game < 0) {
                 const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
                 if (next >= a.n_games) { done = true; break; }
@@ -2455,7 +2509,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         }
         SECT(8);
         // ---- one movegen per busy lane (uniform work)
-        const bool idle = done;
+        const bool idle = done || m.mode == MC_SELECT;
         const int p = idle ? 0 : (m.mode == MC_EXPAND ? ((m.root_player + m.depth) & 3) : m.cur);
         Planes P;
         {
@@ -2569,11 +2623,11 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             ch.n_exp = 0; ch.n_legal = 0; ch.flags = 0;
             pool[c] = ch;
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
-            ok = mc_copy_tables(&L->B.s, &L->A.s, htab);
         }
-        ok &= mc_place_staged(m, slab, p, gs, ar, &L->B, htab, pm, cells, A, lk);
+        // expand: new_board = board.copy() is table A itself (A is a copy, see mc_replay)
+        ok &= mc_place_staged(m, slab, p, gs, ar, expand ? &L->A : &L->B, htab, pm, cells, A, lk);
         if (expand) {
-            ok &= mc_copy_tables(&L->A.s, &L->B.s, htab);  // MCTSNode(new_board): board.copy()
+            ok &= mc_copy_tables(&L->B.s, &L->A.s, htab);  // MCTSNode(new_board): board.copy()
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             m.hash = mc_hash_step(Z, m.hash, p, (m.root_cp + m.depth) & 3, gs, ar, ac);
@@ -2584,8 +2638,8 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
                 mc_complete(a, m, L, reward, true);
                 continue;
             }
-            // _rollout (mcts_agent.py:470-554) on sim = node.board.copy()
-            if (!mc_copy_tables(&L->B.s, &L->A.s, htab)) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            // _rollout (mcts_agent.py:470-554) on sim = node.board.copy(): the copy of the
+            // copy in B is B
             m.player = m.cur = (m.root_player + m.depth) & 3;
             m.score0 = mc_score(m, m.player);
             m.plies = 0;
@@ -3355,14 +3409,18 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     if (khz <= 0) khz = 100000;
     HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
     const uint64_t per_lane = ((uint64_t)n_games + nslots - 1) / nslots + 1;
-    const uint64_t steps = per_lane * ((uint64_t)cfg->iterations + 1) * ((uint64_t)cfg->max_rollout_moves + 2) + 64;
+    // a waiting lane waits at most one simulation of the others (2x)
+    const uint64_t steps = 2 * per_lane * ((uint64_t)cfg->iterations + 1) * ((uint64_t)cfg->max_rollout_moves + 2) + 64;
+    int32_t tree_batch = MC_TREE_BATCH;
+    if (const char* env = getenv("BK_TREE_BATCH")) tree_batch = atoi(env);  // tuning override
+    if (tree_batch < 1) tree_batch = 1;
     MctsArgs a{(const bk_state*)sec[0].dev, (const bk_fset*)sec[1].dev, (const uint8_t*)sec[2].dev,
                (const uint64_t*)sec[3].dev, n_games, *cfg, (const uint64_t*)sec[4].dev,
                (const int32_t*)sec[5].dev, (uint32_t*)sec[6].dev, (uint64_t*)sec[7].dev, (double*)sec[8].dev,
                (int32_t*)sec[9].dev, (const double*)sec[10].dev, log_len, (bk_mcts_node*)sec[11].dev,
                (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
-               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u};
+               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (heur)
         hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);

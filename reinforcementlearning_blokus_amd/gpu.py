@@ -357,7 +357,8 @@ class BlokusGPU:
     def mcts_device(self, roots, root_sets, players, root_hash, zobrist, zobrist_index, mt_state, log_table, nodes,
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
                     hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
-                    on_chunk=None, stop_after: int | None = None, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM):
+                    on_chunk=None, stop_after: int | None = None, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM,
+                    resume_from: int | None = None):
         """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
@@ -395,9 +396,12 @@ class BlokusGPU:
         stops = mcts_chunks(iterations, chunk)
         if stop_after is not None and 0 < stop_after < iterations:
             stops = [x for x in stops if 0 < x < stop_after] + [stop_after]
+        if resume_from is not None:  # continue searches a stop_after call left at resume_from
+            stops = [x for x in stops if x == 0 or x > resume_from]
         for j, stop in enumerate(stops):
+            resume = int(j > 0 or resume_from is not None)
             cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
-                              tt_keys.shape[1] if use_tt else 0, 0, stop, int(j > 0), int(rollout_policy), 0)
+                              tt_keys.shape[1] if use_tt else 0, 0, stop, resume, int(rollout_policy), 0)
             self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
                              d(zobrist_index), d(mt_state), d(tt_keys), d(tt_vals), d(tt_count), d(log_table),
                              log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)

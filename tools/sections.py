@@ -26,7 +26,7 @@ def build():
     sys.path.insert(0, ROOT)
     from reinforcementlearning_blokus_amd import build as B
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call([B.hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+    subprocess.check_call([B.hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread",
                            "-DBK_SECTION_PROF", "-Wno-unused-command-line-argument", "-o", LIB, B.SRC])
     print(LIB)
 
@@ -76,5 +76,45 @@ def run():
         read("k_mcts", {"games": games, "iterations": 16, "kernel_ms": gpu.last_kernel_ms()})
 
 
+def run_mcts():
+    """k_mcts sections in the config-5 regime (65,536 searches, deep trees: a warm-up of
+    `iterations` then a measured chunk of 64 more) and k_mcts_h (heuristic rollouts)."""
+    os.environ["BK_LIB_PATH"] = LIB
+    sys.path.insert(0, ROOT)
+    import ctypes as C
+
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    gpu = BlokusGPU(0)
+    L = N.load()
+    buf = (C.c_uint64 * 16)()
+
+    def read(tag, extra):
+        rc = L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
+        assert rc == 0, rc
+        tot = sum(buf)
+        rows = {NAMES.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
+        print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows}), flush=True)
+
+    for games, iters, policy in ((65536, 512, N.MCTS_ROLLOUT_RANDOM), (4096, 96, N.MCTS_ROLLOUT_HEURISTIC)):
+        roots, sets = frontier_roots(gpu, games, 20, seed=11)
+        b = MctsBatch(gpu, roots, sets, iterations=iters, seed0=3)
+        gpu.mcts_device(b.roots, b.sets, b.players, b.root_hash, b.zobrist, b.zidx, b.mt, b.log_table, b.nodes,
+                        b.out, iterations=iters, tt_keys=b.tt_keys, tt_vals=b.tt_vals, tt_count=b.tt_count,
+                        chunk=64, stop_after=iters - 64, rollout_policy=policy)
+        L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
+        gpu.mcts_device(b.roots, b.sets, b.players, b.root_hash, b.zobrist, b.zidx, b.mt, b.log_table, b.nodes,
+                        b.out, iterations=iters, tt_keys=b.tt_keys, tt_vals=b.tt_vals, tt_count=b.tt_count,
+                        chunk=64, resume_from=iters - 64, rollout_policy=policy)
+        read("k_mcts" if policy == N.MCTS_ROLLOUT_RANDOM else "k_mcts_h",
+             {"games": games, "iterations": f"{iters - 64}..{iters}", "kernel_ms": gpu.last_kernel_ms()})
+
+
 if __name__ == "__main__":
-    build() if "--build" in sys.argv else run()
+    if "--build" in sys.argv:
+        build()
+    elif "--mcts" in sys.argv:
+        run_mcts()
+    else:
+        run()
