@@ -709,19 +709,21 @@ static const uint64_t kCellHashHost[BK_CELLS] = BK_CELL_HASH_INIT;
 #define FS_UNUSED ((int16_t)-1)
 #define FS_DUMMY ((int16_t)-2)
 
-struct FsetRef {  // one player's table: slot i at key[i * stride]
+struct FsetRef {  // one player's table: slots 2j, 2j + 1 at key[j * stride], key[j * stride + 1]
     int16_t* key;
-    int stride;
+    int stride;       // 2: a plain array; 2 * WAVE: slot pairs of one lane interleaved in LDS
     uint16_t* mask;
     uint16_t* fill;
     uint16_t* used;
     uint32_t cap;     // largest table this storage holds (power of 2)
     const uint64_t* hash;  // hash((r, c)) by cell
-    __host__ __device__ __forceinline__ int16_t& at(uint64_t i) const { return key[i * (uint64_t)stride]; }
+    __host__ __device__ __forceinline__ int16_t& at(uint64_t i) const {
+        return key[(i >> 1) * (uint64_t)stride + (i & 1u)];
+    }
 };
 
 __host__ __device__ __forceinline__ FsetRef fs_ref(bk_fset* s, int p, const uint64_t* htab) {
-    return FsetRef{s->key[p], 1, &s->mask[p], &s->fill[p], &s->used[p], BK_FSET_SLOTS, htab};
+    return FsetRef{s->key[p], 2, &s->mask[p], &s->fill[p], &s->used[p], BK_FSET_SLOTS, htab};
 }
 
 // set_insert_clean: first unused slot of the probe sequence
@@ -912,43 +914,39 @@ struct AddRows {
 
 // update_frontier_after_move (engine/board.py:315-367) of player p's table in fl for a
 // piece at cells[0..n) whose top row is ar, addability from A.  A table of <= 128
-// slots is staged in LDS (lk: [slot][lane] int16, stride WAVE) so the probe chains of
-// the ~45 add/discard ops wait on LDS, not L2/HBM; a 256-slot table (or a move that
-// grows one past 128) is updated in place.  false: table overflow.
+// slots is staged in LDS so the probe chains of the ~45 add/discard ops wait on LDS, not
+// L2/HBM: lk = this lane's dword of [slot pair][lane] (slots 2j, 2j + 1 in dword j *
+// WAVE): one ds_write_b32 / ds_read_b32 per slot pair, and a probe of ANY slot by each
+// lane hits bank `lane` (conflict-free).  A 256-slot table (or a move that grows one
+// past 128) is updated in place.  false: table overflow.
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
                                                const int32_t (&cells)[5], int n, int ar, const uint32_t (&A)[7]) {
     const AddRows rows7(A);
     auto addable = [&](int nr, int nc) { return rows7.at(ar, nr, nc); };
     bk_fset* gfs = &fl->s;
     const uint32_t gmask = gfs->mask[p];
+    uint32_t* lw = reinterpret_cast<uint32_t*>(lk);
     if (gmask < 128u) {
         const uint4* src4 = reinterpret_cast<const uint4*>(gfs->key[p]);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             if ((uint32_t)(8 * i) <= gmask) {
                 const uint4 v = src4[i];
-                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    lk[(8 * i + 2 * j) * WAVE] = (int16_t)(w[j] & 0xFFFFu);
-                    lk[(8 * i + 2 * j + 1) * WAVE] = (int16_t)(w[j] >> 16);
-                }
+                lw[(4 * i + 0) * WAVE] = v.x;
+                lw[(4 * i + 1) * WAVE] = v.y;
+                lw[(4 * i + 2) * WAVE] = v.z;
+                lw[(4 * i + 3) * WAVE] = v.w;
             }
         }
         uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
-        FsetRef t{lk, WAVE, &m, &f, &u, 128u, htab};
+        FsetRef t{lk, 2 * WAVE, &m, &f, &u, 128u, htab};
         if (fs_place_pred(t, fl->tmp, cells, n, addable)) {
             uint4* dst4 = reinterpret_cast<uint4*>(gfs->key[p]);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                if ((uint32_t)(8 * i) <= m) {
-                    uint32_t w[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        w[j] = (uint16_t)lk[(8 * i + 2 * j) * WAVE] |
-                               ((uint32_t)(uint16_t)lk[(8 * i + 2 * j + 1) * WAVE] << 16);
-                    dst4[i] = make_uint4(w[0], w[1], w[2], w[3]);
-                }
+                if ((uint32_t)(8 * i) <= m)
+                    dst4[i] = make_uint4(lw[(4 * i + 0) * WAVE], lw[(4 * i + 1) * WAVE], lw[(4 * i + 2) * WAVE],
+                                         lw[(4 * i + 3) * WAVE]);
             }
             gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
             return true;
@@ -1794,7 +1792,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             }
             uint32_t A[7];
             frontier_addable(rows_lds, ar, m, A);  // before the table staging reuses the area
-            int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + lane;
+            int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + 2 * lane;
             if (!place_frontier(&a.fslab[slot], p, lk, htab, cells, n, ar, A)) g.status |= 2u;
         }
         SECT(6);
@@ -2462,7 +2460,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint32_t* my = lds + wv * AREA;
     uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
-    int16_t* lk = reinterpret_cast<int16_t*>(my) + lane;
+    int16_t* lk = reinterpret_cast<int16_t*>(my) + 2 * lane;
     uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
     HeurShared* hs = reinterpret_cast<HeurShared*>(lds + AREA * (BLK / WAVE) + 2 * BK_CELLS);
     double* psum = reinterpret_cast<double*>(my + HEUR_PSUM * WAVE) + lane;

@@ -28,8 +28,10 @@ def per_launch(path, kernel):
     by = collections.defaultdict(list)
     for (_d, c), v in sorted(agg.items(), key=lambda kv: int(kv[0][0])):
         by[c].append(v)
-    # drop the warm-up launch (first k_rollout dispatch)
-    return {c: sum(v[1:]) / len(v[1:]) if len(v) > 1 else v[0] for c, v in by.items()}
+    # drop the warm-up launch (first dispatch of the kernel) unless the profiled run had
+    # no warm-up step (KEEP_FIRST=1: e.g. config5, whose 8 launches are one search)
+    k = 0 if os.environ.get("KEEP_FIRST") == "1" else 1
+    return {c: sum(v[k:]) / len(v[k:]) if len(v) > k else v[0] for c, v in by.items()}
 
 
 def main(src, tag, kernel=KERNEL):
