@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--rollouts", type=int, default=1024)
     ap.add_argument("--iterations", type=int, default=4096, help="config5 MCTS iterations per search")
     ap.add_argument("--chunk", type=int, default=512, help="config5 iterations per launch")
+    ap.add_argument("--rollout-policy", choices=("random", "heuristic"), default="random",
+                    help="config5: RandomAgent rollouts (the workload) or HeuristicAgent rollouts "
+                         "(MCTSAgent's default rollout agent)")
     ap.add_argument("--boards", type=int, default=4096, help="config2 boards")
     ap.add_argument("--all-players", action="store_true", help="config2: all 4 players of every board")
     ap.add_argument("--root-plies", type=int, default=20)
@@ -295,6 +298,9 @@ def run_config5(args, world, rank, local, dist):
     from reinforcementlearning_blokus_amd.shard import shard_indices
     from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
 
+    from reinforcementlearning_blokus_amd import _native as N
+    heur = args.rollout_policy == "heuristic"
+    policy = N.MCTS_ROLLOUT_HEURISTIC if heur else N.MCTS_ROLLOUT_RANDOM
     total = args.games or 65536
     gpu = BlokusGPU(local)
     dev = torch.device("cuda", local)
@@ -310,7 +316,8 @@ def run_config5(args, world, rank, local, dist):
     def timed_run(stop_after=None):
         kms.clear()
         batch.reset()
-        batch.run(chunk=args.chunk, stop_after=stop_after, on_chunk=lambda k: kms.append(gpu.last_kernel_ms()))
+        batch.run(chunk=args.chunk, stop_after=stop_after, on_chunk=lambda k: kms.append(gpu.last_kernel_ms()),
+                  rollout_policy=policy)
 
     for _ in range(args.warmup):  # warmup: the first 64 iterations of the same searches
         timed_run(stop_after=64)
@@ -337,24 +344,34 @@ def run_config5(args, world, rank, local, dist):
     sims_rank0 = int(res["iterations_run"].sum())
     bytes_rank0 = 2.0 * STATE_B * plies_local + (RESULT_B + 16 + 24 + 48) * sims_rank0
     achieved = bytes_rank0 / (kernel_ms * 1e-3) / 1e9
-    traffic, valu_insts = traffic_for("k_mcts")
+    kname = "k_mcts_h" if heur else "k_mcts"
+    traffic, valu_insts = traffic_for(kname)
     line = {
-        "metric": METRIC, "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+        "metric": METRIC if not heur else "MCTSAgent (default HeuristicAgent rollouts) simulations/sec",
+        "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u32+f64", "data": "synthetic",
         "config": {"workload": f"config5: {total} concurrent MCTSAgent searches x {args.iterations} iterations "
-                               "(UCT, Zobrist TT in HBM, 50-ply RandomAgent rollouts, reference frontier move "
-                               f"order, bit-exact) from GPU-generated {args.root_plies}-ply positions",
+                               f"(UCT, Zobrist TT in HBM, 50-ply {'HeuristicAgent' if heur else 'RandomAgent'} "
+                               "rollouts, reference frontier move order, bit-exact) from GPU-generated "
+                               f"{args.root_plies}-ply positions",
                    "games": total, "iterations": args.iterations, "chunk": args.chunk,
                    "simulations_per_step": total * args.iterations,
                    "rollout_plies_per_sim": plies / sims, "tt_hit_rate": hits / sims,
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_mcts",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                      "kernel_ms": kernel_ms, "launches": len(kms)},
         "compute_roofline": compute_roofline(valu_insts / max(1, len(kms)) if valu_insts else None,
                                              kernel_ms / max(1, len(kms))),
     }
+    if heur:  # no C restatement of the heuristic search to time: the reference's own numbers
+        line["reference"] = {"published": {"value": 40.9, "unit": "sims/s", "what": "MCTSAgent (heuristic "
+                                           "rollouts, TT), 200 ms/move, MacBook (BASELINE.md)"},
+                             "measured_build_container": {"value": 1.1, "unit": "sims/s/core",
+                                                          "what": "MCTSAgent default, 30 iterations (BASELINE.md)"},
+                             "gpu_over_published": value / 40.9}
+        return line
     if not args.no_cpu_baseline and world == 1:
         cb = cpu_baseline_mcts(roots, sets, batch, args.cpu_seconds)
         cb["gpu_over_cpu"] = value / cb["value"]
@@ -511,7 +528,7 @@ def run_config2(args, world, rank, local, dist):
         return None
     value = pairs / elapsed
     achieved = n * MOVEGEN_B / (kernel_ms * 1e-3) / 1e9
-    traffic, valu_insts = traffic_for("k_movegen")
+    traffic, valu_insts = traffic_for("k_movegen_g")
     line = {
         "metric": "batched legal-move generation (board-players/s, 20x20, 4p)", "value": value,
         "unit": "board-players/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -523,7 +540,7 @@ def run_config2(args, world, rank, local, dist):
                    "legal_moves_per_board_player": moves / n, "us_per_batch": kernel_ms * 1e3,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen_g",
                      "kernel_ms": kernel_ms, "bytes_per_board_player": MOVEGEN_B,
                      "bytes_written_per_board_player": 256 + 91 * 20 * 4 + 4},
         "compute_roofline": compute_roofline(valu_insts, kernel_ms),

@@ -586,6 +586,7 @@ struct MovegenArgs {
     uint32_t* out_rows;      // n x 91 x 20 (normal layout, bit c = column c) or NULL
     uint32_t* out_count;     // n or NULL
     uint8_t* out_mask4;      // has_moves mode
+    int32_t groups;          // k_movegen_g: orientation groups per board-player
 };
 
 __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&own)[4][20], uint32_t (&occ)[20]) {
@@ -615,15 +616,17 @@ __device__ __forceinline__ void rows_class_group(int i0, int i1, int grp, int G,
     }
 }
 
-// Batched movegen with the 91 orientations of each board-player split over MG_GROUPS
-// wave-uniform groups (every MG_GROUPS-th stencil-table entry): block b = one 64-lane
-// wave for board-players 64 * (b / MG_GROUPS) .. + 63 and group b % MG_GROUPS, so 4,096
-// board-players run as 1,024 waves instead of 64 (config 2 fills the chip).  Counts are
-// summed with one atomicAdd per (board-player, group) into the zeroed out_count.
-#define MG_GROUPS 16
+// Batched movegen with the 91 orientations of each board-player split over G = a.groups
+// wave-uniform groups (every G-th stencil-table entry): block b = one 64-lane wave for
+// board-players 64 * (b / G) .. + 63 and group b % G, so 4,096 board-players run as
+// 64 G waves instead of 64 (config 2 fills the chip).  Counts are summed with one
+// atomicAdd per (board-player, group) into the zeroed out_count.
+#define MG_GROUPS_MAX 91
+#define MG_GROUPS_DEFAULT_MAX 32
 __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
-    const int grp = blockIdx.x % MG_GROUPS;
-    const int i = (blockIdx.x / MG_GROUPS) * WAVE + threadIdx.x;
+    const int G = a.groups;
+    const int grp = blockIdx.x % G;
+    const int i = (blockIdx.x / G) * WAVE + threadIdx.x;
     const bool live = i < a.n;
     const int idx = live ? i : 0;
     const bk_state* s = a.states + idx;
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
             if (live && dst) dst[q] = v;
         }
     };
-#define BK_ROWS_GROUP(i0, i1, H, ...) rows_class_group<H, __VA_ARGS__>(i0, i1, grp, MG_GROUPS, P, emit);
+#define BK_ROWS_GROUP(i0, i1, H, ...) rows_class_group<H, __VA_ARGS__>(i0, i1, grp, G, P, emit);
     BK_CLASS_LIST(BK_ROWS_GROUP)
 #undef BK_ROWS_GROUP
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
@@ -2861,9 +2864,17 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     } else if (out_rows && ((uintptr_t)out_rows & 15)) {
         return set_err(h, BK_EINVAL, "bk_movegen: out_rows must be 16-byte aligned%s", "");
     }
-    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr};
+    // orientation groups: enough waves to fill the chip (~8 per CU) without splitting a
+    // board-player's work finer than needed
+    const int waves = (n + WAVE - 1) / WAVE;
+    int groups = (8 * h->num_cu + waves - 1) / waves;
+    groups = groups < 4 ? 4 : (groups > MG_GROUPS_DEFAULT_MAX ? MG_GROUPS_DEFAULT_MAX : groups);
+    if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
+    if (groups < 1) groups = 1;
+    if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
+    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
-    const int grid = ((n + WAVE - 1) / WAVE) * MG_GROUPS;
+    const int grid = waves * groups;
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     hipLaunchKernelGGL(k_movegen_g, dim3(grid), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());

@@ -102,7 +102,8 @@ class MctsBatch:
             self.tt_vals.fill_(float("nan"))
             self.tt_count.zero_()
 
-    def run(self, chunk: int = 0, on_chunk=None, stop_after: int | None = None):
+    def run(self, chunk: int = 0, on_chunk=None, stop_after: int | None = None,
+            rollout_policy: int = N.MCTS_ROLLOUT_RANDOM):
         """Run the searches (launches of `chunk` iterations); stop_after: only the
         first stop_after iterations (a warm-up)."""
         self.gpu.mcts_device(self.roots, self.sets, self.players, self.root_hash, self.zobrist, self.zidx, self.mt,
@@ -110,7 +111,7 @@ class MctsBatch:
                              tt_keys=self.tt_keys, tt_vals=self.tt_vals, tt_count=self.tt_count,
                              rewards=self.rewards, hit_flags=self.hit_flags,
                              max_rollout_moves=self.max_rollout_moves, chunk=chunk, on_chunk=on_chunk,
-                             stop_after=stop_after)
+                             stop_after=stop_after, rollout_policy=rollout_policy)
 
     def results(self) -> np.ndarray:
         return self.out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(-1)

@@ -56,6 +56,21 @@ def test_movegen_4096_synthetic_boards_bit_exact(gpu):
         assert int(cnt[i]) == len(O.legal_moves(boards[i], boards[i].cur, O.ORDER_NAIVE))
 
 
+@pytest.mark.parametrize("groups", [1, 7, 16, 32, 91])
+def test_movegen_orientation_groups_equal(gpu, groups, monkeypatch):
+    """k_movegen_g splits a board-player's 91 orientations over G waves (G from the batch
+    size; BK_MG_GROUPS overrides it): every split gives the same rows and counts."""
+    boards = oracle_states(300, seed0=77)
+    st = pack_many(boards)
+    players = np.array([b.cur for b in boards], dtype=np.uint8)
+    cnt0, rows0 = gpu.movegen(st, players)
+    monkeypatch.setenv("BK_MG_GROUPS", str(groups))
+    cnt, rows = gpu.movegen(st, players)
+    assert np.array_equal(cnt, cnt0) and np.array_equal(rows, rows0)
+    for i in range(0, 300, 29):
+        assert int(cnt[i]) == len(O.legal_moves(boards[i], boards[i].cur, O.ORDER_NAIVE))
+
+
 def test_has_moves(gpu):
     boards = [replay(r) for r in POS]
     mask = gpu.has_moves(pack_many(boards))
