@@ -443,12 +443,17 @@ def run_config4(args, world, rank, local, dist):
                                "seat_policy": "round_robin"})
     mine = shard_indices(total, rank, world).tolist()
     dev = torch.device("cuda", local)
+    def progress(rnd, left, prof):  # a line per round on stderr: long runs show they are alive
+        if rnd % 10 == 1:
+            print(f"config4 rank {rank}: round {rnd}, {left} games in play, mcts {prof['mcts_s']:.1f} s",
+                  file=sys.stderr, flush=True)
+
     for _ in range(args.warmup):
         run_games_batched(cfg, mine[:64], device=local)
     barrier_sync(dist)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        recs = run_games_batched(cfg, mine, device=local)
+        recs = run_games_batched(cfg, mine, device=local, progress=progress)
     barrier_sync(dist)
     elapsed = time.perf_counter() - t0
     from reinforcementlearning_blokus_amd.arena.runner import LAST_BATCH_PROFILE

@@ -349,7 +349,7 @@ LAST_BATCH_PROFILE: Dict[str, float] = {}  # phase times of the last run_games_b
 
 
 def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
-                      device: int = 0) -> List[Dict[str, Any]]:
+                      device: int = 0, progress=None) -> List[Dict[str, Any]]:
     """Mixed seatings (Random / Heuristic / MCTS / FastMCTS, config 4) in lockstep batches:
     every game's random and heuristic turns run inside bk_arena_advance (one launch
     advances all games to their next search-seat turn, each seat drawing from its own
@@ -357,7 +357,8 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     (MCTSAgent.search_packed) and all FastMCTS seats in one bk_fastmcts launch
     (FastMCTSAgent.think_many), their moves are placed, and the loop repeats.  Records
     equal run_single_game's (arena_runner.py:578-777): same agents, seeds, streams and
-    move order.  Per-move times are launch shares."""
+    move order.  Per-move times are launch shares.  progress(round, games_left, profile),
+    if given, is called at the start of every round."""
     from .. import _native as N
     from ..engine.move_generator import order_moves
     from ..engine.pieces import ORIENT_CELLS, ORIENT_LIST
@@ -405,6 +406,8 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0)
     while len(active):
         prof["rounds"] += 1
+        if progress is not None:
+            progress(prof["rounds"], len(active), prof)
         ta = time.perf_counter()
         sub_st, sub_fs, sub_rng = states[active].copy(), sets[active].copy(), rng[active].copy()
         before = sub_st["reserved"].copy()

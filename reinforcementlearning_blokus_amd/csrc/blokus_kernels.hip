@@ -1046,15 +1046,28 @@ __device__ __forceinline__ double heur_orient_sum(int g, int nr, const uint2* ro
     uint32_t cd[5], cc[5];
     orient_cells(g, n, cd, cc);
     double sum = 0.0;
+    // rows holding legal anchors, then ONE per-lane loop over this lane's moves (row-major,
+    // columns ascending: the summation order of a per-row loop).  The wave iterates max
+    // over lanes of the orientation's move count, not the sum over rows of the per-row
+    // maxima (most rows of most lanes are empty).
+    uint32_t rm = 0;
 #pragma unroll 1
     for (int r = 0; r < nr; ++r) {
-        uint32_t ok = rows[r * WAVE].y;
+        const uint32_t ok = rows[r * WAVE].y;
         count += __builtin_popcount(ok);
-        while (ok) {
-            const int x = __builtin_ctz(ok);
-            ok &= ok - 1u;
-            sum += heur_e(n, cd, cc, r, x, rows, hs, edge_w);
+        rm |= (ok != 0u ? 1u : 0u) << r;
+    }
+    int r = 0;
+    uint32_t ok = 0;
+    while (ok | rm) {
+        if (ok == 0u) {
+            r = __builtin_ctz(rm);
+            rm &= rm - 1u;
+            ok = rows[r * WAVE].y;
         }
+        const int x = __builtin_ctz(ok);
+        ok &= ok - 1u;
+        sum += heur_e(n, cd, cc, r, x, rows, hs, edge_w);
     }
     return sum;
 }
@@ -2864,11 +2877,11 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     } else if (out_rows && ((uintptr_t)out_rows & 15)) {
         return set_err(h, BK_EINVAL, "bk_movegen: out_rows must be 16-byte aligned%s", "");
     }
-    // orientation groups: enough waves to fill the chip (~8 per CU) without splitting a
-    // board-player's work finer than needed
+    // orientation groups: about 4 waves per CU, at least 8 groups (measured best at 4,096
+    // and 16,384 board-players, profiles/r02/sweeps/movegen_groups.jsonl)
     const int waves = (n + WAVE - 1) / WAVE;
-    int groups = (8 * h->num_cu + waves - 1) / waves;
-    groups = groups < 4 ? 4 : (groups > MG_GROUPS_DEFAULT_MAX ? MG_GROUPS_DEFAULT_MAX : groups);
+    int groups = (4 * h->num_cu + waves - 1) / waves;
+    groups = groups < 8 ? 8 : (groups > MG_GROUPS_DEFAULT_MAX ? MG_GROUPS_DEFAULT_MAX : groups);
     if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
     if (groups < 1) groups = 1;
     if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
