@@ -23,7 +23,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from .bitboard import BIT_TABLE
+from .bitboard import BIT_TABLE, coords_to_mask, mask_to_coords, shift_mask
 from .board import Board, Player, Position
 from .pieces import (ALL_PIECE_ORIENTATIONS, GID, ORIENT_CELLS, ORIENT_LIST, PieceGenerator,
                      PieceOrientation, PiecePlacement)
@@ -199,6 +199,25 @@ class LegalMoveGenerator:
             return False
         return board.can_place_piece(move.get_positions(shapes), player)
 
+    def is_placement_legal_bitboard(self, board: Board, player: Player, orientation: PieceOrientation,
+                                    anchor_board_coord, anchor_piece_index: int = 0) -> bool:
+        """Anchor-cell legality (move_generator.py:561-655): offsets[anchor_piece_index] is put
+        on anchor_board_coord; the shape is shifted with strict shift_mask (off-board -> False),
+        neighbours are derived from the shifted cells, first-move status from the board."""
+        if anchor_piece_index >= len(orientation.offsets):
+            return False
+        pr, pc = orientation.offsets[anchor_piece_index]
+        shifted = shift_mask(orientation.shape_mask, anchor_board_coord[0] - pr, anchor_board_coord[1] - pc)
+        if shifted is None:
+            return False
+        return self.is_placement_legal_bitboard_coords(
+            board, player, mask_to_coords(shifted), is_first_move=board.player_first_move[player])
+
+    def is_placement_legal_grid(self, board: Board, player: Player, orientation: PieceOrientation,
+                                anchor_board_coord, anchor_piece_index: int, placement_coords) -> bool:
+        """Grid legality of explicit cells (move_generator.py:657-680); orientation/anchor unused."""
+        return board.can_place_piece([Position(r, c) for r, c in placement_coords], player)
+
     def is_placement_legal_bitboard_fast(self, board: Board, player: Player, piece_orientation: PieceOrientation,
                                          anchor_row: int, anchor_col: int, is_first_move: bool = False) -> bool:
         """Single-anchor legality from bitboards (move_generator.py:760-831)."""
@@ -254,6 +273,77 @@ def get_shared_generator() -> LegalMoveGenerator:
         if _SHARED is None:
             _SHARED = LegalMoveGenerator()
     return _SHARED
+
+
+def _neighbour_sets(cells):
+    n = Board.SIZE
+    placed = set(cells)
+    diag, orth = set(), set()
+    for r, c in cells:
+        for (dr, dc), dst in (((-1, -1), diag), ((-1, 1), diag), ((1, -1), diag), ((1, 1), diag),
+                              ((-1, 0), orth), ((1, 0), orth), ((0, -1), orth), ((0, 1), orth)):
+            rr, cc = r + dr, c + dc
+            if 0 <= rr < n and 0 <= cc < n and (rr, cc) not in placed:
+                dst.add((rr, cc))
+    return diag, orth
+
+
+def debug_compare_bitboard_vs_grid(board: Board, player: Player, orientation: PieceOrientation,
+                                   anchor_board_coord, anchor_piece_index: int, placement_coords) -> None:
+    """Debug report (move_generator.py:1083-1217): masks from the explicit cells vs the
+    orientation's precomputed masks shifted to the anchor, the overlap/adjacency hits, and
+    grid vs bitboard legality.  Prints only when BLOKUS_DEBUG_BITBOARD is set."""
+    if not DEBUG_BITBOARD:
+        return
+    diag_set, orth_set = _neighbour_sets(placement_coords)
+    pr, pc = orientation.offsets[anchor_piece_index]
+    d_row, d_col = anchor_board_coord[0] - pr, anchor_board_coord[1] - pc
+    shifted = {k: shift_mask(getattr(orientation, k + "_mask"), d_row, d_col) for k in ("shape", "diag", "orth")}
+    line = "=" * 80
+    print("\n" + line)
+    print("=== DEBUG BITBOARD VS GRID ===")
+    print(f"player={player.name} (value={player.value})")
+    print(f"piece_id={orientation.piece_id}")
+    print(f"anchor_board_coord={anchor_board_coord}, anchor_piece_index={anchor_piece_index}")
+    print(f"d_row={d_row}, d_col={d_col} (computed from board_r={anchor_board_coord[0]} - piece_r={pr}, "
+          f"board_c={anchor_board_coord[1]} - piece_c={pc})")
+    print(f"placement_coords={sorted(placement_coords)}")
+    print()
+    for title, a_label, a, b_label, key in (
+            ("Shape from coords vs shifted shape:", "coords -> mask -> coords",
+             sorted(mask_to_coords(coords_to_mask(placement_coords))), "shifted orientation shape coords", "shape"),
+            ("Diag neighbors from coords vs shifted diag mask:", "diag from coords", sorted(diag_set),
+             "diag mask coords", "diag"),
+            ("Orth neighbors from coords vs shifted orth mask:", "orth from coords", sorted(orth_set),
+             "orth mask coords", "orth")):
+        b = sorted(mask_to_coords(shifted[key] or 0))
+        print(title)
+        print(f"  {a_label}: {a}")
+        print(f"  {b_label}: {b}")
+        print(f"  MATCH: {a == b}")
+        print()
+    own, occ = board.player_bits[player], board.occupied_bits
+    hits = {"Overlap": (shifted["shape"] or 0) & occ, "Orth adj": (shifted["orth"] or 0) & own,
+            "Diag adj": (shifted["diag"] or 0) & own}
+    print("Adjacency & overlap checks:")
+    print(f"  shape & occupied_bits -> {bool(hits['Overlap'])} (should be False for legal)")
+    print(f"  orth & player_bits     -> {bool(hits['Orth adj'])} (should be False for legal)")
+    print(f"  diag & player_bits      -> {bool(hits['Diag adj'])} (should be True if not first move)")
+    print()
+    for name, m in hits.items():
+        if m:
+            print(f"  {name} cells: {sorted(mask_to_coords(m))}")
+    print()
+    gen = LegalMoveGenerator()
+    grid_legal = gen.is_placement_legal_grid(board, player, orientation, anchor_board_coord,
+                                             anchor_piece_index, placement_coords)
+    bit_legal = gen.is_placement_legal_bitboard(board, player, orientation, anchor_board_coord, anchor_piece_index)
+    print(f"RESULT: grid_legal={grid_legal}, bitboard_legal={bit_legal}")
+    if grid_legal != bit_legal:
+        print("  *** MISMATCH DETECTED ***")
+    print("=== END DEBUG ===")
+    print(line)
+    print()
 
 
 def move_to_int(m: Move) -> int:

@@ -166,3 +166,54 @@ def test_mcts_tt_load_and_reserve_keep_entries():
             assert not np.isnan(tt.vals[1, s])
             s = (s + 1) % tt.cap
         assert tt.vals[1, s] == val
+
+
+@pytest.mark.parametrize("i", range(0, len(POS), 3))
+def test_placement_legal_bitboard_anchor_cells_match_legal_set(i):
+    """is_placement_legal_bitboard (move_generator.py:561-655) with the anchor on any of the
+    orientation's cells agrees with the reference's naive legal set, and with the grid check
+    (is_placement_legal_grid, :657-680) on the same cells.  Tolerance: exact."""
+    from reinforcementlearning_blokus_amd.engine.move_generator import LegalMoveGenerator
+    from reinforcementlearning_blokus_amd.engine.pieces import ALL_PIECE_ORIENTATIONS, ORIENT_LIST
+    rec = POS[i]
+    b = engine_board(rec)
+    ob = replay(rec)
+    gen = LegalMoveGenerator()
+    rnd = random.Random(i)
+    for p in range(4):
+        pl = Player(p + 1)
+        legal = set(rec["players"][p].get("naive_list") or O.legal_moves(ob, p, O.ORDER_NAIVE))
+        probes = list(legal)[:40] + [rnd.randrange(36400) for _ in range(200)]
+        for a in probes:
+            g, rest = divmod(a, 400)
+            r, c = divmod(rest, 20)
+            orient = ALL_PIECE_ORIENTATIONS[ORIENT_LIST[g][0]][ORIENT_LIST[g][1]]
+            k = rnd.randrange(len(orient.offsets))
+            dr, dc = orient.offsets[k]
+            got = gen.is_placement_legal_bitboard(b, pl, orient, (r + dr, c + dc), k)
+            if ORIENT_LIST[g][0] not in b.player_pieces_used[pl]:  # (the check ignores pieces used)
+                assert got == (a in legal), (p, a, k)
+            if got or all(0 <= r + y < 20 and 0 <= c + x < 20 for y, x in orient.offsets):
+                cells = [(r + y, c + x) for y, x in orient.offsets]
+                assert gen.is_placement_legal_grid(b, pl, orient, (r + dr, c + dc), k, cells) == got
+        assert not gen.is_placement_legal_bitboard(b, pl, orient, (0, 0), 5)  # index past the offsets
+
+
+def test_debug_compare_bitboard_vs_grid_report(capsys, monkeypatch):
+    """debug_compare_bitboard_vs_grid (move_generator.py:1083-1217): silent unless
+    BLOKUS_DEBUG_BITBOARD; otherwise reports MATCH lines and both legality results."""
+    from reinforcementlearning_blokus_amd.engine import move_generator as MG
+    from reinforcementlearning_blokus_amd.engine.pieces import ALL_PIECE_ORIENTATIONS
+    rec = POS[0]
+    b = engine_board(rec)
+    o = ALL_PIECE_ORIENTATIONS[1][0]
+    MG.debug_compare_bitboard_vs_grid(b, Player.RED, o, (0, 0), 0, [(0, 0)])
+    assert capsys.readouterr().out == ""
+    monkeypatch.setattr(MG, "DEBUG_BITBOARD", True)
+    MG.debug_compare_bitboard_vs_grid(b, Player.RED, o, (5, 5), 0, [(5, 5)])
+    out = capsys.readouterr().out
+    assert "=== DEBUG BITBOARD VS GRID ===" in out and out.count("MATCH: ") == 3
+    # the shape always matches; the precomputed diag/orth masks hold only non-negative
+    # offsets, so at an interior anchor they miss the up/left neighbours (as in the reference)
+    assert "shifted orientation shape coords: [(5, 5)]\n  MATCH: True" in out
+    assert "RESULT: grid_legal=" in out and "MISMATCH" not in out
