@@ -68,3 +68,57 @@ def test_shard_indices_partition():
         for w in (1, 2, 3, 8):
             allidx = np.sort(np.concatenate([shard_indices(n, r, w) for r in range(w)]))
             assert np.array_equal(allidx, np.arange(n))
+
+
+def _exp_worker(rank, world, port, out_root, q):
+    """run_experiment on one gloo rank; the reference's own game records (arena_runs.json)
+    stand in for the device play, so the test covers sharding, the gather and the writer."""
+    import copy
+    import torch.distributed as dist
+    from reinforcementlearning_blokus_amd.arena import RunConfig, runner
+    from tests.helpers import load_golden
+    fx = load_golden("arena_runs.json")
+    played = []
+
+    def fake_play(run_config, indices, **kw):
+        played.extend(int(i) for i in indices)
+        return [copy.deepcopy(fx["games"][int(i)]) for i in indices]
+
+    runner.run_games_gpu = fake_play
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg = RunConfig.from_dict(dict(fx["config"], output_root=out_root))
+        out = runner.run_experiment(cfg, rank=rank, world=world, dist=dist)
+        q.put((rank, played, out.get("run_dir")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_run_experiment(tmp_path):
+    """run_experiment(world=2): each rank plays game index == rank (mod 2); rank 0 gathers
+    and writes games.jsonl / summary.json equal to the reference run (arena_runner.py:914-996)."""
+    import json
+    from tests.helpers import load_golden
+    fx = load_golden("arena_runs.json")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exp_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (played, d)) for r, played, d in (q.get(timeout=300) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] == list(range(0, 16, 2)) and got[1][0] == list(range(1, 16, 2))
+    assert got[1][1] is None
+    run_dir = got[0][1]
+    games = [json.loads(x) for x in open(os.path.join(run_dir, "games.jsonl")).read().splitlines()]
+    assert [g["game_index"] for g in games] == list(range(16))
+    for g, ref in zip(games, fx["games"]):
+        assert g["final_scores"] == ref["final_scores"] and g["seat_assignment"] == ref["seat_assignment"]
+    summary = json.load(open(os.path.join(run_dir, "summary.json")))
+    assert summary["completed_games"] == 16
+    for k in ("win_stats", "wins_by_seat", "score_stats", "pairwise_matchups"):
+        assert summary[k] == json.loads(json.dumps(fx["summary"][k]))
