@@ -66,6 +66,10 @@ __device__ unsigned long long g_sections[BK_NSECT];
 #define BLOCK 256
 #define ROWMASK 0x000FFFFFu  // columns 0..19
 #define OFFBOARD 0xFFF00000u // columns 20..31
+// word views of int16 frontier tables: may_alias, or type-based alias analysis lets the
+// compiler move them across int16 accesses of the same bytes
+typedef uint32_t bk_u32_alias __attribute__((may_alias));
+typedef uint4 bk_u4_alias __attribute__((may_alias));
 
 __constant__ uint32_t kInfo[BK_NUM_ORIENTS] = BK_ORIENT_INFO_INIT;
 __constant__ uint32_t kCells[BK_NUM_ORIENTS][5] = BK_ORIENT_CELLS_INIT;
@@ -469,14 +473,14 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
         ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
         ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
         // the anchors go to the C half: row r's C word is not read again (later rows
-        // read rows >= r + 1), and the B half stays intact for frontier_addable
+        // read rows >= r + 1), and the B half stays intact for frontier_ops
         rows[r * WAVE].y = r <= rlim ? (ac & ~ab) : 0u;
     }
     // Pass 2 reads the table 16 slots per pair of uint4 loads into registers, all
     // indices static (a dynamically indexed key array would live in scratch memory)
     int found_r = -1, found_c = 0;
     uint32_t cnt = 0;
-    const uint4* k4 = reinterpret_cast<const uint4*>(key);
+    const bk_u4_alias* k4 = reinterpret_cast<const bk_u4_alias*>(key);
 #pragma unroll 1
     for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 16) {
         const uint4 qa = k4[b0 >> 3], qb = k4[(b0 >> 3) + 1];
@@ -504,20 +508,88 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
     out_c = found_c;
 }
 
-// After locate_move_frontier (B half of the LDS rows = the mover's blocked rows BEFORE
-// the move): the cells update_frontier_after_move may add for the placed piece, i.e.
-// empty and not orthogonally adjacent to the mover on the board AFTER the move
-// (engine/board.py:340-352), for rows ar - 1 .. ar + 5 (A[i] = row ar - 1 + i).
-// m[d] = the piece's cells in row ar + d.
-__device__ __forceinline__ void frontier_addable(const uint2* rows, int ar, const uint32_t (&m)[5], uint32_t (&A)[7]) {
+// The set operations of update_frontier_after_move that CHANGE the mover's set.  The
+// reference runs 9 ops per placed cell q (o = 0: discard the cell, 1..4: add the
+// diagonals (-1,-1) (-1,1) (1,-1) (1,1) when addable, 5..8: discard the orthogonals
+// (-1,0) (1,0) (0,-1) (0,1)); most are no-ops (an add of a member, a discard of a
+// non-member), and a no-op leaves the CPython table untouched.  Membership is known
+// without probing the table, from the board alone:
+// * an EMPTY cell is a member iff it is on the true frontier (diagonal to own, not
+//   orthogonal to own), or, before the player's first move, iff it is the start corner
+//   (init_frontier_for_player, engine/board.py:389-404): adds happen exactly when a cell
+//   joins the true frontier, discards exactly when it leaves;
+// * an own cell is never a member (discarded when placed);
+// * a cell another player occupied may be a stale member: a discard of it is a real op
+//   whenever it is diagonal and not orthogonal to own (conservative; a discard of a
+//   non-member is a harmless no-op).
+// Adds target empty, non-orthogonal cells only, so no key is both added and discarded
+// within a move; a key added twice (a diagonal of two cells, e.g. inside the U piece) or
+// discarded twice (an orthogonal of two cells) is real at most at its first op.
+// Bit 9 q + o of the result marks the ops to run, in the reference's order.  Window:
+// 7 x 7 bits, rows ar - 1 .. ar + 5 and columns ac - 1 .. ac + 5 (bit 7 i + j).
+// rows[R * WAVE].x = the mover's blocked rows BEFORE the move; slab = own planes before
+// or after the move (the piece's cells m are masked out).
+__device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& slab, int p, bool first, int gs,
+                                                 int ar, int ac, const uint32_t (&m)[5]) {
+    uint32_t o[9];  // own rows ar - 2 .. ar + 6 before the move
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const int R = ar - 2 + j;
+        const uint32_t pr = (j >= 2 && j <= 6) ? m[j - 2] : 0u;
+        const uint32_t v = slab.at(p, R < 0 ? 0 : R > 19 ? 19 : R);
+        o[j] = (R >= 0 && R <= 19) ? (v & ~pr) : 0u;
+    }
+    const int crow = (p == 0 || p == 1) ? 0 : 19;
+    const uint32_t cbit = (p == 0 || p == 3) ? 0x00000001u : 0x00080000u;
+    uint64_t wm = 0, wa = 0;  // maybe-member / real-add windows
 #pragma unroll
     for (int i = 0; i < 7; ++i) {
         const int R = ar - 1 + i;
+        const bool inb = R >= 0 && R <= 19;
+        const uint32_t own = o[i + 1], up = o[i], dn = o[i + 2];
+        const uint32_t orth = own | (own << 1) | (own >> 1) | up | dn;
+        const uint32_t vd = up | dn;
+        const uint32_t diag = ((vd << 1) | (vd >> 1)) & ROWMASK;
+        const uint32_t b = inb ? rows[(R < 0 ? 0 : R > 19 ? 19 : R) * WAVE].x : ~0u;
         const uint32_t pr = (i >= 1 && i <= 5) ? m[i - 1] : 0u;
-        const uint32_t up = (i >= 2) ? m[i - 2] : 0u, dn = (i <= 4) ? m[i] : 0u;
-        const uint32_t b = (R >= 0 && R <= 19) ? rows[(R < 0 ? 0 : R > 19 ? 19 : R) * WAVE].x : ~0u;
-        A[i] = ~(b | pr | (pr << 1) | (pr >> 1) | up | dn) & ROWMASK;
+        const uint32_t pu = (i >= 2) ? m[i - 2] : 0u, pd = (i <= 4) ? m[i] : 0u;
+        const uint32_t addable = ~(b | pr | (pr << 1) | (pr >> 1) | pu | pd) & ROWMASK;
+        const uint32_t corner = (R == crow) ? cbit : 0u;
+        const uint32_t mm = inb ? (first ? corner : (diag & ~orth)) : 0u;   // maybe a member
+        const uint32_t mem = inb ? (first ? corner : (diag & ~b)) : 0u;     // a member (empty cells)
+        const uint32_t ra = addable & ~mem;
+        wm |= (uint64_t)(((mm << 1) >> ac) & 0x7Fu) << (7 * i);
+        wa |= (uint64_t)(((ra << 1) >> ac) & 0x7Fu) << (7 * i);
     }
+    const uint32_t n = (kInfo[gs] >> 8) & 0xFFu;
+    uint64_t real = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const uint32_t cell = kCells[gs][q < (int)n ? q : 0];
+        const int pq = ((int)(cell >> 8) + 1) * 7 + (int)(cell & 0xFFu) + 1;
+        const bool live = q < (int)n;
+#pragma unroll
+        for (int op = 0; op < 9; ++op) {
+            const int dr = (op == 1 || op == 2 || op == 5) ? -1 : (op == 3 || op == 4 || op == 6) ? 1 : 0;
+            const int dc = (op == 1 || op == 3 || op == 7) ? -1 : (op == 2 || op == 4 || op == 8) ? 1 : 0;
+            const int pos = pq + 7 * dr + dc;
+            // after its first op on a key, later ops of the same kind are no-ops
+            uint64_t bit;
+            if (op >= 1 && op <= 4) {
+                bit = (wa >> pos) & 1ull;
+                wa &= live ? ~(1ull << pos) : ~0ull;
+            } else {
+                bit = (wm >> pos) & 1ull;
+                wm &= live ? ~(1ull << pos) : ~0ull;
+            }
+            real |= (live ? bit : 0ull) << (9 * q + op);
+        }
+    }
+    // the LDS rows of this lane are overwritten by other lanes' table staging right after
+    // this call: every load above must complete first (no sinking past those stores)
+    uint32_t lo = (uint32_t)real, hi = (uint32_t)(real >> 32);
+    asm volatile("" : "+v"(lo), "+v"(hi) : : "memory");
+    return ((uint64_t)hi << 32) | lo;
 }
 
 // ------------------------------------------------------------------------------------
@@ -893,44 +965,45 @@ __host__ __device__ inline bool fs_copy(FsetRef d, const int16_t* skey, uint32_t
     return true;
 }
 
+// Run the ops marked in `real` (frontier_ops) on table t, in order: one probe routine in
+// a per-lane loop, so a wave runs as many probe chains as its busiest lane has real ops
+// (typically ~10) instead of all 45.  false: table overflow.
+__device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_t (&cells)[5], uint64_t real) {
+    // key offset + 21 of op o, 6 bits each: 0, -21, -19, 19, 21, -20, 20, -1, 1
+    constexpr uint64_t KD = (21ull << 0) | (0ull << 6) | (2ull << 12) | (40ull << 18) | (42ull << 24) |
+                            (1ull << 30) | (41ull << 36) | (20ull << 42) | (22ull << 48);
+#pragma unroll 1
+    while (real) {
+        const int s = (int)__builtin_ctzll(real);
+        real &= real - 1ull;
+        const int q = (s * 57) >> 9;  // s / 9 for s < 45
+        const int op = s - 9 * q;
+        const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
+        const int key = cell + (int)((KD >> (6 * op)) & 63ull) - 21;
+        if (!fs_op(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u)) return false;
+    }
+    return true;
+}
+
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch
 struct FsLane {
     bk_fset s;
     int16_t tmp[BK_FSET_SLOTS];
 };
 
-// the 7 addable rows of frontier_addable as opaque register values: a select chain over
-// array elements gets folded into a dynamically indexed (scratch) load otherwise
-struct AddRows {
-    uint32_t a0, a1, a2, a3, a4, a5, a6;
-    __device__ __forceinline__ explicit AddRows(const uint32_t (&A)[7])
-        : a0(A[0]), a1(A[1]), a2(A[2]), a3(A[3]), a4(A[4]), a5(A[5]), a6(A[6]) {
-        asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6));
-    }
-    // bit (nr, nc), nr in ar-1 .. ar+5 (row index i = nr - ar + 1)
-    __device__ __forceinline__ bool at(int ar, int nr, int nc) const {
-        const int i = nr - ar + 1;
-        const uint32_t row = i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : i == 3 ? a3 : i == 4 ? a4 : i == 5 ? a5 : a6;
-        return ((row >> nc) & 1u) != 0u;
-    }
-};
-
 // update_frontier_after_move (engine/board.py:315-367) of player p's table in fl for a
-// piece at cells[0..n) whose top row is ar, addability from A.  A table of <= 128
-// slots is staged in LDS so the probe chains of the ~45 add/discard ops wait on LDS, not
-// L2/HBM: lk = this lane's dword of [slot pair][lane] (slots 2j, 2j + 1 in dword j *
+// piece at cells[0..n): the ops marked in `real` (frontier_ops).  A table of <= 128
+// slots is staged in LDS so the probe chains wait on LDS, not L2/HBM: lk = this lane's dword of [slot pair][lane] (slots 2j, 2j + 1 in dword j *
 // WAVE): one ds_write_b32 / ds_read_b32 per slot pair, and a probe of ANY slot by each
 // lane hits bank `lane` (conflict-free).  A 256-slot table (or a move that grows one
 // past 128) is updated in place.  false: table overflow.
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
-                                               const int32_t (&cells)[5], int n, int ar, const uint32_t (&A)[7]) {
-    const AddRows rows7(A);
-    auto addable = [&](int nr, int nc) { return rows7.at(ar, nr, nc); };
+                                               const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
     const uint32_t gmask = gfs->mask[p];
-    uint32_t* lw = reinterpret_cast<uint32_t*>(lk);
+    bk_u32_alias* lw = reinterpret_cast<bk_u32_alias*>(lk);
     if (gmask < 128u) {
-        const uint4* src4 = reinterpret_cast<const uint4*>(gfs->key[p]);
+        const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             if ((uint32_t)(8 * i) <= gmask) {
@@ -943,8 +1016,8 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
         }
         uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, 128u, htab};
-        if (fs_place_pred(t, fl->tmp, cells, n, addable)) {
-            uint4* dst4 = reinterpret_cast<uint4*>(gfs->key[p]);
+        if (fs_run_ops(t, fl->tmp, cells, real)) {
+            bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 if ((uint32_t)(8 * i) <= m)
@@ -955,7 +1028,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
             return true;
         }
     }
-    return fs_place_pred(fs_ref(gfs, p, htab), fl->tmp, cells, n, addable);
+    return fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1215,7 +1288,7 @@ __device__ __forceinline__ void heur_walk_frontier(int gs, const uint32_t (&ok)[
     orient_cells(gs, n, cd, cc);
     int found_r = -1, found_c = 0, last_r = -1, last_c = 0;
     double last_lo = R, last_e = 0.0;
-    const uint4* k4 = reinterpret_cast<const uint4*>(key);
+    const bk_u4_alias* k4 = reinterpret_cast<const bk_u4_alias*>(key);
 #pragma unroll 1
     for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 16) {
         const uint4 qa = k4[b0 >> 3], qb = k4[(b0 >> 3) + 1];
@@ -1350,16 +1423,16 @@ __device__ __forceinline__ void store_state(const RolloutArgs& a, const Game& g,
 // the counters, as uint4
 __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
     static_assert(sizeof(bk_fset) % 16 == 0 && BK_FSET_SLOTS % 8 == 0, "bk_fset is copied as uint4");
-    const uint4* tail_s = reinterpret_cast<const uint4*>(&src->mask[0]);
-    uint4* tail_d = reinterpret_cast<uint4*>(&dst->mask[0]);
+    const bk_u4_alias* tail_s = reinterpret_cast<const bk_u4_alias*>(&src->mask[0]);
+    bk_u4_alias* tail_d = reinterpret_cast<bk_u4_alias*>(&dst->mask[0]);
     const uint4 t0 = tail_s[0], t1 = tail_s[1];  // mask[4] fill[4] used[4] reserved[4]
     tail_d[0] = t0;
     tail_d[1] = t1;
     const uint32_t masks[4] = {t0.x & 0xFFFFu, t0.x >> 16, t0.y & 0xFFFFu, t0.y >> 16};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const uint4* s4 = reinterpret_cast<const uint4*>(src->key[q]);
-        uint4* d4 = reinterpret_cast<uint4*>(dst->key[q]);
+        const bk_u4_alias* s4 = reinterpret_cast<const bk_u4_alias*>(src->key[q]);
+        bk_u4_alias* d4 = reinterpret_cast<bk_u4_alias*>(dst->key[q]);
         const int nv = (int)(masks[q] + 1u) / 8;  // 8 slots per uint4
 #pragma unroll 2
         for (int i = 0; i < nv; ++i) d4[i] = s4[i];
@@ -1374,8 +1447,8 @@ __device__ __forceinline__ bool fs_copy_dev(bk_fset* d, int q, const bk_fset* s,
     uint32_t newsize = 8;
     if (sused * 5 >= 7u * 3u)
         while (newsize <= sused * 2) newsize <<= 1;
-    uint4* d4 = reinterpret_cast<uint4*>(d->key[q]);
-    const uint4* s4 = reinterpret_cast<const uint4*>(s->key[q]);
+    bk_u4_alias* d4 = reinterpret_cast<bk_u4_alias*>(d->key[q]);
+    const bk_u4_alias* s4 = reinterpret_cast<const bk_u4_alias*>(s->key[q]);
     if (newsize > BK_FSET_SLOTS) {
         fs_clear(fs_ref(d, q, htab));
         return false;
@@ -1806,10 +1879,10 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 const uint32_t cell = kCells[gs][q < n ? q : 0];
                 cells[q] = (ar + (int)(cell >> 8)) * 20 + ac + (int)(cell & 0xFFu);
             }
-            uint32_t A[7];
-            frontier_addable(rows_lds, ar, m, A);  // before the table staging reuses the area
+            // before the table staging reuses the area
+            const uint64_t real = frontier_ops(rows_lds, slab, p, (g.first >> p) & 1u, gs, ar, ac, m);
             int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + 2 * lane;
-            if (!place_frontier(&a.fslab[slot], p, lk, htab, cells, n, ar, A)) g.status |= 2u;
+            if (!place_frontier(&a.fslab[slot], p, lk, htab, cells, real)) g.status |= 2u;
         }
         SECT(6);
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
@@ -2188,12 +2261,12 @@ __device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&p
 }
 
 // mc_place with the frontier update on the LDS-staged table (place_frontier).  pm /
-// cells from piece_cells, A from frontier_addable -- computed by EVERY lane of the wave
+// cells from piece_cells, real from frontier_ops -- computed by EVERY lane of the wave
 // before any lane stages a table: the staged tables of some lanes overlay the LDS rows
 // of others.
 __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
                                                 const uint64_t* htab, const uint32_t (&pm)[5],
-                                                const int32_t (&cells)[5], const uint32_t (&A)[7], int16_t* lk) {
+                                                const int32_t (&cells)[5], uint64_t real, int16_t* lk) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
 #pragma unroll
@@ -2203,7 +2276,7 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
             slab.at(4, ar + d) |= pm[d];
         }
     }
-    const bool ok = place_frontier(T, p, lk, htab, cells, n, ar, A);
+    const bool ok = place_frontier(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
     m.first &= ~(1u << p);
@@ -2616,10 +2689,11 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             m.mode = MC_SELECT;
             continue;
         }
-        uint32_t pm[5], A[7];
+        uint32_t pm[5];
         int32_t cells[5];
         piece_cells(gs, ar, ac, pm, cells);
-        frontier_addable(rows_lds, ar, pm, A);  // all lanes, before any table staging
+        // all lanes, before any table staging
+        const uint64_t real = frontier_ops(rows_lds, slab, p, (m.first >> p) & 1u, gs, ar, ac, pm);
         // MCTSNode.expand (mcts_agent.py:113-145) places on new_board = board.copy() (B),
         // a rollout ply on sim (B): one place call site for both
         const bool expand = m.mode == MC_EXPAND;
@@ -2639,7 +2713,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
         }
         // expand: new_board = board.copy() is table A itself (A is a copy, see mc_replay)
-        ok &= mc_place_staged(m, slab, p, gs, ar, expand ? &L->A : &L->B, htab, pm, cells, A, lk);
+        ok &= mc_place_staged(m, slab, p, gs, ar, expand ? &L->A : &L->B, htab, pm, cells, real, lk);
         if (expand) {
             ok &= mc_copy_tables(&L->B.s, &L->A.s, htab);  // MCTSNode(new_board): board.copy()
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }

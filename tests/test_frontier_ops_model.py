@@ -1,0 +1,126 @@
+"""The device's frontier-op prefilter (csrc/blokus_kernels.hip frontier_ops), restated
+bit for bit in Python and checked against the reference's update_frontier_after_move
+(engine/board.py:315-367) on a Python set over random self-play games (oracle move
+generation, test infrastructure).  Every op that changes the set must be marked; the
+only extra marks allowed are discards of cells another player occupies (no-ops on the
+table).  Tolerance: exact.
+"""
+import random
+
+import pytest
+
+from oracle import pyoracle as O
+from reinforcementlearning_blokus_amd.engine.pieces import ORIENT_CELLS, ORIENT_LIST
+
+ROWMASK = 0xFFFFF
+CORNER = [(0, 0), (0, 19), (19, 19), (19, 0)]
+OPS = [(0, 0), (-1, -1), (-1, 1), (1, -1), (1, 1), (-1, 0), (1, 0), (0, -1), (0, 1)]
+
+
+def frontier_ops(own_rows, occ_rows, p, first, g, ar, ac):
+    """Python restatement of the kernel's frontier_ops (own/occ rows after the move)."""
+    cells = ORIENT_CELLS[g]
+    m = [0] * 5
+    for dr, dc in cells:
+        m[dr] |= 1 << (ac + dc)
+
+    def masked(rows, R):
+        if R < 0 or R > 19:
+            return 0
+        return rows[R] & ~(m[R - ar] if 0 <= R - ar <= 4 else 0)
+
+    crow = 0 if p in (0, 1) else 19
+    cbit = 1 if p in (0, 3) else 1 << 19
+    wm = wa = 0
+    for i in range(7):
+        R = ar - 1 + i
+        inb = 0 <= R <= 19
+        o, up, dn = masked(own_rows, R), masked(own_rows, R - 1), masked(own_rows, R + 1)
+        orth = o | o << 1 | o >> 1 | up | dn
+        diag = (((up | dn) << 1) | ((up | dn) >> 1)) & ROWMASK
+        b = ((masked(occ_rows, R) | orth | 0xFFF00000) & 0xFFFFFFFF) if inb else 0xFFFFFFFF
+        pr = m[i - 1] if 1 <= i <= 5 else 0
+        pu = m[i - 2] if i >= 2 else 0
+        pd = m[i] if i <= 4 else 0
+        addable = ~(b | pr | pr << 1 | pr >> 1 | pu | pd) & ROWMASK
+        corner = cbit if R == crow else 0
+        mm = (corner if first else diag & ~orth) if inb else 0
+        mem = (corner if first else diag & ~b) if inb else 0
+        wm |= (((mm << 1) >> ac) & 0x7F) << (7 * i)
+        wa |= ((((addable & ~mem) << 1) >> ac) & 0x7F) << (7 * i)
+    real = 0
+    for q, (cd, cc) in enumerate(cells):
+        pq = (cd + 1) * 7 + cc + 1
+        for op, (dr, dc) in enumerate(OPS):
+            pos = pq + 7 * dr + dc
+            if 1 <= op <= 4:
+                bit = (wa >> pos) & 1
+                wa &= ~(1 << pos)
+            else:
+                bit = (wm >> pos) & 1
+                wm &= ~(1 << pos)
+            real |= bit << (9 * q + op)
+    return real
+
+
+def reference_update(S, grid, p, cells_abs):
+    """update_frontier_after_move on a Python set; bit 9 q + o set for ops that changed S."""
+    changed = 0
+    for q, (r, c) in enumerate(cells_abs):
+        for op, (dr, dc) in enumerate(OPS):
+            nr, nc = r + dr, c + dc
+            if not (0 <= nr < 20 and 0 <= nc < 20):
+                continue
+            if 1 <= op <= 4:
+                if grid[nr][nc] != -1 or any(0 <= nr + a < 20 and 0 <= nc + b < 20 and grid[nr + a][nc + b] == p
+                                             for a, b in ((-1, 0), (1, 0), (0, -1), (0, 1))):
+                    continue
+                if (nr, nc) not in S:
+                    changed |= 1 << (9 * q + op)
+                    S.add((nr, nc))
+            elif (nr, nc) in S:
+                changed |= 1 << (9 * q + op)
+                S.discard((nr, nc))
+    return changed
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_frontier_ops_mark_every_real_op(seed):
+    rng = random.Random(seed)
+    n_real = n_marked = 0
+    for _ in range(6):
+        b = O.new_board()
+        grid = [[-1] * 20 for _ in range(20)]
+        S = [{CORNER[p]} for p in range(4)]
+        first = [True] * 4
+        own = [[0] * 20 for _ in range(4)]
+        occ = [0] * 20
+        passes, p = 0, 0
+        while passes < 4:
+            moves = O.legal_moves(b, p, O.ORDER_NAIVE)
+            if moves:
+                passes = 0
+                g, rest = divmod(rng.choice(moves), 400)
+                ar, ac = divmod(rest, 20)
+                cells_abs = [(ar + dr, ac + dc) for dr, dc in ORIENT_CELLS[g]]
+                for r, c in cells_abs:
+                    own[p][r] |= 1 << c
+                    occ[r] |= 1 << c
+                    grid[r][c] = p
+                marked = frontier_ops(own[p], occ, p, first[p], g, ar, ac)
+                real = reference_update(S[p], grid, p, cells_abs)
+                assert real & ~marked == 0
+                for s in range(45):
+                    if (marked & ~real) >> s & 1:
+                        q, op = divmod(s, 9)
+                        r, c = cells_abs[q][0] + OPS[op][0], cells_abs[q][1] + OPS[op][1]
+                        assert op not in (1, 2, 3, 4) and grid[r][c] not in (-1, p)
+                n_real += bin(real).count("1")
+                n_marked += bin(marked).count("1")
+                first[p] = False
+                O.place_cells(b, p, ORIENT_LIST[g][0], [r * 20 + c for r, c in cells_abs])
+            else:
+                passes += 1
+            p = (p + 1) & 3
+            b.cur = p
+    assert n_marked <= 1.05 * n_real
