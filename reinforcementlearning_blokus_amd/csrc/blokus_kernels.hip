@@ -75,6 +75,36 @@ __constant__ uint32_t kInfo[BK_NUM_ORIENTS] = BK_ORIENT_INFO_INIT;
 __constant__ uint32_t kCells[BK_NUM_ORIENTS][5] = BK_ORIENT_CELLS_INIT;
 __constant__ uint32_t kClass[BK_NUM_ORIENTS][2] = BK_CLASS_TABLE_INIT;
 
+// frontier_ops: per orientation, bit 9 q + o set iff q < n and op o of cell q is the first
+// op of its kind (add / discard) on its cell relative to the anchor -- later ones are
+// no-ops of update_frontier_after_move (a diagonal or orthogonal shared by two cells, or
+// a cell that is also another cell's orthogonal).  Built at compile time from the cells.
+struct FopsTable {
+    uint64_t m[BK_NUM_ORIENTS];
+};
+constexpr FopsTable make_fops_first() {
+    constexpr uint32_t info[BK_NUM_ORIENTS] = BK_ORIENT_INFO_INIT;
+    constexpr uint32_t cells[BK_NUM_ORIENTS][5] = BK_ORIENT_CELLS_INIT;
+    constexpr int dr[9] = {0, -1, -1, 1, 1, -1, 1, 0, 0}, dc[9] = {0, -1, 1, -1, 1, 0, 0, -1, 1};
+    FopsTable t{};
+    for (int g = 0; g < BK_NUM_ORIENTS; ++g) {
+        const int n = (int)((info[g] >> 8) & 0xFFu);
+        uint64_t seen_add = 0, seen_dis = 0, m = 0;
+        for (int q = 0; q < n; ++q) {
+            const int pq = ((int)(cells[g][q] >> 8) + 1) * 7 + (int)(cells[g][q] & 0xFFu) + 1;
+            for (int o = 0; o < 9; ++o) {
+                const uint64_t b = 1ull << (pq + 7 * dr[o] + dc[o]);
+                uint64_t& seen = (o >= 1 && o <= 4) ? seen_add : seen_dis;
+                if (!(seen & b)) m |= 1ull << (9 * q + o);
+                seen |= b;
+            }
+        }
+        t.m[g] = m;
+    }
+    return t;
+}
+__constant__ FopsTable kFopsFirst = make_fops_first();
+
 // ------------------------------------------------------------------------------------
 // state <-> rows
 // ------------------------------------------------------------------------------------
@@ -524,7 +554,8 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
 //   non-member is a harmless no-op).
 // Adds target empty, non-orthogonal cells only, so no key is both added and discarded
 // within a move; a key added twice (a diagonal of two cells, e.g. inside the U piece) or
-// discarded twice (an orthogonal of two cells) is real at most at its first op.
+// discarded twice (an orthogonal of two cells) is real at most at its first op
+// (kFopsFirst).
 // Bit 9 q + o of the result marks the ops to run, in the reference's order.  Window:
 // 7 x 7 bits, rows ar - 1 .. ar + 5 and columns ac - 1 .. ac + 5 (bit 7 i + j).
 // rows[R * WAVE].x = the mover's blocked rows BEFORE the move; slab = own planes before
@@ -561,30 +592,20 @@ __device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& 
         wm |= (uint64_t)(((mm << 1) >> ac) & 0x7Fu) << (7 * i);
         wa |= (uint64_t)(((ra << 1) >> ac) & 0x7Fu) << (7 * i);
     }
-    const uint32_t n = (kInfo[gs] >> 8) & 0xFFu;
+    // cell q's 3 x 3 neighbourhood moved to window bits 0..2, 7..9, 14..16 (centre 8), then
+    // op o's bit gathered to bit o: discards (o = 0, 5..8) from wm, adds (1..4) from wa
     uint64_t real = 0;
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
-        const uint32_t cell = kCells[gs][q < (int)n ? q : 0];
-        const int pq = ((int)(cell >> 8) + 1) * 7 + (int)(cell & 0xFFu) + 1;
-        const bool live = q < (int)n;
-#pragma unroll
-        for (int op = 0; op < 9; ++op) {
-            const int dr = (op == 1 || op == 2 || op == 5) ? -1 : (op == 3 || op == 4 || op == 6) ? 1 : 0;
-            const int dc = (op == 1 || op == 3 || op == 7) ? -1 : (op == 2 || op == 4 || op == 8) ? 1 : 0;
-            const int pos = pq + 7 * dr + dc;
-            // after its first op on a key, later ops of the same kind are no-ops
-            uint64_t bit;
-            if (op >= 1 && op <= 4) {
-                bit = (wa >> pos) & 1ull;
-                wa &= live ? ~(1ull << pos) : ~0ull;
-            } else {
-                bit = (wm >> pos) & 1ull;
-                wm &= live ? ~(1ull << pos) : ~0ull;
-            }
-            real |= (live ? bit : 0ull) << (9 * q + op);
-        }
+        const uint32_t cell = kCells[gs][q];  // entries past the piece's cells: masked below
+        const int sh = ((int)(cell >> 8) + 1) * 7 + (int)(cell & 0xFFu) + 1 - 8;
+        const uint32_t tm = (uint32_t)(wm >> sh), ta = (uint32_t)(wa >> sh);
+        const uint32_t code = ((tm >> 8) & 1u) | ((ta << 1) & 2u) | (ta & 4u) | ((ta >> 11) & 8u) |
+                              ((ta >> 12) & 16u) | ((tm << 4) & 32u) | ((tm >> 9) & 64u) | (tm & 128u) |
+                              ((tm >> 1) & 256u);
+        real |= (uint64_t)code << (9 * q);
     }
+    real &= kFopsFirst.m[gs];
     // the LDS rows of this lane are overwritten by other lanes' table staging right after
     // this call: every load above must complete first (no sinking past those stores)
     uint32_t lo = (uint32_t)real, hi = (uint32_t)(real >> 32);
@@ -986,6 +1007,11 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
 }
 
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch
+// frontier tables smaller than this many slots are staged in LDS for place_frontier
+// (0: probe the table in global memory)
+#ifndef BK_FS_STAGE_MAX
+#define BK_FS_STAGE_MAX 128
+#endif
 struct FsLane {
     bk_fset s;
     int16_t tmp[BK_FSET_SLOTS];
@@ -1002,7 +1028,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     bk_fset* gfs = &fl->s;
     const uint32_t gmask = gfs->mask[p];
     bk_u32_alias* lw = reinterpret_cast<bk_u32_alias*>(lk);
-    if (gmask < 128u) {
+    if (BK_FS_STAGE_MAX > 0 && gmask < (uint32_t)BK_FS_STAGE_MAX) {
         const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {

@@ -17,6 +17,19 @@ CORNER = [(0, 0), (0, 19), (19, 19), (19, 0)]
 OPS = [(0, 0), (-1, -1), (-1, 1), (1, -1), (1, 1), (-1, 0), (1, 0), (0, -1), (0, 1)]
 
 
+def first_ops(g):
+    """kFopsFirst[g]: op o of cell q is the first op of its kind on its relative cell."""
+    seen = {True: set(), False: set()}
+    m = 0
+    for q, (cd, cc) in enumerate(ORIENT_CELLS[g]):
+        for op, (dr, dc) in enumerate(OPS):
+            key = (cd + dr, cc + dc)
+            if key not in seen[1 <= op <= 4]:
+                m |= 1 << (9 * q + op)
+            seen[1 <= op <= 4].add(key)
+    return m
+
+
 def frontier_ops(own_rows, occ_rows, p, first, g, ar, ac):
     """Python restatement of the kernel's frontier_ops (own/occ rows after the move)."""
     cells = ORIENT_CELLS[g]
@@ -50,17 +63,12 @@ def frontier_ops(own_rows, occ_rows, p, first, g, ar, ac):
         wa |= ((((addable & ~mem) << 1) >> ac) & 0x7F) << (7 * i)
     real = 0
     for q, (cd, cc) in enumerate(cells):
-        pq = (cd + 1) * 7 + cc + 1
-        for op, (dr, dc) in enumerate(OPS):
-            pos = pq + 7 * dr + dc
-            if 1 <= op <= 4:
-                bit = (wa >> pos) & 1
-                wa &= ~(1 << pos)
-            else:
-                bit = (wm >> pos) & 1
-                wm &= ~(1 << pos)
-            real |= bit << (9 * q + op)
-    return real
+        sh = (cd + 1) * 7 + cc + 1 - 8  # cell q's 3 x 3 neighbourhood at bits 0..2, 7..9, 14..16
+        tm, ta = (wm >> sh) & 0xFFFFFFFF, (wa >> sh) & 0xFFFFFFFF
+        code = (((tm >> 8) & 1) | ((ta << 1) & 2) | (ta & 4) | ((ta >> 11) & 8) | ((ta >> 12) & 16)
+                | ((tm << 4) & 32) | ((tm >> 9) & 64) | (tm & 128) | ((tm >> 1) & 256))
+        real |= code << (9 * q)
+    return real & first_ops(g)
 
 
 def reference_update(S, grid, p, cells_abs):
