@@ -82,7 +82,13 @@ class BlokusGame:
 
     def _check_game_over(self) -> None:
         """Over iff no player has a legal move (engine/game.py:182-214)."""
-        if any(self.move_generator.has_legal_moves(self.board, p) for p in Player):
+        mg = self.move_generator
+        batched = ("has_legal_moves" not in vars(mg) and hasattr(mg, "players_with_moves")
+                   and getattr(type(mg), "has_legal_moves", None) is LegalMoveGenerator.has_legal_moves)
+        if batched:  # one launch for the four players; a patched has_legal_moves is honoured
+            if any(mg.players_with_moves(self.board)):
+                return
+        elif any(mg.has_legal_moves(self.board, p) for p in Player):
             return
         self.board.game_over = True
         res = self.get_game_result()

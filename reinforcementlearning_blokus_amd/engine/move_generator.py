@@ -175,6 +175,12 @@ class LegalMoveGenerator:
     def has_legal_moves(self, board: Board, player: Player) -> bool:
         return self.get_move_count(board, player) > 0
 
+    def players_with_moves(self, board: Board) -> List[bool]:
+        """has_legal_moves for all four players in ONE launch (BlokusGame._check_game_over)."""
+        from .board import pack_states
+        cnt, _ = self._engine().movegen(pack_states([board] * 4), np.arange(4, dtype=np.uint8), rows=False)
+        return [int(c) > 0 for c in cnt]
+
     def _has_any_legal_move_frontier(self, board: Board, player: Player) -> bool:
         return self.has_legal_moves(board, player)
 

@@ -29,6 +29,8 @@ def test_legal_moves_in_reference_frontier_order():
                 assert got == ref["frontier_list"]
             assert sha_ints(got) == ref["sha_frontier"]
             assert gen.has_legal_moves(b, Player(p + 1)) == ref["has_moves"]
+        # the one-launch check of all four players (BlokusGame._check_game_over)
+        assert gen.players_with_moves(b) == [rec["players"][p]["has_moves"] for p in range(4)]
 
 
 def test_legal_moves_batch_equals_single():
