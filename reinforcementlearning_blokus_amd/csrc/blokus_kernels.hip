@@ -159,18 +159,31 @@ __device__ __forceinline__ void derive_rows(const uint32_t (&own)[20], const uin
 // cells (BP[R] = B[R] | B[R] >> 1), BV/CV for a vertical pair (BV[R] = B[R] | B[R + 1]):
 // a pair of cells of a piece costs one term instead of two.  The stencil table
 // (tools/gen_tables.py) covers the 410 cells of the 91 orientations with the fewest
-// terms.
+// terms.  Each row is stored as one 64-bit word, C in the high half and B in the low
+// half, so ONE v_lshrrev_b64 shifts a term's B and C rows together (the stream runs at
+// the single-issue rate, where a 64-bit shift costs what a 32-bit one does).  Shifts are
+// at most 3 (tools/gen_tables.py), so the C bits that enter B's top bits (>= 29) are
+// never read, and B's bits 20..28 stay the OFFBOARD ones.
 struct Planes {
-    uint32_t B[20], C[20], BP[20], CP[20], BV[20], CV[20];
+    uint64_t BC[20], BCP[20], BCV[20];
+    __device__ __forceinline__ uint32_t b(int R) const { return (uint32_t)BC[R]; }
+    __device__ __forceinline__ uint32_t c(int R) const { return (uint32_t)(BC[R] >> 32); }
 };
+
+__device__ __forceinline__ void derive_rows(const uint32_t (&own)[20], const uint32_t (&occ)[20], bool first, int p,
+                                            Planes& P) {
+    uint32_t B[20], C[20];
+    derive_rows(own, occ, first, p, B, C);
+#pragma unroll
+    for (int R = 0; R < 20; ++R) P.BC[R] = ((uint64_t)C[R] << 32) | B[R];
+}
 
 __device__ __forceinline__ void make_pairs(Planes& P) {
 #pragma unroll
     for (int R = 0; R < 20; ++R) {
-        P.BP[R] = P.B[R] | (P.B[R] >> 1);
-        P.CP[R] = P.C[R] | (P.C[R] >> 1);
-        P.BV[R] = R < 19 ? (P.B[R] | P.B[R + 1]) : P.B[R];  // row 19: never a pair's top
-        P.CV[R] = R < 19 ? (P.C[R] | P.C[R + 1]) : P.C[R];
+        // B's bit 31 (OFFBOARD) absorbs C's bit 0
+        P.BCP[R] = P.BC[R] | (P.BC[R] >> 1);
+        P.BCV[R] = R < 19 ? (P.BC[R] | P.BC[R + 1]) : P.BC[R];  // row 19: never a pair's top
     }
 }
 
@@ -199,32 +212,31 @@ struct StencilClass {
     static constexpr int ts[NT] = {T...};
 
     template <int K>
-    __device__ __forceinline__ static uint32_t tb(const Planes& P, int r, const uint32_t (&sh)[5]) {
+    __device__ __forceinline__ static uint64_t tv(const Planes& P, int r, const uint32_t (&sh)[5]) {
         constexpr int d = ts[K] >> 2, kind = ts[K] & 3;
-        const uint32_t v = kind == 1 ? P.BP[r + d] : kind == 2 ? P.BV[r + d] : P.B[r + d];
+        const uint64_t v = kind == 1 ? P.BCP[r + d] : kind == 2 ? P.BCV[r + d] : P.BC[r + d];
         return K == 0 ? v : v >> sh[K];
     }
-    template <int K>
-    __device__ __forceinline__ static uint32_t tc(const Planes& P, int r, const uint32_t (&sh)[5]) {
-        constexpr int d = ts[K] >> 2, kind = ts[K] & 3;
-        const uint32_t v = kind == 1 ? P.CP[r + d] : kind == 2 ? P.CV[r + d] : P.C[r + d];
-        return K == 0 ? v : v >> sh[K];
-    }
+    __device__ __forceinline__ static uint32_t lo(uint64_t v) { return (uint32_t)v; }
+    __device__ __forceinline__ static uint32_t hi(uint64_t v) { return (uint32_t)(v >> 32); }
     // OR of terms K.. into (b, c); the last C term folds into ok
     template <int K>
     __device__ __forceinline__ static uint32_t fold(const Planes& P, int r, const uint32_t (&sh)[5], uint32_t b,
                                                     uint32_t c) {
         if constexpr (K + 2 <= NT - 1) {
-            b = BITOP3(b, tb<K>(P, r, sh), tb<K + 1>(P, r, sh), LUT_OR3);
-            c = BITOP3(c, tc<K>(P, r, sh), tc<K + 1>(P, r, sh), LUT_OR3);
+            const uint64_t t0 = tv<K>(P, r, sh), t1 = tv<K + 1>(P, r, sh);
+            b = BITOP3(b, lo(t0), lo(t1), LUT_OR3);
+            c = BITOP3(c, hi(t0), hi(t1), LUT_OR3);
             return fold<K + 2>(P, r, sh, b, c);
         } else if constexpr (K + 2 == NT) {  // two left: B merges both, C merges one + ok
-            b = BITOP3(b, tb<K>(P, r, sh), tb<K + 1>(P, r, sh), LUT_OR3);
-            c = c | tc<K>(P, r, sh);
-            return BITOP3(c, tc<K + 1>(P, r, sh), b, LUT_OR2_ANDN);
+            const uint64_t t0 = tv<K>(P, r, sh), t1 = tv<K + 1>(P, r, sh);
+            b = BITOP3(b, lo(t0), lo(t1), LUT_OR3);
+            c = c | hi(t0);
+            return BITOP3(c, hi(t1), b, LUT_OR2_ANDN);
         } else if constexpr (K + 1 == NT) {  // one left
-            b = b | tb<K>(P, r, sh);
-            return BITOP3(c, tc<K>(P, r, sh), b, LUT_OR2_ANDN);
+            const uint64_t t0 = tv<K>(P, r, sh);
+            b = b | lo(t0);
+            return BITOP3(c, hi(t0), b, LUT_OR2_ANDN);
         } else {
             return BITOP3(c, b, b, LUT_ANDN);
         }
@@ -245,7 +257,8 @@ struct StencilClass {
         // and the live set no longer fits 3 waves per SIMD (other waves hide latency)
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            f(r, fold<1>(P, r, sh, tb<0>(P, r, sh), tc<0>(P, r, sh)));
+            const uint64_t t0 = tv<0>(P, r, sh);
+            f(r, fold<1>(P, r, sh, lo(t0), hi(t0)));
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -736,7 +749,7 @@ __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
             own[R] |= (q == p) ? row : 0u;
         }
     Planes P;
-    derive_rows(own, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
+    derive_rows(own, occ, (s->first_move >> p) & 1u, p, P);
     make_pairs(P);
     const uint32_t avail = live ? (~s->used[p] & 0x1FFFFFu) : 0u;
     uint32_t total = 0;
@@ -783,7 +796,7 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
         Planes P;
 #pragma unroll
         for (int R = 0; R < 20; ++R) ow[R] = plane_row(s->planes[p], R);
-        derive_rows(ow, occ, (s->first_move >> p) & 1u, p, P.B, P.C);
+        derive_rows(ow, occ, (s->first_move >> p) & 1u, p, P);
         make_pairs(P);
         const uint32_t total = movegen_counts<false>(P, live ? (~s->used[p] & 0x1FFFFFu) : 0u, nullptr, lane);
         mask |= (uint8_t)((total > 0) << p);
@@ -1779,7 +1792,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 own[R] = idle ? 0u : slab.at(p, R);
                 occ[R] = idle ? 0u : slab.at(4, R);
             }
-            derive_rows(own, occ, (g.first >> p) & 1u, p, P.B, P.C);
+            derive_rows(own, occ, (g.first >> p) & 1u, p, P);
         }
         make_pairs(P);
         const uint32_t avail = idle ? 0u : (~g.used.get(p) & 0x1FFFFFu);
@@ -1805,10 +1818,10 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             if (__builtin_amdgcn_ballot_w64(heur)) {
                 const int edge_w = (g.move_count0 + g.plies) < 30 ? 6 : 3;  // move_count / 100.0 < 0.3
 #pragma unroll
-                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE].x = P.B[R];
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE].x = P.b(R);
                 const uint32_t t = heur_pass_a(P, heur ? avail : 0u, rows_lds, psum, hs, edge_w);
 #pragma unroll
-                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
                 if (heur) {
                     total = t;
                     if (t > 0u) {
@@ -1845,7 +1858,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         }
         // counts are consumed: the area now takes the mover's rows for locate
 #pragma unroll
-        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
         SECT(3);
         int ar, ac;
         if constexpr (FR) {
@@ -2632,7 +2645,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
                 own[R] = idle ? 0u : slab.at(p, R);
                 occ[R] = idle ? 0u : slab.at(4, R);
             }
-            derive_rows(own, occ, (m.first >> p) & 1u, p, P.B, P.C);
+            derive_rows(own, occ, (m.first >> p) & 1u, p, P);
         }
         make_pairs(P);
         const uint32_t avail = idle ? 0u : (~m.used.get(p) & 0x1FFFFFu);
@@ -2680,10 +2693,10 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
                 // Board.move_count of the rollout board: placements on the way from the root
                 edge_w = (int)(a.roots[m.game].move_count + m.depth + m.plies) < 30 ? 6 : 3;
 #pragma unroll
-                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE].x = P.B[R];
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE].x = P.b(R);
                 heur_pass_a(P, hroll ? avail : 0u, rows_lds, psum, hs, edge_w);
 #pragma unroll
-                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+                for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
                 if (hroll) {
 #pragma unroll 1
                     for (int q = 0; q < BK_PIECES; ++q) h_total += psum[q * WAVE];
@@ -2693,7 +2706,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             }
         }
 #pragma unroll
-        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.B[R], P.C[R]);
+        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
         FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
         int ar, ac;
         SECT(10);
