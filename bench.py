@@ -17,9 +17,13 @@ Other workloads (one JSON line each, same contract):
                       synthetic mid-game boards (plies 16..40), player to move (and
                       --all-players: all 4); one step = one bk_movegen launch.
 
-N>1: one process per GPU (torchrun), weak scaling for config3 (each rank plays its own
-256 games, no data-path collective); after the timed region the per-rank results are
-all-gathered over RCCL.  Prints ONE JSON line on rank 0.
+N>1: one process per GPU, weak scaling for config3 (each rank plays its own 256 games,
+no data-path collective); after the timed region the per-rank results are all-gathered
+over RCCL.  Prints ONE JSON line on rank 0.  Either launch works:
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  python bench.py --gpus N        (bench.py starts the N rank processes itself)
+`--gpus` must equal the process group's size; `n_gpus` is taken from the group.
+`--selftest [--gpus N]` checks the N-rank launch/shard/gather path on CPU with gloo.
 """
 from __future__ import annotations
 
@@ -53,9 +57,13 @@ STATE_B, RESULT_B = 256, 32
 MOVEGEN_B = 256 + 5096  # state in + dense 91 x 400-bit mask out, per board-player
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU).  Under torch.distributed.run it must equal WORLD_SIZE; "
+                         "run directly with N > 1, bench.py starts the N rank processes itself")
+    ap.add_argument("--selftest", action="store_true",
+                    help="CPU check of the N-rank path (gloo): launch, shard, gather, compare with one process")
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 20; config5: 1)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; config5: 1, "
                                                               "a 64-iteration chunk)")
@@ -76,7 +84,7 @@ def parse():
     ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
                     help="config3 in-kernel move order: naive (default) or the reference's frontier order "
                          "(CPython set tables carried per game)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.steps is None:
         a.steps = 1 if a.workload in ("config5", "config4") else (200 if a.workload == "config2" else 20)
     if a.warmup is None:
@@ -138,17 +146,70 @@ def cpu_baseline_playouts(roots_np, seconds, order):
                       f"{order} move order, {threads} threads (one per usable core), {dt:.1f} s"}
 
 
-# ------------------------------------------------------------------ common
-def setup():
-    import torch
+# ------------------------------------------------------------------ N-rank launch
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the environment): start N rank
+    processes of this same script, one per GPU (LOCAL_RANK r -> device r), with the
+    torch.distributed env contract of torch.distributed.run, and wait for them.  This
+    process never touches the GPU and never execs; rank 0 prints the JSON line on the
+    inherited stdout.  If one rank fails the others are stopped (they would wait at
+    a barrier forever).  Returns the exit code to use (first failing rank's, else 0).
+    This replaces the reference's only parallelism, the process pool over whole games
+    (scripts/arena_tuning.py:124-131)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
+def setup(args):
+    """Join the job: world size from the process group (RCCL on GPUs, gloo for the
+    --selftest), checked against --gpus."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    import torch
     dist = None
+    if not args.selftest:
+        torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.selftest:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        got = dist.get_world_size()
+        if got != world or (args.gpus is not None and got != args.gpus):
+            raise SystemExit(f"bench.py: process group has {got} ranks, expected {args.gpus or world}")
+        world, rank = got, dist.get_rank()
     return world, rank, local, dist
 
 
@@ -362,8 +423,8 @@ def run_config5(args, world, rank, local, dist):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                      "kernel_ms": kernel_ms, "launches": len(kms)},
-        "compute_roofline": compute_roofline(valu_insts / max(1, len(kms)) if valu_insts else None,
-                                             kernel_ms / max(1, len(kms))),
+        # traffic_for gives VALU instructions per launch: pair them with the average launch time
+        "compute_roofline": compute_roofline(valu_insts, kernel_ms / max(1, len(kms))),
     }
     if heur:  # no C restatement of the heuristic search to time: the reference's own numbers
         line["reference"] = {"published": {"value": 40.9, "unit": "sims/s", "what": "MCTSAgent (heuristic "
@@ -589,11 +650,56 @@ def cpu_baseline_movegen(st, pl, seconds, value):
                                            "get_legal_moves at ply 20 (boards/s/core)")}
 
 
+def run_selftest(args, world, rank, local, dist):
+    """CPU check of the N-rank path with gloo (no GPU, no kernels): every rank takes its
+    shard of a config-3-sized job's game indices (shard.shard_indices), makes each
+    game's 32-byte record from the same per-game quantities the GPU path derives from
+    the global index (root seed, arena agent seeds, MctsBatch zobrist table / rollout
+    stream seed / MT state), all-gathers them with shard.gather_results, and rank 0
+    checks the result equals one process making every record."""
+    import numpy as np
+    import torch
+
+    from reinforcementlearning_blokus_amd.shard import gather_results, shard_indices
+    from reinforcementlearning_blokus_amd.workloads import mcts_game_inputs
+    total = args.games or 1001  # odd: shards of unequal size
+
+    def records(idx):
+        idx = np.asarray(idx, dtype=np.int64)
+        zi, mt = mcts_game_inputs(idx, seed0=args.seed)
+        rec = np.zeros((len(idx), 32), np.uint8)
+        w = rec.view(np.uint32)
+        w[:, 0] = idx
+        w[:, 1] = zi
+        w[:, 2:6] = mt[:, :4]
+        w[:, 6] = mt[:, 624]
+        w[:, 7] = np.bitwise_xor.reduce(mt[:, :624], axis=1)
+        return rec
+
+    if os.environ.get("BENCH_SELFTEST_FAIL_RANK") == str(rank):  # failure injection (tests)
+        raise SystemExit(3)
+    mine = shard_indices(total, rank, world)
+    got = gather_results(torch.from_numpy(records(mine)), total, rank, world, dist) if dist else \
+        torch.from_numpy(records(mine))
+    if rank != 0:
+        return None
+    ok = bool(np.array_equal(got.numpy(), records(range(total))))
+    if not ok:
+        raise SystemExit("bench.py --selftest: gathered records differ from the one-process records")
+    return {"selftest": "ok", "n_ranks": world, "backend": "gloo" if dist else "none", "games": total,
+            "shard_sizes": [len(shard_indices(total, r, world)) for r in range(world)]}
+
+
 def main():
     args = parse()
-    world, rank, local, dist = setup()
+    n = args.gpus or 1
+    if "WORLD_SIZE" not in os.environ and n > 1:
+        sys.exit(launch_ranks(n, sys.argv[1:]))
+    world, rank, local, dist = setup(args)
     run = {"config3": run_config3, "config5": run_config5, "config2": run_config2,
            "config4": run_config4}[args.workload]
+    if args.selftest:
+        run = run_selftest
     line = run(args, world, rank, local, dist)
     if line is not None:
         print(json.dumps(line), flush=True)

@@ -39,6 +39,17 @@ def numpy_mt_states(seeds) -> np.ndarray:
     return out
 
 
+def mcts_game_inputs(index, seed0: int = 0, n_tables: int = 8):
+    """Per-game search inputs of global games `index` (a rank's shard or the whole job):
+    zobrist table index i % n_tables (ZobristHash(seed=table), mcts/zobrist.py:41-68) and
+    the rollout RandomAgent's MT19937 state for seed seed0 + i (agents/random_agent.py:29).
+    Pure functions of the global index, so a sharded job searches exactly what one
+    process would."""
+    index = np.asarray(index, dtype=np.int64)
+    zi = (index % n_tables).astype(np.int32)
+    return zi, numpy_mt_states(seed0 + int(g) for g in index)
+
+
 class MctsBatch:
     """Device-resident inputs and outputs of one bk_mcts batch (config 5 layout).
 
@@ -62,13 +73,12 @@ class MctsBatch:
         # global game indices (a rank's shard of a multi-GPU job): seeds and tables follow them
         self.index = np.arange(n) if index is None else np.asarray(index, dtype=np.int64)
         assert len(self.index) == n
-        zi = (self.index % n_tables).astype(np.int32)
+        zi, self.mt0 = mcts_game_inputs(self.index, seed0, n_tables)
         rh = np.zeros(n, np.uint64)
         for t in range(n_tables):
             sel = zi == t
             rh[sel] = hash_states(roots[sel], zob[t])
         self.zobrist_np, self.zidx_np, self.hash_np = zob, zi, rh
-        self.mt0 = numpy_mt_states(seed0 + int(g) for g in self.index)
         u8 = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(n, -1)).to(dev)  # noqa: E731
         self.roots, self.sets = u8(roots), u8(sets)
         self.players = torch.from_numpy(self.players_np.copy()).to(dev)
