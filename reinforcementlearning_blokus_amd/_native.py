@@ -191,7 +191,10 @@ def orient_table():
     return out
 
 
-POW_FIX_ROWS = 16385  # FastMCTS UCB bit-exact for searches of up to 16,384 iterations
+# FastMCTS UCB bit-exact for searches of up to 65,536 iterations (a 65,537-row table takes
+# ~7 s to build once per process and 7 MB; an arena seat at thinking_time_ms=1000 and the
+# default iterations_per_ms=20 needs 20,001 rows).  Beyond it gpu.fastmcts warns.
+POW_FIX_ROWS = 65537
 _POW_FIX = {"lt": np.zeros(0), "off": np.zeros(1, np.int32), "ent": np.zeros(0, np.int32)}
 
 

@@ -331,7 +331,8 @@ _SEARCH_KINDS = ("mcts", "fast_mcts", "gameplay_fast_mcts", "gameplay_mcts")
 
 def _batchable(run_config: RunConfig, seats: Mapping[str, str]) -> bool:
     """run_games_batched can play this seating: random / default-weight heuristic seats
-    each with their own agent (a stream per seat), search seats of the supported kinds."""
+    each with their own agent (a stream per seat), search seats of the supported kinds
+    (FastMCTS kinds only with deterministic_time_budget, the default)."""
     cfgs = {a.name: a for a in run_config.agents}
     names = list(seats.values())
     for name in set(names):
@@ -341,6 +342,10 @@ def _batchable(run_config: RunConfig, seats: Mapping[str, str]) -> bool:
             if names.count(name) > 1 or (kind == "heuristic" and c.params.get("weights")):
                 return False
         elif kind not in _SEARCH_KINDS:
+            return False
+        elif kind != "mcts" and not bool(c.params.get("deterministic_time_budget", True)):
+            # a wall-clock FastMCTS budget: its iteration count depends on the seat's own
+            # timing (arena_runner.py:352-369), so it plays in the host loop
             return False
     return True
 

@@ -6,6 +6,8 @@ implementation behind any of these functions.
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 
 from . import _native as N
@@ -264,7 +266,14 @@ class BlokusGPU:
         b = np.ascontiguousarray(base, dtype=np.float64)
         assert mt_state.dtype == np.uint32 and mt_state.shape == (n, 625) and mt_state.flags.c_contiguous
         lt = np.ascontiguousarray(log_table, dtype=np.float64)
-        fo, fe = N.pow_half_fix(lt, rows=int(it.max(initial=0)), cached_only=not exact_ucb)
+        need = int(it.max(initial=0))
+        fo, fe = N.pow_half_fix(lt, rows=need, cached_only=not exact_ucb)
+        if exact_ucb and len(fo) - 1 < need:
+            # parent visits >= the table's rows use plain sqrt: the UCB of a child can be one
+            # ulp off CPython's (2*log(N)/v) ** 0.5 there, so a near-tie may pick another child
+            warnings.warn(f"FastMCTS: {need} iterations exceed the {len(fo) - 1} pow-correction rows "
+                          "(_native.POW_FIX_ROWS); UCB1 is bit-exact only below that", RuntimeWarning,
+                          stacklevel=2)
         out = np.zeros(n, dtype=N.FASTMCTS_OUT_DTYPE)
         vis = np.zeros(max(int(off[-1]), 1), dtype=np.int32) if want_visits else None
         self.handle.set_stream(None)

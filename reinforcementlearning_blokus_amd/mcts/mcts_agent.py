@@ -28,7 +28,9 @@ The learned-evaluator options of the reference are out of scope and rejected.
 """
 from __future__ import annotations
 
+import math
 import time
+import warnings
 from typing import Any, Dict, List, Optional
 
 import numpy as np
@@ -56,6 +58,13 @@ def _search_policy(agent) -> Optional[int]:
 def _positions(move: Move) -> List[Position]:
     shape = get_shared_generator().piece_orientations_cache[move.piece_id][move.orientation]
     return [Position(move.anchor_row + int(r), move.anchor_col + int(c)) for r, c in zip(*np.nonzero(shape))]
+
+
+# Timed searches (time_limit): iteration bound per second of limit, and overall.  One
+# search runs ~100-1,000 iterations/s on the GPU (a lane of a persistent wave), so the
+# bound is not reached in practice; if it is, stats say so and a warning is issued.
+TIMED_MAX_ITERS_PER_S = 20000
+TIMED_MAX_ITERS = 1 << 18
 
 
 class MCTSNode:
@@ -224,14 +233,21 @@ class MCTSAgent:
         for i, a in enumerate(agents):
             if a.rollout_backend != "search":
                 raise ValueError("search_batch needs rollout_backend='search' agents")
-            # time_limit (seconds, mcts_agent.py:325-333): iterate until it runs out; the
-            # kernel stops each search at the first iteration boundary past it, with the
-            # iteration count bounded by `iterations` (the node pool / log table size)
+            # time_limit (seconds, mcts_agent.py:325-333, :349-356): iterate until it runs
+            # out, ignoring `iterations`, as _run_mcts_with_time_limit does.  The kernel stops
+            # each search at the first iteration boundary past the limit; the launch still
+            # needs an iteration bound to size the node pool / log table / reward buffers,
+            # so a timed search gets time_limit x TIMED_MAX_ITERS_PER_S (far above what one
+            # search reaches on the GPU); stats["iteration_bound_reached"] reports a search
+            # that hit the bound before its time ran out
             tl_us = int(round(float(a.time_limit) * 1e6)) if a.time_limit else 0
+            iters = int(a.iterations)
+            if tl_us:
+                iters = int(min(TIMED_MAX_ITERS, max(16, math.ceil(float(a.time_limit) * TIMED_MAX_ITERS_PER_S))))
             policy = _search_policy(a.rollout_agent)
             if policy is None:
                 raise ValueError("search_batch: the rollout agent cannot be replayed on the GPU")
-            key = (int(a.iterations), a.max_rollout_moves, float(a.exploration_constant), a.use_transposition_table,
+            key = (iters, a.max_rollout_moves, float(a.exploration_constant), a.use_transposition_table,
                    tl_us, policy)
             groups.setdefault(key, []).append(i)
         for (iters, max_roll, c, use_tt, tl_us, policy), idx in groups.items():
@@ -270,6 +286,12 @@ class MCTSAgent:
                 hits = r["hit_flags"][j, :int(o["iterations_run"])]
                 rew = r["rewards"][j, :int(o["iterations_run"])]
                 a.stats["iterations_run"] = int(o["iterations_run"])
+                if tl_us:
+                    a.stats["iteration_bound"] = iters
+                    a.stats["iteration_bound_reached"] = int(o["iterations_run"]) >= iters
+                    if a.stats["iteration_bound_reached"]:
+                        warnings.warn(f"MCTSAgent: a {a.time_limit} s search stopped at its {iters}-iteration "
+                                      "bound before the time ran out", RuntimeWarning, stacklevel=2)
                 a.stats["time_elapsed"] = dt
                 a.stats["transposition_hits"] += int(o["tt_hits"])
                 a.stats["rollout_rewards"].extend(float(x) for x in rew[hits == 0])

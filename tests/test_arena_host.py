@@ -50,3 +50,41 @@ def test_legacy_config_shape():
     cfg = RunConfig.from_dict({"a": {"type": "random"}, "b": {"type": "random", "time_limit": 0.2},
                                "c": {"type": "random"}, "d": {"type": "random"}, "num_games": 3, "seed": 1})
     assert cfg.agent_names == ["a", "b", "c", "d"] and cfg.agents[1].thinking_time_ms == 200
+
+
+@pytest.mark.parametrize("kind", ["fast_mcts", "gameplay_fast_mcts"])
+def test_wall_clock_fastmcts_seat_plays_in_host_loop(kind, tmp_path, monkeypatch):
+    """A FastMCTS seat with deterministic_time_budget false has a wall-clock iteration
+    count (arena_runner.py:352-369): run_experiment must send its games to the host loop
+    (run_single_game), never to run_games_batched, which needs fixed iteration counts."""
+    from reinforcementlearning_blokus_amd.arena import runner
+    calls = {"batched": 0, "single": 0}
+
+    def fake_batched(*a, **k):
+        calls["batched"] += 1
+        raise AssertionError("batched path taken")
+
+    def fake_single(*, game_index, game_seed, seat_assignment, **k):
+        calls["single"] += 1
+        return {"game_index": game_index, "game_seed": game_seed, "seat_assignment": seat_assignment,
+                "final_scores": {}, "winner_ids": [], "winner_agents": [], "is_tie": False,
+                "moves_made": 0, "error": None, "agent_move_stats": {}}
+
+    monkeypatch.setattr(runner, "run_games_batched", fake_batched)
+    monkeypatch.setattr(runner, "run_single_game", fake_single)
+    monkeypatch.setattr(runner, "compute_summary", lambda records, **k: {"completed_games": len(records)})
+    cfg = RunConfig.from_dict({"agents": [
+        {"name": "r", "type": "random"}, {"name": "h", "type": "heuristic"},
+        {"name": "m", "type": "mcts", "params": {"iterations": 8}},
+        {"name": "f", "type": kind, "thinking_time_ms": 20, "params": {"deterministic_time_budget": False}}],
+        "num_games": 3, "seed": 5, "seat_policy": "round_robin", "output_root": str(tmp_path)})
+    seats = seat_assignment_for_game(cfg.agent_names, 0, game_seed_from_run_seed(5, 0), "round_robin")
+    assert not runner._batchable(cfg, seats)
+    runner.run_experiment(cfg)
+    assert calls == {"batched": 0, "single": 3}
+    cfg2 = RunConfig.from_dict(dict(cfg.to_dict(), agents=[
+        {"name": "r", "type": "random"}, {"name": "h", "type": "heuristic"},
+        {"name": "m", "type": "mcts", "params": {"iterations": 8}},
+        {"name": "f", "type": kind, "thinking_time_ms": 20}]))
+    seats2 = seat_assignment_for_game(cfg2.agent_names, 0, game_seed_from_run_seed(5, 0), "round_robin")
+    assert runner._batchable(cfg2, seats2)

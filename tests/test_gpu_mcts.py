@@ -204,8 +204,8 @@ def test_agent_search_batch_equals_sequential():
 
 def test_agent_time_limit_runs_on_the_search_backend():
     """MCTSAgent(time_limit=..., rollout_agent=RandomAgent) -- a valid reference
-    configuration (mcts_agent.py:327-333) -- searches on the GPU until the limit (bounded
-    by `iterations`) and returns one of the legal moves."""
+    configuration (mcts_agent.py:327-333) -- searches on the GPU until the limit and
+    returns one of the legal moves."""
     from reinforcementlearning_blokus_amd.agents.random_agent import RandomAgent
     from reinforcementlearning_blokus_amd.engine.board import Player
     from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator, move_to_int
@@ -220,3 +220,23 @@ def test_agent_time_limit_runs_on_the_search_backend():
     mv = agent.select_action(board, cur, legal)
     assert move_to_int(mv) in {move_to_int(m) for m in legal}
     assert 1 <= agent.stats["iterations_run"] < 100000
+
+
+def test_agent_time_limit_ignores_iterations():
+    """_run_mcts_with_time_limit (mcts_agent.py:349-356) loops until the time is up and
+    never looks at `iterations`: MCTSAgent(iterations=4, time_limit=0.2) searches far
+    more than 4 iterations, and the iteration bound the launch needs is not reached."""
+    from reinforcementlearning_blokus_amd.agents.random_agent import RandomAgent
+    from reinforcementlearning_blokus_amd.engine.board import Player
+    from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator, move_to_int
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
+    from tests.helpers import engine_board
+    rec = POS[20]
+    board = engine_board(rec)
+    cur = Player(rec["state"]["current_player"])
+    legal = get_shared_generator().get_legal_moves(board, cur)
+    agent = MCTSAgent(iterations=4, time_limit=0.2, rollout_agent=RandomAgent(seed=3), seed=1)
+    mv = agent.select_action(board, cur, legal)
+    assert move_to_int(mv) in {move_to_int(m) for m in legal}
+    assert agent.stats["iterations_run"] > 4
+    assert agent.stats["iteration_bound"] >= 4000 and not agent.stats["iteration_bound_reached"]
