@@ -123,27 +123,42 @@ def ref_python(value, per_core, cores, what):
             "gpu_over_ref_1core": value / per_core, "gpu_over_ref_all_cores": value / (per_core * cores)}
 
 
-def cpu_baseline_playouts(roots_np, seconds, order):
+def cpu_baseline_playouts(roots_np, seconds, order, rollouts, seed=None, gpu_out=None):
     """oracle/blokus_oracle.c (C restatement of the reference engine) timed on this
     host's cores on a bounded sample of the same workload, in the SAME move order as the
-    GPU line, game-over check after every move like the reference."""
+    GPU line, game-over check after every move like the reference.  Naive order: the
+    sample is the first playouts of the last timed step -- same roots (root i //
+    rollouts), same Philox streams (seed, playout id) -- so the CPU plays exactly the
+    GPU's games, and their result records are compared (gpu_out: that step's uint8
+    [n, 32] results)."""
     from oracle import pyoracle as O
     cpu = host_cpu()
     threads = cpu["cores"]
     o = O.ORDER_NAIVE if order == "naive" else O.ORDER_FRONTIER
+    same = order == "naive" and seed is not None
     st = (O.State * len(roots_np)).from_buffer_copy(roots_np.tobytes())
+    kw = dict(threads=threads, order=o)
+    if same:
+        import numpy as np
+        kw.update(rng=O.RNG_PHILOX, root_index=np.arange(len(roots_np) * rollouts, dtype=np.int32) // rollouts)
     n = 8 * threads
     t0 = time.perf_counter()
-    O.batch_playouts(st, n, 1, threads=threads, order=o)
+    O.batch_playouts(st, n, seed if same else 1, **kw)
     dt = time.perf_counter() - t0
     n2 = max(n, int(n * seconds / max(dt, 1e-3)))  # scale the sample to ~`seconds`
+    n2 = min(n2, len(roots_np) * rollouts) if same else n2
     t0 = time.perf_counter()
-    O.batch_playouts(st, n2, 2, threads=threads, order=o)
+    res = O.batch_playouts(st, n2, seed if same else 2, **kw)
     dt = time.perf_counter() - t0
-    return {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
-            "host": cpu, "order": order,
-            "sample": f"{n2} arena playouts from the same {len(roots_np)} roots, oracle/blokus_oracle.c in "
-                      f"{order} move order, {threads} threads (one per usable core), {dt:.1f} s"}
+    out = {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+           "host": cpu, "order": order,
+           "sample": f"{n2} arena playouts from the same {len(roots_np)} roots, oracle/blokus_oracle.c in "
+                     f"{order} move order, {threads} threads (one per usable core), {dt:.1f} s"}
+    if same and gpu_out is not None:
+        g = gpu_out[:n2].cpu().numpy().tobytes()
+        out["sample"] += "; the GPU's own games (same roots and Philox streams as the last timed step)"
+        out["same_games_bit_identical"] = g == bytes(res)
+    return out
 
 
 # ------------------------------------------------------------------ N-rank launch
@@ -342,7 +357,8 @@ def run_config3(args, world, rank, local, dist):
         "compute_roofline": compute_roofline(valu_insts, avg_ms),
     }
     if not args.no_cpu_baseline and world == 1:
-        cb = cpu_baseline_playouts(roots_np, args.cpu_seconds, args.order)
+        cb = cpu_baseline_playouts(roots_np, args.cpu_seconds, args.order, args.rollouts,
+                                   seed=seed * 7919 + 1000 + args.steps - 1, gpu_out=out)
         cb["gpu_over_cpu"] = value / cb["value"]
         cb["reference_python"] = ref_python(value, REF_PY_ARENA_SIMS_PER_CORE, cb["cores"],
                                             "terminal random playout from ply 20, telemetry off")

@@ -565,6 +565,60 @@ static void py_seed_int(or_mt* m, int64_t seed) {
     or_mt_seed_python(m, key, kl);
 }
 
+/* ---------------------------------------------------------- Philox4x32-10 -------
+ * Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1, 2, 3" (SC'11),
+ * the philox4x32 generator of Random123 with 10 rounds: per round
+ *   (hi0, lo0) = M0 * x0, (hi1, lo1) = M1 * x2  (32x32 -> 64-bit products)
+ *   x = {hi1 ^ x1 ^ k0, lo1, hi0 ^ x3 ^ k1, lo0},  then the key is bumped by (W0, W1).
+ * Checked against Random123's published known-answer vectors (tests/test_oracle_philox.py).
+ * The native BK_RNG_PHILOX stream (include/blokus_hip.h) is word 0 of
+ * philox4x32_10({draw counter, playout id, 0x5bd1e995, 0}, {seed lo, seed hi}); the
+ * reference itself uses MT19937 (agents/random_agent.py:29,49), so this stream pins the
+ * native timed path, not a reference stream. */
+void or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t x0 = ctr[0], x1 = ctr[1], x2 = ctr[2], x3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        const uint64_t p0 = (uint64_t)0xD2511F53u * x0, p1 = (uint64_t)0xCD9E8D57u * x2;
+        const uint32_t y0 = (uint32_t)(p1 >> 32) ^ x1 ^ k0, y2 = (uint32_t)(p0 >> 32) ^ x3 ^ k1;
+        x0 = y0; x1 = (uint32_t)p1; x2 = y2; x3 = (uint32_t)p0;
+    }
+    out[0] = x0; out[1] = x1; out[2] = x2; out[3] = x3;
+}
+
+uint32_t or_philox_stream(uint64_t seed, uint32_t pid, uint32_t counter) {
+    const uint32_t c[4] = {counter, pid, 0x5bd1e995u, 0u}, k[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    or_philox4x32_10(c, k, o);
+    return o[0];
+}
+
+/* A seat's random source in the arena loop: numpy RandomState(seed) per seat (the
+ * reference's RandomAgent, agents/random_agent.py:29,49) or the native Philox stream
+ * of one playout (all seats draw from it in turn order).  Either way an index in
+ * [0, n) is the numpy legacy masked rejection: rng = n-1; rng == 0 draws nothing;
+ * else draw u32 & mask until <= rng. */
+typedef struct {
+    int philox;
+    or_mt mt[4];
+    uint64_t seed;
+    uint32_t pid, counter, draws;
+} or_seat_rng;
+
+static int64_t seat_randint(or_seat_rng* r, int seat, int64_t n) {
+    if (!r->philox) return or_np_randint(&r->mt[seat], n);
+    uint32_t rng = (uint32_t)(n - 1);
+    if (rng == 0) return 0;
+    uint32_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t v;
+    do {
+        v = or_philox_stream(r->seed, r->pid, r->counter++) & mask;
+        r->draws++;
+    } while (v > rng);
+    return v;
+}
+
 /* --------------------------------------------------------------- drivers ---------- */
 /* tests/utils_game_states.py:12-57 generate_random_valid_state */
 int or_gen_state(or_board* b, int num_moves, int64_t seed, int32_t* log, int logcap) {
@@ -592,15 +646,16 @@ static int game_over(const or_board* b) {
     return 1;
 }
 
-/* analytics/tournament/arena_runner.py:652-697 with RandomAgent(seed) per seat */
-int or_playout_arena(or_board* b, const uint32_t* seeds4, int order, int max_turns,
-                     bk_result* res, int32_t* trace, int tracecap) {
-    or_mt rng[4];
-    for (int p = 0; p < 4; ++p) or_mt_seed_numpy(&rng[p], seeds4[p]);
+/* analytics/tournament/arena_runner.py:652-697: a player without a move passes, the
+ * game is over when nobody can move (game_over after every move, engine/game.py:182-214).
+ * max_plies >= 0: stop after that many placements instead (bk_advance, BK_SEM_ADVANCE:
+ * the synthetic-root generator, tests/utils_game_states.py:12 with uniform draws). */
+static int arena_loop(or_board* b, or_seat_rng* rng, int order, int max_turns, int max_plies,
+                      bk_result* res, int32_t* trace, int tracecap) {
     static __thread int32_t moves[BK_ORIENTS * 400];
     int passes = 0, turns = 0, nt = 0, plies = 0;
     int over = game_over(b);
-    while (!over && turns < max_turns) {
+    while (!over && turns < max_turns && (max_plies < 0 || plies < max_plies)) {
         int p = b->cur;
         int n = or_legal_moves(b, p, order, moves, BK_ORIENTS * 400);
         ++turns;
@@ -612,20 +667,44 @@ int or_playout_arena(or_board* b, const uint32_t* seeds4, int order, int max_tur
             over = game_over(b);
             continue;
         }
-        int mv = moves[or_np_randint(&rng[p], n)];
+        int mv = moves[seat_randint(rng, p, n)];
         if (trace && nt < tracecap) trace[nt] = mv;
         ++nt;
         or_place_move(b, p, mv);
         ++plies;
         over = game_over(b);
     }
-    memset(res, 0, sizeof *res);
-    int32_t sc[4], wm;
-    or_game_scores(b, sc, &wm);
-    for (int p = 0; p < 4; ++p) res->scores[p] = (int16_t)sc[p];
-    res->winner_mask = (uint8_t)wm;
-    res->plies = (uint16_t)plies; res->passes = (uint16_t)passes; res->turns = (uint16_t)turns;
+    if (res) {
+        memset(res, 0, sizeof *res);
+        int32_t sc[4], wm;
+        or_game_scores(b, sc, &wm);
+        for (int p = 0; p < 4; ++p) res->scores[p] = (int16_t)sc[p];
+        res->winner_mask = (uint8_t)wm;
+        res->plies = (uint16_t)plies; res->passes = (uint16_t)passes; res->turns = (uint16_t)turns;
+        res->draws = rng->draws;
+    }
     return nt;
+}
+
+/* ... with RandomAgent(seeds4[p]) per seat */
+int or_playout_arena(or_board* b, const uint32_t* seeds4, int order, int max_turns,
+                     bk_result* res, int32_t* trace, int tracecap) {
+    or_seat_rng rng;
+    memset(&rng, 0, sizeof rng);
+    for (int p = 0; p < 4; ++p) or_mt_seed_numpy(&rng.mt[p], seeds4[p]);
+    int nt = arena_loop(b, &rng, order, max_turns, -1, res, trace, tracecap);
+    res->draws = 0;  /* not counted for the per-seat streams */
+    return nt;
+}
+
+/* ... with playout `pid`'s Philox stream keyed by `seed` (BK_RNG_PHILOX); max_plies >= 0
+ * is bk_advance's placement budget */
+int or_playout_arena_philox(or_board* b, uint64_t seed, uint32_t pid, int order, int max_turns, int max_plies,
+                            bk_result* res, int32_t* trace, int tracecap) {
+    or_seat_rng rng;
+    memset(&rng, 0, sizeof rng);
+    rng.philox = 1; rng.seed = seed; rng.pid = pid;
+    return arena_loop(b, &rng, order, max_turns, max_plies, res, trace, tracecap);
 }
 
 /* MCTSAgent._rollout, mcts/mcts_agent.py:470-554, rollout_agent = RandomAgent(seed) */
@@ -743,14 +822,18 @@ uint64_t or_zobrist_hash(const or_board* b, const uint64_t* t) {
 /* ------------------------------------------------- CPU baseline batch driver ------- */
 typedef struct {
     const bk_state* roots; int n_roots; int begin, end; uint64_t seed; int sem, max_plies, order;
-    bk_result* out;
+    bk_result* out; const int32_t* root_index; int rng;
 } batch_job;
 
 static void* batch_worker(void* arg) {
     batch_job* j = (batch_job*)arg;
     or_board* b = (or_board*)malloc(sizeof(or_board));
     for (int i = j->begin; i < j->end; ++i) {
-        or_unpack_state(b, &j->roots[i % j->n_roots], NULL, NULL);
+        or_unpack_state(b, &j->roots[j->root_index ? j->root_index[i] : i % j->n_roots], NULL, NULL);
+        if (j->rng == BK_RNG_PHILOX && j->sem == BK_SEM_ARENA) {
+            or_playout_arena_philox(b, j->seed, (uint32_t)i, j->order, j->max_plies, -1, &j->out[i], NULL, 0);
+            continue;
+        }
         uint32_t seeds[4];
         for (int p = 0; p < 4; ++p) seeds[p] = (uint32_t)(j->seed * 2654435761u + (uint64_t)i * 4 + p);
         if (j->sem == BK_SEM_ARENA) {
@@ -768,13 +851,22 @@ static void* batch_worker(void* arg) {
 
 int or_batch_playouts(const bk_state* roots, int n_roots, int n_playouts, uint64_t seed,
                       int semantics, int max_plies, int threads, int order, bk_result* out) {
+    return or_batch_playouts2(roots, n_roots, NULL, n_playouts, seed, semantics, max_plies, threads, order,
+                              BK_RNG_NUMPY_MT, out);
+}
+
+/* root_index[i] (NULL: i mod n_roots) is playout i's root; rng BK_RNG_PHILOX (arena
+ * semantics): playout i draws from Philox stream (seed, i) as bk_rollout does */
+int or_batch_playouts2(const bk_state* roots, int n_roots, const int32_t* root_index, int n_playouts, uint64_t seed,
+                       int semantics, int max_plies, int threads, int order, int rng, bk_result* out) {
     or_init();
     if (threads < 1) threads = 1;
     pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
     batch_job* jobs = (batch_job*)malloc(sizeof(batch_job) * (size_t)threads);
     for (int t = 0; t < threads; ++t) {
         jobs[t] = (batch_job){roots, n_roots, (int)((int64_t)n_playouts * t / threads),
-                              (int)((int64_t)n_playouts * (t + 1) / threads), seed, semantics, max_plies, order, out};
+                              (int)((int64_t)n_playouts * (t + 1) / threads), seed, semantics, max_plies, order, out,
+                              root_index, rng};
         pthread_create(&th[t], NULL, batch_worker, &jobs[t]);
     }
     for (int t = 0; t < threads; ++t) pthread_join(th[t], NULL);

@@ -97,6 +97,12 @@ def lib():
             "or_zobrist_hash": (C.c_uint64, [P(Board), P(C.c_uint64)]),
             "or_batch_playouts": (C.c_int, [P(State), C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
                                             C.c_int, C.c_int, P(Result)]),
+            "or_batch_playouts2": (C.c_int, [P(State), C.c_int, C.c_void_p, C.c_int, C.c_uint64, C.c_int,
+                                             C.c_int, C.c_int, C.c_int, C.c_int, P(Result)]),
+            "or_philox4x32_10": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+            "or_philox_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32]),
+            "or_playout_arena_philox": (C.c_int, [P(Board), C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_int,
+                                                  P(Result), P(C.c_int32), C.c_int]),
             "or_set_frontier_table": (C.c_int, [P(Board), C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
             "or_mcts": (C.c_int, [P(Board), C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int,
                                   C.c_void_p, P(MT), C.c_int, C.c_void_p, C.c_void_p, C.c_int,
@@ -218,6 +224,28 @@ def playout_arena(b, seeds, order=ORDER_FRONTIER, max_turns=2500):
     return res, list(tr[:n])
 
 
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 block (Random123 philox4x32, 10 rounds) -> 4 words."""
+    c, k, o = (C.c_uint32 * 4)(*ctr), (C.c_uint32 * 2)(*key), (C.c_uint32 * 4)()
+    lib().or_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def philox_stream(seed, pid, counter):
+    """Word `counter` of playout `pid`'s BK_RNG_PHILOX stream keyed by `seed`."""
+    return lib().or_philox_stream(seed, pid, counter)
+
+
+def playout_arena_philox(b, seed, pid, order=ORDER_NAIVE, max_turns=2500, max_plies=-1):
+    """Arena playout drawing from the native Philox stream (seed, pid), as bk_rollout
+    (BK_RNG_PHILOX) plays it; max_plies >= 0: bk_advance's placement budget.  The board
+    is advanced in place; returns (Result, trace of moves, -1 = pass)."""
+    res = Result()
+    tr = _i32(4096)
+    n = lib().or_playout_arena_philox(C.byref(b), seed, pid, order, max_turns, max_plies, C.byref(res), tr, 4096)
+    return res, list(tr[:n])
+
+
 def rollout_a(b, player, seed, order=ORDER_FRONTIER, max_moves=50):
     rw, pl, dr = C.c_int32(), C.c_int32(), C.c_int32()
     lib().or_rollout_a(C.byref(b), player, seed, order, max_moves, C.byref(rw), C.byref(pl), C.byref(dr))
@@ -242,9 +270,21 @@ def orient_table():
     return out
 
 
-def batch_playouts(states, n_playouts, seed, semantics=SEM_ARENA, max_plies=2500, threads=1, order=ORDER_FRONTIER):
+RNG_PHILOX, RNG_NUMPY_MT = 0, 1
+
+
+def batch_playouts(states, n_playouts, seed, semantics=SEM_ARENA, max_plies=2500, threads=1, order=ORDER_FRONTIER,
+                   rng=RNG_NUMPY_MT, root_index=None):
+    """n_playouts playouts on `threads` threads; playout i starts from
+    states[root_index[i]] (default i mod len).  rng=RNG_PHILOX (arena semantics): playout
+    i draws from Philox stream (seed, i), exactly the games bk_rollout plays."""
     out = (Result * n_playouts)()
-    lib().or_batch_playouts(states, len(states), n_playouts, seed, semantics, max_plies, threads, order, out)
+    ri = None
+    if root_index is not None:
+        ri = np.ascontiguousarray(root_index, dtype=np.int32)
+        assert len(ri) >= n_playouts
+    lib().or_batch_playouts2(states, len(states), ri.ctypes.data if ri is not None else None, n_playouts, seed,
+                             semantics, max_plies, threads, order, rng, out)
     return out
 
 
