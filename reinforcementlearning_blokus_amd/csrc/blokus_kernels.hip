@@ -280,9 +280,28 @@ struct StencilClass {
 #ifndef ROLL_BLOCKS_PER_CU
 #define ROLL_BLOCKS_PER_CU 3
 #endif
-// frontier-order kernel: 64 dwords per lane; after the move is located the area also
-// stages the mover's frontier table ([slot][lane] int16, up to 128 slots)
-#define ROLL_WORDS_FR (64 * WAVE)
+// frontier tables smaller than this many slots are staged in LDS for place_frontier
+// (0: probe the table in global memory).  k_rollout_fr: 64, so its area stays at the 40
+// dwords per lane the counts and rows need and 3 blocks of 256 lanes fit a CU's LDS (3
+// waves/SIMD); the ~12 % of plies whose mover has a 128-slot table probe it in place.
+// k_mcts (config 5: 65,536 searches = one 256-lane block per CU, LDS to spare): 128.
+#ifndef BK_FS_STAGE_FR
+#define BK_FS_STAGE_FR 64
+#endif
+#ifndef BK_FS_STAGE_MCTS
+#define BK_FS_STAGE_MCTS 128
+#endif
+// frontier-order kernels: per lane max(40, stage / 2) dwords; after the move is located
+// the area also stages the mover's frontier table ([slot pair][lane])
+#define ROLL_WORDS_STAGE(S) (((S) / 2 > 40 ? (S) / 2 : 40) * WAVE)
+#define ROLL_WORDS_FR ROLL_WORDS_STAGE(BK_FS_STAGE_FR)
+// resident 256-lane blocks per CU of k_rollout_fr / k_mcts (the launch bound; <= 168 VGPRs at 3)
+#ifndef FR_BLOCKS_PER_CU
+#define FR_BLOCKS_PER_CU 3
+#endif
+#ifndef MCTS_BLOCKS_PER_CU
+#define MCTS_BLOCKS_PER_CU 2
+#endif
 
 // Legal-move counts of one board-player for the class's table entries [i0, i1); with
 // STORE, also the per-orientation counts (cl = this lane's dword 0, stride WAVE).
@@ -1020,31 +1039,27 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
 }
 
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch
-// frontier tables smaller than this many slots are staged in LDS for place_frontier
-// (0: probe the table in global memory)
-#ifndef BK_FS_STAGE_MAX
-#define BK_FS_STAGE_MAX 128
-#endif
 struct FsLane {
     bk_fset s;
     int16_t tmp[BK_FSET_SLOTS];
 };
 
 // update_frontier_after_move (engine/board.py:315-367) of player p's table in fl for a
-// piece at cells[0..n): the ops marked in `real` (frontier_ops).  A table of <= 128
+// piece at cells[0..n): the ops marked in `real` (frontier_ops).  A table of < STAGE
 // slots is staged in LDS so the probe chains wait on LDS, not L2/HBM: lk = this lane's dword of [slot pair][lane] (slots 2j, 2j + 1 in dword j *
 // WAVE): one ds_write_b32 / ds_read_b32 per slot pair, and a probe of ANY slot by each
-// lane hits bank `lane` (conflict-free).  A 256-slot table (or a move that grows one
-// past 128) is updated in place.  false: table overflow.
+// lane hits bank `lane` (conflict-free).  A larger table (or a move that grows one past
+// the stage) is updated in place.  false: table overflow.
+template <int STAGE>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
                                                const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
     const uint32_t gmask = gfs->mask[p];
     bk_u32_alias* lw = reinterpret_cast<bk_u32_alias*>(lk);
-    if (BK_FS_STAGE_MAX > 0 && gmask < (uint32_t)BK_FS_STAGE_MAX) {
+    if (STAGE > 0 && gmask < (uint32_t)STAGE) {
         const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < STAGE / 8; ++i) {
             if ((uint32_t)(8 * i) <= gmask) {
                 const uint4 v = src4[i];
                 lw[(4 * i + 0) * WAVE] = v.x;
@@ -1054,11 +1069,11 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
             }
         }
         uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
-        FsetRef t{lk, 2 * WAVE, &m, &f, &u, 128u, htab};
+        FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab};
         if (fs_run_ops(t, fl->tmp, cells, real)) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < STAGE / 8; ++i) {
                 if ((uint32_t)(8 * i) <= m)
                     dst4[i] = make_uint4(lw[(4 * i + 0) * WAVE], lw[(4 * i + 1) * WAVE], lw[(4 * i + 2) * WAVE],
                                          lw[(4 * i + 3) * WAVE]);
@@ -1921,7 +1936,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             // before the table staging reuses the area
             const uint64_t real = frontier_ops(rows_lds, slab, p, (g.first >> p) & 1u, gs, ar, ac, m);
             int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + 2 * lane;
-            if (!place_frontier(&a.fslab[slot], p, lk, htab, cells, real)) g.status |= 2u;
+            // (HEUR: the area holds 84 dwords per lane, a 128-slot stage fits)
+            if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real)) g.status |= 2u;
         }
         SECT(6);
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
@@ -1941,7 +1957,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
 __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_rollout(RolloutArgs a) { rollout_body<false>(a); }
 __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_advance(RolloutArgs a) { rollout_body<false>(a); }
 // reference frontier order (compat parity mode)
-__global__ __launch_bounds__(BLOCK, 2) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
+__global__ __launch_bounds__(BLOCK, FR_BLOCKS_PER_CU) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
 // reference frontier order with HeuristicAgent seats (cfg.heuristic_seats)
 __global__ __launch_bounds__(HBLOCK, 2) void k_rollout_fr_h(RolloutArgs a) { rollout_body<true, true>(a); }
 
@@ -2192,6 +2208,7 @@ struct MctsArgs {
     uint64_t max_steps;
     uint64_t limit_ticks;  // cfg.time_limit_us in wall-clock (s_memrealtime) ticks
     int32_t tree_batch;    // tree phase once this many lanes of a wave wait for it (or no lane is busy)
+    int32_t spread;        // only lanes with lane % spread == 0 take searches (more waves, fewer lanes each)
 };
 
 struct Mc {
@@ -2315,7 +2332,7 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
             slab.at(4, ar + d) |= pm[d];
         }
     }
-    const bool ok = place_frontier(T, p, lk, htab, cells, real);
+    const bool ok = place_frontier<BK_FS_STAGE_MCTS>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
     m.first &= ~(1u << p);
@@ -2581,7 +2598,7 @@ __device__ __forceinline__ double mc_random_sample(uint32_t* st, uint32_t& pos) 
 template <bool HEUR>
 __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     constexpr int BLK = HEUR ? HBLOCK : BLOCK;
-    constexpr int AREA = HEUR ? HEUR_WORDS : ROLL_WORDS_FR;
+    constexpr int AREA = HEUR ? HEUR_WORDS : ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS);
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
     // per wave: counts / B,C rows (+ HEUR: per-piece e sums) / the staged frontier table
     __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + 2 * BK_CELLS + HS_WORDS];
@@ -2601,7 +2618,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     Mc m;
     m.game = -1;
     m.mode = MC_SELECT;
-    bool done = false;
+    bool done = (lane % a.spread) != 0;
     SECT_DECL
     for (uint64_t step = 0;; ++step) {
         SECT(13);
@@ -2785,7 +2802,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     SECT_FLUSH;
 }
 
-__global__ __launch_bounds__(BLOCK, 2) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
+__global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
 __global__ __launch_bounds__(HBLOCK, 2) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
 
 // ------------------------------------------------------------------------------------
@@ -2811,6 +2828,8 @@ struct bk_handle_s {
     uint32_t* d_counter = nullptr;
     int num_cu = 0;
     int rollout_blocks_per_cu = 0;
+    int fr_blocks_per_cu = 0;    // k_rollout_fr
+    int mcts_blocks_per_cu = 0;  // k_mcts
 };
 
 static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
@@ -2878,6 +2897,18 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
     if (const char* env = getenv("BK_BLOCKS_PER_CU")) {  // tuning override
         const int v = atoi(env);
         if (v > 0 && v < bpc) h->rollout_blocks_per_cu = v;
+    }
+    // resident blocks of the frontier-order kernels, from their real register / LDS use
+    bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_rollout_fr, BLOCK, 0) != hipSuccess || bpc < 1) bpc = 1;
+    h->fr_blocks_per_cu = bpc;
+    bpc = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_mcts, BLOCK, 0) != hipSuccess || bpc < 1) bpc = 1;
+    h->mcts_blocks_per_cu = bpc;
+    if (const char* env = getenv("BK_FR_BLOCKS_PER_CU")) {  // tuning override (both kernels)
+        const int v = atoi(env);
+        if (v > 0 && v < h->fr_blocks_per_cu) h->fr_blocks_per_cu = v;
+        if (v > 0 && v < h->mcts_blocks_per_cu) h->mcts_blocks_per_cu = v;
     }
     h->cur = h->own;
     *out = h;
@@ -3116,7 +3147,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     // persistent grid: every resident slot pulls playouts from the counter
     const bool heur = fr && ((cfg->heuristic_seats & 0xF) != 0 || seat_masks != nullptr);
     const int blk = heur ? HBLOCK : BLOCK;
-    int blocks = h->num_cu * (heur ? 3 : fr ? 2 : h->rollout_blocks_per_cu);
+    int blocks = h->num_cu * (heur ? 3 : fr ? h->fr_blocks_per_cu : h->rollout_blocks_per_cu);
     const int need = (n_playouts + blk - 1) / blk;
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
@@ -3530,8 +3561,15 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     // persistent grid: every resident slot pulls whole searches from the counter
     const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;
     const int blk = heur ? HBLOCK : BLOCK;
-    int blocks = h->num_cu * (heur ? 3 : 2);
-    const int need = (n_games + blk - 1) / blk;
+    int blocks = h->num_cu * (heur ? 3 : h->mcts_blocks_per_cu);
+    // k_mcts is latency-bound at one wave per SIMD (config 5: 65,536 searches fill one
+    // 256-lane block per CU): when the resident slots allow, every other lane takes a
+    // search, so twice the waves hide each other's latency (11.14 vs 10.84 M sims/s,
+    // profiles/r03/sweeps/mcts_spread.jsonl; 4 measured slower)
+    int spread = (!heur && (int64_t)n_games * 2 <= (int64_t)blocks * blk) ? 2 : 1;
+    if (const char* env = getenv("BK_MCTS_SPREAD")) spread = atoi(env);  // tuning override
+    if (spread < 1 || spread > WAVE || (spread & (spread - 1))) spread = 1;
+    const int need = (int)(((int64_t)n_games * spread + blk - 1) / blk);
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
     const uint32_t nslots = (uint32_t)blocks * blk;
@@ -3543,7 +3581,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     HIPCHK(h, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, h->device));
     if (khz <= 0) khz = 100000;
     HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
-    const uint64_t per_lane = ((uint64_t)n_games + nslots - 1) / nslots + 1;
+    const uint64_t per_lane = ((uint64_t)n_games * spread + nslots - 1) / nslots + 1;
     // a waiting lane waits at most one simulation of the others (2x)
     const uint64_t steps = 2 * per_lane * ((uint64_t)cfg->iterations + 1) * ((uint64_t)cfg->max_rollout_moves + 2) + 64;
     int32_t tree_batch = MC_TREE_BATCH;
@@ -3555,7 +3593,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (int32_t*)sec[9].dev, (const double*)sec[10].dev, log_len, (bk_mcts_node*)sec[11].dev,
                (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
-               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch};
+               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (heur)
         hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
