@@ -407,9 +407,10 @@ def run_config5(args, world, rank, local, dist):
     res = batch.results()
     sims_local = int(res["iterations_run"].sum()) * args.steps
     plies_local = int(res["rollout_plies"].astype(np.int64).sum())
-    elapsed, (sims, plies, hits, rollouts) = reduce_max_sum(
+    unc_local = int(((res["status"] & N.MCTS_EUNCERT) != 0).sum())  # heuristic rollouts only
+    elapsed, (sims, plies, hits, rollouts, unc) = reduce_max_sum(
         dist, dev, elapsed, [sims_local, plies_local * args.steps, int(res["tt_hits"].sum()) * args.steps,
-                             int(res["rollouts"].sum()) * args.steps])
+                             int(res["rollouts"].sum()) * args.steps, unc_local])
     del stream
     if rank != 0:
         return None
@@ -435,6 +436,9 @@ def run_config5(args, world, rank, local, dist):
                    "games": total, "iterations": args.iterations, "chunk": args.chunk,
                    "simulations_per_step": total * args.iterations,
                    "rollout_plies_per_sim": plies / sims, "tt_hit_rate": hits / sims,
+                   # searches with a HeuristicAgent draw within 2^-40 of a probability boundary
+                   # (BK_MCTS_EUNCERT; 0 = every choice certified equal to the reference's)
+                   "uncertified_searches": int(unc) if heur else None,
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
@@ -554,6 +558,7 @@ def run_config4(args, world, rank, local, dist):
                                "round-robin, MCTS 64 iterations/move (heuristic rollouts), FastMCTS 1,000 "
                                "iterations/move, lockstep batches (bk_arena_advance + bk_mcts + bk_fastmcts)",
                    "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
+                   "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
                    "rank0_phase_seconds": phases,
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "reference_python": {"value": 1.0 / 20.3, "unit": "games/s/core",

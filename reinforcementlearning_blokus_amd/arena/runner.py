@@ -11,6 +11,7 @@ from __future__ import annotations
 import json
 import random
 import time
+import warnings
 import traceback
 from datetime import datetime
 from pathlib import Path
@@ -408,7 +409,12 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     active = np.arange(n)
     prof = LAST_BATCH_PROFILE
     prof.clear()
-    prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0)
+    # uncertified_heuristic: advance launches whose game had a HeuristicAgent draw within
+    # 2^-40 of a cumulative-probability boundary (bk_result status bit 4), plus MCTS searches
+    # with such a rollout draw (BK_MCTS_EUNCERT): the choice is the exact-arithmetic one,
+    # but a host's rounding could pick the neighbour (HeuristicAgent)
+    prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0,
+                uncertified_heuristic=0)
     while len(active):
         prof["rounds"] += 1
         if progress is not None:
@@ -422,6 +428,8 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
         stopped = []
         for j, i in enumerate(active):
             r = res[j]
+            if int(r["status"]) & N.STATUS_UNCERT:
+                prof["uncertified_heuristic"] += 1
             if int(r["status"]) & N.STATUS_STOP:
                 stopped.append(i)
                 continue
@@ -467,6 +475,8 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                     tm = time.perf_counter()
                     mv = MCTSAgent.search_packed([t[1].agent for t in todo], states[ti], sets[ti], [t[2] for t in todo])
                     prof["mcts_s"] += time.perf_counter() - tm
+                    prof["uncertified_heuristic"] += sum(int(t[1].agent.stats.get("last_search_uncertified", False))
+                                                         for t in todo)
                     for (i, a, p, lg), m in zip(todo, mv):
                         chosen[i] = m
                         e = per_agent[i][seats[i][str(p + 1)]]
@@ -515,6 +525,10 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
     prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"]
+    if prof["uncertified_heuristic"]:
+        warnings.warn(f"run_games_batched: {prof['uncertified_heuristic']} HeuristicAgent draw(s) fell within 2^-40 "
+                      "of a probability boundary (choice not certified equal to the reference's on every host)",
+                      RuntimeWarning, stacklevel=2)
     out = []
     for i, gi in enumerate(idx):
         r, turns, passes, truncated = results[i]

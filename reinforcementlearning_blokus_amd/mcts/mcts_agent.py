@@ -166,6 +166,7 @@ class MCTSAgent:
     @staticmethod
     def _fresh_stats():
         return {"iterations_run": 0, "time_elapsed": 0.0, "transposition_hits": 0, "rollout_rewards": [],
+                "uncertified_searches": 0, "last_search_uncertified": False,
                 "leaf_eval_calls": 0, "progressive_bias_updates": 0, "potential_shaping_terms": [],
                 "evaluator_errors": 0}
 
@@ -286,6 +287,11 @@ class MCTSAgent:
                 hits = r["hit_flags"][j, :int(o["iterations_run"])]
                 rew = r["rewards"][j, :int(o["iterations_run"])]
                 a.stats["iterations_run"] = int(o["iterations_run"])
+                # HeuristicAgent rollouts: a draw within 2^-40 of a probability boundary
+                # (BK_MCTS_EUNCERT; the kernel flags the search, it does not count draws)
+                unc = bool(int(o["status"]) & N.MCTS_EUNCERT)
+                a.stats["last_search_uncertified"] = unc
+                a.stats["uncertified_searches"] = a.stats.get("uncertified_searches", 0) + int(unc)
                 if tl_us:
                     a.stats["iteration_bound"] = iters
                     a.stats["iteration_bound_reached"] = int(o["iterations_run"]) >= iters

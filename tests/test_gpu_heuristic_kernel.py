@@ -136,3 +136,74 @@ def test_mcts_heuristic_rollouts_match_reference(gpu, case):
     assert rew == c["rollout_rewards"]
     assert int(o["tt_hits"]) == c["transposition_hits"]
     assert int(mt[0, 624]) == c["rng_pos"] and sha_ints(mt[0, :624].tolist()) == c["rng_sha"]
+
+
+def _temper(y):
+    y ^= y >> 11
+    y ^= (y << 7) & 0x9D2C5680
+    y ^= (y << 15) & 0xEFC60000
+    y ^= y >> 18
+    return y & 0xFFFFFFFF
+
+
+def _untemper(y):
+    y ^= y >> 18
+    y ^= (y << 15) & 0xEFC60000
+    t = y
+    for _ in range(5):
+        t = y ^ ((t << 7) & 0x9D2C5680)
+    y = t & 0xFFFFFFFF
+    t = y
+    for _ in range(3):
+        t = y ^ (t >> 11)
+    return t & 0xFFFFFFFF
+
+
+def _mt_state_for(u53):
+    """A RandomState MT19937 state whose next random_sample() is exactly u53 / 2**53
+    (genrand_res53 of words 622 and 623, no twist before them)."""
+    key = np.random.RandomState(7).get_state()[1].copy()
+    a, b = (u53 >> 26) << 5, (u53 & ((1 << 26) - 1)) << 6
+    key[622], key[623] = _untemper(a), _untemper(b)
+    assert _temper(int(key[622])) == a and _temper(int(key[623])) == b
+    return ("MT19937", key, 622, 0, 0.0)
+
+
+@pytest.mark.parametrize("on_boundary", [True, False])
+def test_uncertified_heuristic_draw_is_flagged_and_reported(on_boundary):
+    """A HeuristicAgent rollout draw placed (by constructing the agent's MT state) exactly
+    on a cumulative-probability boundary of the first rollout ply: the kernel cannot
+    certify that every host's rounding picks its index, sets BK_MCTS_EUNCERT, and
+    MCTSAgent.stats reports the search ("uncertified_searches").  The same draw moved to
+    the middle of the interval is certified (reported as zero).
+    Reference: agents/heuristic_agent.py:61-65 (rng.choice), :223-244 (softmax);
+    mcts/mcts_agent.py:113-145 (expand pops the last move), :470-554 (_rollout)."""
+    from reinforcementlearning_blokus_amd.agents.heuristic_agent import HeuristicAgent
+    from reinforcementlearning_blokus_amd.engine.board import Player
+    from reinforcementlearning_blokus_amd.engine.move_generator import get_shared_generator
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import MCTSAgent
+    from tests.helpers import POS, engine_board
+    gen = get_shared_generator()
+    rec = POS[20]
+    board = engine_board(rec)
+    cur = Player(rec["state"]["current_player"])
+    legal = gen.get_legal_moves(board, cur)
+    # iteration 1 expands the root's LAST legal move; the rollout starts with the next seat
+    child = board.copy()
+    mv = legal[-1]
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import _positions
+    child.place_piece(_positions(mv), cur, mv.piece_id, validate=False)
+    nxt = Player(cur.value % 4 + 1)
+    l1 = gen.get_legal_moves(child, nxt)
+    h = HeuristicAgent(seed=0)
+    p = h._softmax(h.score_legal_moves(child, nxt, l1), temperature=1.0)
+    cdf = np.cumsum(p)
+    cdf /= cdf[-1]
+    j = len(l1) // 2
+    u = cdf[j] if on_boundary else 0.5 * (cdf[j - 1] + cdf[j])
+    agent = MCTSAgent(iterations=1, rollout_agent=HeuristicAgent(seed=1), seed=3)
+    agent.rollout_agent.rng.set_state(_mt_state_for(int(round(u * 2.0 ** 53))))
+    agent.select_action(board, cur, legal)
+    assert agent.stats["iterations_run"] == 1
+    assert agent.stats["last_search_uncertified"] is on_boundary
+    assert agent.stats["uncertified_searches"] == int(on_boundary)
