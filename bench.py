@@ -15,7 +15,7 @@ Other workloads (one JSON line each, same contract):
                       over the ranks (strong scaling).
   --workload config2  BASELINE.json configs[1]: batched legal-move generation for 4,096
                       synthetic mid-game boards (plies 16..40), player to move (and
-                      --all-players: all 4); one step = one bk_movegen launch.
+                      --all-players: all 4); one step = one bk_movegen_mask launch.
 
 N>1: one process per GPU, weak scaling for config3 (each rank plays its own 256 games,
 no data-path collective); after the timed region the per-rank results are all-gathered
@@ -598,13 +598,13 @@ def run_config2(args, world, rank, local, dist):
     stream = torch.cuda.Stream(dev)
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
-            cnt, rows = gpu.movegen(states, players)
+            cnt, masks = gpu.movegen_mask(states, players)
         barrier_sync(dist)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(stream)
         for _ in range(args.steps):
-            cnt, rows = gpu.movegen(states, players)
+            cnt, masks = gpu.movegen_mask(states, players)
         e1.record(stream)
         barrier_sync(dist)
         elapsed = time.perf_counter() - t0
@@ -615,7 +615,7 @@ def run_config2(args, world, rank, local, dist):
         return None
     value = pairs / elapsed
     achieved = n * MOVEGEN_B / (kernel_ms * 1e-3) / 1e9
-    traffic, valu_insts = traffic_for("k_movegen_g")
+    traffic, valu_insts = traffic_for("k_movegen_m")
     line = {
         "metric": "batched legal-move generation (board-players/s, 20x20, 4p)", "value": value,
         "unit": "board-players/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -623,13 +623,14 @@ def run_config2(args, world, rank, local, dist):
         "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": f"config2: {nb} synthetic mid-game boards (plies 16..40) x "
                                f"{'all 4 players' if args.all_players else 'player to move'}: dense legal "
-                               "masks + counts (bk_movegen)", "boards": nb, "board_players": n,
+                               "masks, 91 x 7 u64 per board-player, + counts (bk_movegen_mask)",
+                   "boards": nb, "board_players": n,
                    "legal_moves_per_board_player": moves / n, "us_per_batch": kernel_ms * 1e3,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen_g",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen_m",
                      "kernel_ms": kernel_ms, "bytes_per_board_player": MOVEGEN_B,
-                     "bytes_written_per_board_player": 256 + 91 * 20 * 4 + 4},
+                     "bytes_written_per_board_player": 91 * 7 * 8 + 4},
         "compute_roofline": compute_roofline(valu_insts, kernel_ms),
     }
     if not args.no_cpu_baseline and world == 1:

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 2
+#define BK_ABI_VERSION 3
 #define BK_BOARD 20
 #define BK_CELLS 400
 #define BK_PLAYERS 4
@@ -155,6 +155,19 @@ int bk_orient_info(int g, int32_t* piece_id, int32_t* orient, int32_t* ncells, i
  */
 int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int32_t n,
                uint32_t* out_rows, uint32_t* out_count, int mem);
+
+/*
+ * The same legal-move sets as dense 400-bit masks (the SURVEY 8(b) bk_movegen form):
+ *   out_mask  : n x 91 x 7 uint64; bit b of word w is cell 64 w + b = r * 20 + c (the
+ *               numbering of Board.player_bits, engine/bitboard.py:19-40): orientation g
+ *               anchored at (r, c) is legal.  Bits 400..447 are zero.  5,096 B per
+ *               board-player; 8-byte aligned; may be NULL (counts only)
+ *   out_count : n uint32 total legal moves; may be NULL
+ * Replaces LegalMoveGenerator.get_legal_moves (engine/move_generator.py:130-151, the set;
+ * the host orders it).  ABI version 3.
+ */
+int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players, int32_t n,
+                    uint64_t* out_mask, uint32_t* out_count, int mem);
 
 /* has_legal_moves for all 4 players of n states (move_generator.py:961): out_mask4[i]
    bit p set if player p has a legal move. */

@@ -28,7 +28,7 @@ STREAM_OWN = (1 << 64) - 1  # BK_STREAM_OWN
 # every symbol include/blokus_hip.h declares
 EXPORTS = (
     "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream",
-    "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_has_moves",
+    "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_movegen_mask", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
@@ -108,7 +108,7 @@ RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("statu
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
 assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
 
-ABI_VERSION = 2  # include/blokus_hip.h BK_ABI_VERSION
+ABI_VERSION = 3  # include/blokus_hip.h BK_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -150,6 +150,7 @@ def load():
             "bk_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
             "bk_orient_info": (C.c_int, [C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
             "bk_movegen": (C.c_int, [vp, vp, vp, C.c_int32, vp, vp, C.c_int]),
+            "bk_movegen_mask": (C.c_int, [vp, vp, vp, C.c_int32, vp, vp, C.c_int]),
             "bk_has_moves": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int]),
             "bk_rollout": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
             "bk_advance": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32, P(BkRolloutCfg), vp, vp, C.c_int]),
@@ -332,6 +333,12 @@ class Handle:
             rc = self._L.bk_movegen(self._h, C.c_void_p(states_ptr), C.c_void_p(players_ptr), n,
                                     C.c_void_p(rows_ptr or 0), C.c_void_p(count_ptr or 0), mem)
         self.check(rc, "bk_movegen")
+
+    def movegen_mask(self, states_ptr, players_ptr, n, mask_ptr, count_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_movegen_mask(self._h, C.c_void_p(states_ptr), C.c_void_p(players_ptr), n,
+                                         C.c_void_p(mask_ptr or 0), C.c_void_p(count_ptr or 0), mem)
+        self.check(rc, "bk_movegen_mask")
 
     def has_moves(self, states_ptr, n, out_ptr, mem):
         with self._lock:

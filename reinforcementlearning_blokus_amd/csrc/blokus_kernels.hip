@@ -712,6 +712,7 @@ struct MovegenArgs {
     uint32_t* out_count;     // n or NULL
     uint8_t* out_mask4;      // has_moves mode
     int32_t groups;          // k_movegen_g: orientation groups per board-player
+    uint64_t* out_mask;      // k_movegen_m: n x 91 x 7 (bit 20 r + c of the 400-bit mask) or NULL
 };
 
 __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&own)[4][20], uint32_t (&occ)[20]) {
@@ -791,6 +792,65 @@ __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
 #define BK_ROWS_GROUP(i0, i1, H, ...) rows_class_group<H, __VA_ARGS__>(i0, i1, grp, G, P, emit);
     BK_CLASS_LIST(BK_ROWS_GROUP)
 #undef BK_ROWS_GROUP
+    if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
+}
+
+// k_movegen_g with the SURVEY 8(b) output: each orientation's legal anchors as one
+// 400-bit mask (7 u64, bit 20 r + c, the reference's player_bits numbering), 5,096 B per
+// board-player instead of 91 x 20 row words (7,280 B).  XCD-aware grid: block b runs on
+// XCD b % 8 (round-robin dispatch), and the G group waves of one 64-board-player set all
+// get blocks with the same b % 8, so the set's states are fetched from HBM once into that
+// XCD's L2 (not once per XCD) and the partial 128-B lines of one board's mask, written by
+// different group waves, merge in the same L2.
+#define MG_XCDS 8
+__global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
+    const int G = a.groups;
+    const int xcd = blockIdx.x % MG_XCDS, j = blockIdx.x / MG_XCDS;
+    const int set = xcd + MG_XCDS * (j / G), grp = j % G;
+    const int i = set * WAVE + threadIdx.x;
+    const bool live = i < a.n;
+    const int idx = live ? i : 0;
+    const bk_state* s = a.states + idx;
+    const int p = a.players[idx] & 3;
+    uint32_t own[20], occ[20];
+#pragma unroll
+    for (int R = 0; R < 20; ++R) { occ[R] = 0; own[R] = 0; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            const uint32_t row = plane_row(s->planes[q], R);
+            occ[R] |= row;
+            own[R] |= (q == p) ? row : 0u;
+        }
+    Planes P;
+    derive_rows(own, occ, (s->first_move >> p) & 1u, p, P);
+    make_pairs(P);
+    const uint32_t avail = live ? (~s->used[p] & 0x1FFFFFu) : 0u;
+    uint32_t total = 0;
+    auto emit = [&](int g, uint32_t piece, const uint32_t (&ok)[20]) {
+        const bool av = (avail >> (piece - 1u)) & 1u;
+        uint64_t w[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 20; ++r) {
+            const uint32_t v = av ? ok[r] : 0u;
+            total += __builtin_popcount(v);
+            constexpr int kBits = 20;
+            const int off = kBits * r, q = off >> 6, sh = off & 63;  // compile-time per r
+            w[q] |= (uint64_t)v << sh;
+            if (sh > 64 - kBits) w[q + 1] |= (uint64_t)v >> (64 - sh);
+        }
+        if (live && a.out_mask) {
+            uint64_t* dst = a.out_mask + ((size_t)idx * BK_NUM_ORIENTS + g) * 7;
+#pragma unroll
+            for (int q = 0; q < 7; ++q) dst[q] = w[q];
+        }
+    };
+    if (set * WAVE < a.n) {  // a grid rounded up to a multiple of 8 sets has idle blocks
+#define BK_ROWS_GROUP(i0, i1, H, ...) rows_class_group<H, __VA_ARGS__>(i0, i1, grp, G, P, emit);
+        BK_CLASS_LIST(BK_ROWS_GROUP)
+#undef BK_ROWS_GROUP
+    }
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
 }
 
@@ -3029,7 +3089,7 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
     if (groups < 1) groups = 1;
     if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
-    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups};
+    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups, nullptr};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     const int grid = waves * groups;
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
@@ -3040,6 +3100,52 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     if (mem == BK_MEM_HOST) {
         if (out_count) HIPCHK(h, hipMemcpyAsync(out_count, d_count, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, h->cur));
         if (out_rows) HIPCHK(h, hipMemcpyAsync(out_rows, d_rows, rows_bytes, hipMemcpyDeviceToHost, h->cur));
+        HIPCHK(h, hipStreamSynchronize(h->cur));
+    }
+    return BK_OK;
+}
+
+int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players, int32_t n, uint64_t* out_mask,
+                    uint32_t* out_count, int mem) {
+    if (!h || !states || !players || n < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
+        return set_err(h, BK_EINVAL, "bk_movegen_mask: invalid arguments%s", "");
+    if (n == 0) return BK_OK;
+    if (mem == BK_MEM_DEVICE && out_mask && ((uintptr_t)out_mask & 7))
+        return set_err(h, BK_EINVAL, "bk_movegen_mask: out_mask must be 8-byte aligned%s", "");
+    HIPCHK(h, hipSetDevice(h->device));
+    void *d_states, *d_players;
+    int rc = stage_in(h, states, sizeof(bk_state) * (size_t)n, mem, &d_states, &h->d_in, &h->d_in_cap);
+    if (rc) return rc;
+    rc = stage_in(h, players, (size_t)n, mem, &d_players, &h->d_aux, &h->d_aux_cap);
+    if (rc) return rc;
+    uint64_t* d_mask = out_mask;
+    uint32_t* d_count = out_count;
+    const size_t mask_bytes = sizeof(uint64_t) * 7 * BK_NUM_ORIENTS * (size_t)n;
+    if (mem == BK_MEM_HOST) {
+        const size_t cb = (sizeof(uint32_t) * (size_t)n + 15) & ~(size_t)15;
+        rc = grow(h, &h->d_out, &h->d_out_cap, cb + (out_mask ? mask_bytes : 0));
+        if (rc) return rc;
+        d_count = (uint32_t*)h->d_out;
+        d_mask = out_mask ? (uint64_t*)((char*)h->d_out + cb) : nullptr;
+    }
+    // groups as bk_movegen; sets of 64 board-players rounded up to a multiple of the XCDs
+    const int waves = (n + WAVE - 1) / WAVE;
+    int groups = (4 * h->num_cu + waves - 1) / waves;
+    groups = groups < 8 ? 8 : (groups > MG_GROUPS_DEFAULT_MAX ? MG_GROUPS_DEFAULT_MAX : groups);
+    if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
+    if (groups < 1) groups = 1;
+    if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
+    const int sets = ((waves + MG_XCDS - 1) / MG_XCDS) * MG_XCDS;
+    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, nullptr, d_count, nullptr, groups, d_mask};
+    if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
+    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
+    h->timed = true;
+    if (mem == BK_MEM_HOST) {
+        if (out_count) HIPCHK(h, hipMemcpyAsync(out_count, d_count, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, h->cur));
+        if (out_mask) HIPCHK(h, hipMemcpyAsync(out_mask, d_mask, mask_bytes, hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipStreamSynchronize(h->cur));
     }
     return BK_OK;
@@ -3059,7 +3165,7 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
         if (rc) return rc;
         d_mask = (uint8_t*)h->d_out;
     }
-    MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask};
+    MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask, 0, nullptr};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     hipLaunchKernelGGL(k_has_moves, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());

@@ -99,6 +99,33 @@ class BlokusGPU:
                             N.MEM_HOST)
         return cnt, out
 
+    def movegen_mask(self, states, players, masks: bool = True):
+        """movegen with the legal sets as 400-bit masks (bk_movegen_mask): returns
+        (counts[n] uint32, masks[n,91,7] uint64 or None); bit r*20+c of masks[i,g] =
+        anchor (r, c) legal for global orientation g (engine/move_generator.py:130 set,
+        Board.player_bits numbering).  Inputs as movegen; torch in -> torch out."""
+        if _is_torch(states):
+            import torch
+            n = states.shape[0]
+            _check_device_tensor(states, "states", torch.uint8, (n, 256), self.device)
+            _check_device_tensor(players, "players", torch.uint8, (n,), self.device)
+            cnt = torch.empty(n, dtype=torch.int32, device=states.device)
+            out = torch.empty((n, N.N_ORIENTS, 7), dtype=torch.int64, device=states.device) if masks else None
+            self._stream_from_torch()
+            self.handle.movegen_mask(states.data_ptr(), players.data_ptr(), n, out.data_ptr() if masks else 0,
+                                     cnt.data_ptr(), N.MEM_DEVICE)
+            return cnt, out
+        st = np.ascontiguousarray(states).view(np.uint8).reshape(-1, 256)
+        pl = np.ascontiguousarray(players, dtype=np.uint8)
+        n = st.shape[0]
+        assert pl.shape[0] == n
+        cnt = np.zeros(n, dtype=np.uint32)
+        out = np.zeros((n, N.N_ORIENTS, 7), dtype=np.uint64) if masks else None
+        self.handle.set_stream(None)
+        self.handle.movegen_mask(st.ctypes.data, pl.ctypes.data, n, out.ctypes.data if masks else 0, cnt.ctypes.data,
+                                 N.MEM_HOST)
+        return cnt, out
+
     def has_moves(self, states):
         """uint8 mask per state: bit p set iff player p has a legal move (move_generator.py:961)."""
         if _is_torch(states):

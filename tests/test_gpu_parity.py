@@ -155,3 +155,37 @@ def test_native_rollout_invariants(gpu):
     assert (res["plies"] > 0).mean() > 0.99
     # the root's cells + plies bound: score base cells >= root cells
     assert (sc >= 0).all() and (sc <= 89 + 15 + 20 + 32).all()
+
+
+def _rows_to_masks(rows):
+    """[n,91,20] row words -> [n,91,7] uint64 400-bit masks (bit r*20+c)."""
+    n = rows.shape[0]
+    bits = ((rows[..., None] >> np.arange(20, dtype=np.uint32)) & 1).astype(np.uint8).reshape(n, 91, 400)
+    bits = np.concatenate([bits, np.zeros((n, 91, 48), np.uint8)], axis=2)
+    return np.packbits(bits.reshape(n, 91, 7, 64)[..., ::-1], axis=-1).view(">u8")[..., 0].astype(np.uint64)
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 1000, 4096])
+def test_movegen_mask_equals_rows_and_oracle(gpu, n):
+    """bk_movegen_mask (91 x 7 u64 per board-player, the SURVEY 8(b) layout, XCD-aware
+    grid): the same sets as bk_movegen's rows for ragged batch sizes, counts equal, a
+    sample against the oracle's naive lists; host and device pointers agree."""
+    import torch
+    boards = oracle_states(n, seed0=5000 + n)
+    st = pack_many(boards)
+    players = np.array([b.cur for b in boards], dtype=np.uint8)
+    cnt, rows = gpu.movegen(st, players)
+    cm, masks = gpu.movegen_mask(st, players)
+    assert np.array_equal(cnt, cm)
+    assert np.array_equal(masks, _rows_to_masks(rows))
+    for i in range(0, n, max(1, n // 16)):
+        m = masks[i]
+        got = [g * 400 + b for g in range(91) for b in range(400) if int(m[g, b // 64]) >> (b % 64) & 1]
+        assert got == O.legal_moves(boards[i], boards[i].cur, O.ORDER_NAIVE), i
+    dev = torch.device("cuda", 0)
+    cd, md = gpu.movegen_mask(torch.from_numpy(st.view(np.uint8).reshape(n, 256).copy()).to(dev),
+                              torch.from_numpy(players).to(dev))
+    assert np.array_equal(cd.cpu().numpy().astype(np.uint32), cnt)
+    assert np.array_equal(md.cpu().numpy().view(np.uint64), masks)
+    c0, m0 = gpu.movegen_mask(st, players, masks=False)
+    assert m0 is None and np.array_equal(c0, cnt)
