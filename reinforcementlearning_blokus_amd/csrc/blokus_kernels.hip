@@ -539,31 +539,60 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
         rows[r * WAVE].y = r <= rlim ? (ac & ~ab) : 0u;
     }
     // Pass 2 reads the table 16 slots per pair of uint4 loads into registers, all
-    // indices static (a dynamically indexed key array would live in scratch memory)
-    int found_r = -1, found_c = 0;
+    // indices static (a dynamically indexed key array would live in scratch memory); the
+    // next 16 slots' loads are issued before this batch is walked.  Per frontier cell f =
+    // (fr, fc) the new anchors of piece row d (anchor row fr - d) are the legal, not yet
+    // counted anchors among columns fc - c of the row's cells: one LDS row read and a mask
+    // (rev[d] has bit 4 - c per cell (d, c); (rev[d] << fc) >> 4 puts them at fc - c).
+    // A slot whose anchors hold the kk-th is resolved in cell order at the end (the
+    // anchors of one frontier cell are distinct, and counting them as a set keeps every
+    // other slot's contribution exact).
+    const int H = (int)((info >> 16) & 0xFFu);
+    uint32_t rev[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+        for (int d = 0; d < 5; ++d) rev[d] |= (k < n && cd[k] == d) ? (1u << (4 - (int)sh[k])) : 0u;
     uint32_t cnt = 0;
+    int hit_f = -1;
     const bk_u4_alias* k4 = reinterpret_cast<const bk_u4_alias*>(key);
+    uint4 qa = k4[0], qb = k4[1];  // tables hold >= 8 slots; the storage has 256
 #pragma unroll 1
-    for (int b0 = 0; b0 <= mask && found_r < 0; b0 += 16) {
-        const uint4 qa = k4[b0 >> 3], qb = k4[(b0 >> 3) + 1];
+    for (int b0 = 0; b0 <= mask && hit_f < 0; b0 += 16) {
+        const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
+        const uint4 na = k4[nb0 >> 3], nb = k4[(nb0 >> 3) + 1];
         const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
-            if (found_r >= 0 || f < 0 || b0 + j > mask) continue;
+            if (hit_f >= 0 || f < 0 || b0 + j > mask) continue;
             const int fr = f / 20, fc = f - 20 * fr;
+            uint32_t hm[5], tot = 0;
 #pragma unroll
-            for (int k = 0; k < 5; ++k) {
-                if (k >= n || found_r >= 0) continue;
-                const int ar = fr - cd[k], acl = fc - (int)sh[k];
-                if (ar < 0 || ar > 19 || acl < 0 || acl > 19) continue;
-                uint2* rp = rows + ar * WAVE;
-                const uint32_t okw = rp->y;
-                if (!((okw >> acl) & 1u)) continue;
-                if (cnt == kk) { found_r = ar; found_c = acl; continue; }
-                rp->y = okw & ~(1u << acl);
-                ++cnt;
+            for (int d = 0; d < 5; ++d) {
+                const int ar = fr - d;
+                hm[d] = (d < H && ar >= 0) ? (rows[(ar < 0 ? 0 : ar) * WAVE].y & ((rev[d] << fc) >> 4)) : 0u;
+                tot += __builtin_popcount(hm[d]);
             }
+            if (cnt + tot > kk) { hit_f = f; continue; }
+#pragma unroll
+            for (int d = 0; d < 5; ++d)
+                if (hm[d]) rows[(fr - d) * WAVE].y &= ~hm[d];
+            cnt += tot;
+        }
+        qa = na; qb = nb;
+    }
+    int found_r = -1, found_c = 0;
+    if (hit_f >= 0) {  // the (kk - cnt)-th new anchor of frontier cell hit_f, in cell order
+        const int fr = hit_f / 20, fc = hit_f - 20 * fr;
+        uint32_t rem = kk - cnt;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k >= n || found_r >= 0) continue;
+            const int ar = fr - cd[k], acl = fc - (int)sh[k];
+            if (ar < 0 || acl < 0) continue;
+            if (!((rows[ar * WAVE].y >> acl) & 1u)) continue;
+            if (rem == 0u) { found_r = ar; found_c = acl; } else { --rem; }
         }
     }
     out_r = found_r;
@@ -2866,6 +2895,332 @@ __global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts(MctsArgs a) 
 __global__ __launch_bounds__(HBLOCK, 2) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
 
 // ------------------------------------------------------------------------------------
+// Cooperative MCTSAgent searches: ONE 64-lane wave per search, for batches too small to
+// fill the chip with one search per lane (config 4: ~500 MCTS seats to move per arena
+// round, i.e. 8 waves on 1,024 SIMDs; single MCTSAgent.select_action calls: 1 lane).
+// Every lane of the wave holds the same search: the same registers, the same data in its
+// own LDS column, and the wave's slab / McLane / node pool / TT / MT state in HBM.  The
+// serial parts (tree select / replay / backprop, TT, the frontier tables, locate, place)
+// therefore run unchanged and redundantly -- identical stores to identical addresses --
+// and the one atomic (the game counter) is lane 0's.  The per-ply work that is parallel
+// is split over the lanes: lane l evaluates orientations l and l + 64 with data-driven
+// cell terms from the B/C rows in its column (lane_ok_rows), the per-orientation counts
+// are wave-scanned for the pick (naive order: g ascending), and the HeuristicAgent's e
+// sums (lane_orient_sum) go to a wave-shared array and are summed per piece in
+// orientation order.  The searches are the reference's, as in k_mcts / k_mcts_h (tests
+// run both kernels on the same batches).
+// ------------------------------------------------------------------------------------
+#define COOP_WAVES 2                             // searches (waves) per block
+#define COOP_AREA ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS)  // per-wave per-lane area (rows / staged table)
+#define COOP_SHARED (BK_NUM_ORIENTS + BK_PIECES)  // per-wave doubles: e per orientation, per piece
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o);
+        v += lane >= o ? u : 0u;
+    }
+    return v;
+}
+
+// legal-move counts (and with E the e sums, HeuristicAgent pass A) of this lane's
+// orientations g = lane + 64 h; 0 for g >= 91 or a used piece.  rows = {B, C} in the
+// lane's column.
+template <bool E>
+__device__ __forceinline__ void coop_orients(const uint2* rows, uint32_t avail, int lane, const HeurShared* hs,
+                                             int edge_w, uint32_t (&cnt)[2], double (&es)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int g = lane + WAVE * h;
+        cnt[h] = 0u;
+        es[h] = 0.0;
+        const bool live = g < BK_NUM_ORIENTS && ((avail >> ((kInfo[g < BK_NUM_ORIENTS ? g : 0] & 0xFFu) - 1u)) & 1u);
+        if (live) {
+            uint32_t ok[20];
+            lane_ok_rows(g, rows, ok);
+#pragma unroll
+            for (int r = 0; r < 20; ++r) cnt[h] += __builtin_popcount(ok[r]);
+            if constexpr (E) es[h] = lane_orient_sum(g, ok, rows, hs, edge_w);
+        }
+    }
+}
+
+struct CoopScan {
+    uint32_t i0, i1, c0, c1;  // inclusive prefix counts of this lane's two orientations
+    uint32_t total;
+};
+
+__device__ __forceinline__ CoopScan coop_scan(const uint32_t (&cnt)[2], int lane) {
+    CoopScan s;
+    s.c0 = cnt[0];
+    s.c1 = cnt[1];
+    s.i0 = wave_incl_scan(cnt[0], lane);
+    const uint32_t t0 = __shfl(s.i0, WAVE - 1);
+    s.i1 = wave_incl_scan(cnt[1], lane) + t0;
+    s.total = __shfl(s.i1, WAVE - 1);
+    return s;
+}
+
+// pick_orient for the wave's search: the orientation holding the k-th legal move (g
+// ascending) and the move's rank kk in it
+__device__ __forceinline__ int coop_find(const CoopScan& s, uint32_t k, uint32_t& kk) {
+    const uint64_t b0 = __ballot(k < s.i0 && k >= s.i0 - s.c0);
+    const uint64_t b1 = __ballot(k < s.i1 && k >= s.i1 - s.c1);
+    int g = BK_NUM_ORIENTS - 1;
+    uint32_t before = k;
+    if (b0) {
+        const int L = __ffsll((unsigned long long)b0) - 1;
+        g = L;
+        before = __shfl(s.i0 - s.c0, L);
+    } else if (b1) {
+        const int L = __ffsll((unsigned long long)b1) - 1;
+        g = L + WAVE;
+        before = __shfl(s.i1 - s.c1, L);
+    }
+    kk = k - before;
+    return g;
+}
+
+// heur_pick_orient from the wave-shared sums: piece, then orientation (list order: piece
+// asc, orientation asc) whose cumulative e crosses target; R = cumulative e before it.
+// Uncertain when no crossing is found (rounding at the total), as heur_pick_orient.
+__device__ __forceinline__ int coop_heur_pick(const double* es, const double* psum, const HeurShared* hs,
+                                              double target, double& R, bool& uncertain) {
+    int pstar = -1;
+    R = 0.0;
+#pragma unroll 1
+    for (int p = 0; p < BK_PIECES; ++p) {
+        const double sp = psum[p];
+        if (pstar < 0 && sp > 0.0) {
+            if (R + sp > target) pstar = p;
+            else R += sp;
+        }
+    }
+    if (pstar < 0) {
+        uncertain = true;
+        R = 0.0;
+        for (int p = 0; p < BK_PIECES; ++p)
+            if (psum[p] > 0.0) pstar = p;
+#pragma unroll 1
+        for (int p = 0; p < pstar; ++p) R += psum[p];
+    }
+    int gstar = -1;
+    double Rstar = R;
+    bool found = false;
+    const int g1 = hs->first[pstar + 1];
+#pragma unroll 1
+    for (int g = hs->first[pstar]; g < g1 && !found; ++g) {
+        const double sg = es[g];
+        if (sg > 0.0) {
+            gstar = g;
+            Rstar = R;
+            found = R + sg > target;
+            R += sg;
+        }
+    }
+    if (!found) uncertain = true;
+    R = Rstar;
+    return gstar;
+}
+
+template <bool HEUR>
+__device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
+    constexpr int BLK = COOP_WAVES * WAVE;
+    constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[COOP_AREA * COOP_WAVES + 2 * BK_CELLS + HS_WORDS];
+    __shared__ double coop_sh[COOP_WAVES][COOP_SHARED];
+    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    uint32_t* my = lds + wv * COOP_AREA;
+    uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
+    int16_t* lk = reinterpret_cast<int16_t*>(my) + 2 * lane;
+    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + COOP_AREA * COOP_WAVES);
+    HeurShared* hs = reinterpret_cast<HeurShared*>(lds + COOP_AREA * COOP_WAVES + 2 * BK_CELLS);
+    double* es_sh = coop_sh[wv];                      // e sum per orientation
+    double* ps_sh = coop_sh[wv] + BK_NUM_ORIENTS;     // e sum per piece
+    for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab[i] = kCellHash[i];
+    if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
+    __syncthreads();
+    const uint32_t slot = blockIdx.x * COOP_WAVES + wv;  // one slab / McLane per search
+    const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
+    McLane* L = a.lanes + slot;
+    Mc m;
+    m.game = -1;
+    m.mode = MC_SELECT;
+    for (uint64_t step = 0;; ++step) {
+        // ---- tree work until the search needs a movegen (uniform over the wave)
+        bool done = false;
+        while (m.mode == MC_SELECT) {
+            if (m.game < 0) {
+                int32_t next = 0;
+                if (lane == 0) next = (int32_t)atomicAdd(&a.counter[0], 1u);
+                next = __shfl(next, 0);
+                if (next >= a.n_games) { done = true; break; }
+                mc_start_game(a, m, L, next, htab);
+            }
+            const bool timed_out = a.cfg.time_limit_us > 0 && wall_clock64() - m.t0 >= a.limit_ticks;
+            const bool chunk_end = a.cfg.iter_stop > 0 && m.it >= a.cfg.iter_stop;
+            if (m.it >= a.cfg.iterations || chunk_end || timed_out || MC_FATAL(m.status)) { mc_finish_game(a, m); continue; }
+            const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
+            if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
+            if (MC_FATAL(m.status)) continue;
+            mc_replay(a, m, slab, L, htab);
+            m.mode = MC_EXPAND;
+        }
+        if (done) break;
+        if (step > a.max_steps) {  // safety valve: never spin forever
+            if (lane == 0) { atomicOr(&a.counter[1], 1u); atomicOr(&a.counter[2], BK_STICKY_GUARD); }
+            break;
+        }
+        // ---- one movegen, split over the lanes
+        const int p = m.mode == MC_EXPAND ? ((m.root_player + m.depth) & 3) : m.cur;
+        Planes P;
+        {
+            uint32_t own[20], occ[20];
+#pragma unroll
+            for (int R = 0; R < 20; ++R) {
+                own[R] = slab.at(p, R);
+                occ[R] = slab.at(4, R);
+            }
+            derive_rows(own, occ, (m.first >> p) & 1u, p, P);
+        }
+#pragma unroll
+        for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
+        const uint32_t avail = ~m.used.get(p) & 0x1FFFFFu;
+        const bool hroll = HEUR && m.mode == MC_ROLLOUT;
+        // Board.move_count of the rollout board: placements on the way from the root
+        const int edge_w = (int)(a.roots[m.game].move_count + m.depth + m.plies) < 30 ? 6 : 3;
+        uint32_t cnt[2];
+        double es[2];
+        if (hroll) coop_orients<true>(rows_lds, avail, lane, hs, edge_w, cnt, es);
+        else coop_orients<false>(rows_lds, avail, lane, hs, edge_w, cnt, es);
+        const CoopScan sc = coop_scan(cnt, lane);
+        const uint32_t total = sc.total;
+        bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+        uint32_t k = 0;
+        if (m.mode == MC_EXPAND) {
+            bk_mcts_node* nd = pool + m.node;
+            uint32_t n_legal = nd->n_legal, n_exp = nd->n_exp;
+            if (!(nd->flags & BK_MCTS_NODE_EVALUATED)) {  // MCTSNode._initialize_untried_moves
+                n_legal = total;
+                nd->n_legal = (uint16_t)n_legal;
+                nd->child0 = -1;
+                nd->flags = BK_MCTS_NODE_EVALUATED;
+            }
+            if (n_legal != total) {  // an evaluated node's list cannot change
+                m.status |= BK_MCTS_EINTERNAL;
+                m.mode = MC_SELECT;
+                continue;
+            }
+            if (n_legal == n_exp) {  // no legal move: terminal leaf
+                mc_sim_terminal(a, m, L);
+                continue;
+            }
+            k = n_legal - n_exp - 1u;  // untried_moves.pop(): the last list entry
+        } else {
+            if (total == 0u) {  // _rollout: no legal move -> break
+                mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
+                continue;
+            }
+            if (!hroll) k = mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
+        }
+        uint32_t kk = 0;
+        int gs;
+        double h_target = 0.0, h_R = 0.0, h_total = 0.0;
+        uint32_t h_ok[20];
+        bool h_unc = false;
+        if (hroll) {
+            // per-orientation e to the wave-shared array, per-piece sums in orientation order
+            if (lane < BK_NUM_ORIENTS) es_sh[lane] = es[0];
+            if (lane + WAVE < BK_NUM_ORIENTS) es_sh[lane + WAVE] = es[1];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            if (lane < BK_PIECES) {
+                double sp = 0.0;
+#pragma unroll 1
+                for (int g = hs->first[lane]; g < hs->first[lane + 1]; ++g) sp += es_sh[g];
+                ps_sh[lane] = sp;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll 1
+            for (int q = 0; q < BK_PIECES; ++q) h_total += ps_sh[q];
+            h_target = mc_random_sample(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos) * h_total;
+            gs = coop_heur_pick(es_sh, ps_sh, hs, h_target, h_R, h_unc);
+            if (gs >= 0) lane_ok_rows(gs, rows_lds, h_ok);
+        } else {
+            gs = coop_find(sc, k, kk);
+        }
+        FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
+        int ar, ac;
+        if (hroll) {
+            if (gs < 0) {
+                ar = -1;
+                ac = 0;
+            } else {
+                heur_walk_frontier(gs, h_ok, rows_lds, T->s.key[p], T->s.mask[p], hs, edge_w, h_target, h_R, h_total,
+                                   ar, ac, h_unc);
+            }
+            if (h_unc) m.status |= BK_MCTS_EUNCERT;
+        } else {
+            locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+        }
+        if (ar < 0) {  // the table does not list the move: counts and tables disagree
+            m.status |= BK_MCTS_EINTERNAL;
+            m.mode = MC_SELECT;
+            continue;
+        }
+        uint32_t pm[5];
+        int32_t cells[5];
+        piece_cells(gs, ar, ac, pm, cells);
+        const uint64_t real = frontier_ops(rows_lds, slab, p, (m.first >> p) & 1u, gs, ar, ac, pm);
+        const bool expand = m.mode == MC_EXPAND;
+        uint32_t c = 0;
+        bool ok = true;
+        if (expand) {
+            bk_mcts_node* nd = pool + m.node;
+            const int32_t cs = mc_child_slot(pool, nd, m, a.cfg.node_cap);
+            if (cs < 0) { m.status |= BK_MCTS_EPOOL; m.mode = MC_SELECT; continue; }
+            c = (uint32_t)cs;
+            nd->n_exp = (uint16_t)(nd->n_exp + 1u);
+            bk_mcts_node ch;
+            ch.total = 0.0; ch.visits = 0; ch.child0 = -1;
+            ch.move = (uint16_t)(gs * 400 + ar * 20 + ac);
+            ch.n_exp = 0; ch.n_legal = 0; ch.flags = 0;
+            pool[c] = ch;
+            if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
+        }
+        ok &= mc_place_staged(m, slab, p, gs, ar, expand ? &L->A : &L->B, htab, pm, cells, real, lk);
+        if (expand) {
+            ok &= mc_copy_tables(&L->B.s, &L->A.s, htab);  // MCTSNode(new_board): board.copy()
+            if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
+            m.hash = mc_hash_step(Z, m.hash, p, (m.root_cp + m.depth) & 3, gs, ar, ac);
+            L->path[++m.depth] = (int32_t)c;
+            m.node = (int32_t)c;
+            double reward = 0.0;
+            if (a.cfg.use_tt && mc_tt_lookup(a, m, reward)) {
+                mc_complete(a, m, L, reward, true);
+                continue;
+            }
+            m.player = m.cur = (m.root_player + m.depth) & 3;
+            m.score0 = mc_score(m, m.player);
+            m.plies = 0;
+            m.mode = MC_ROLLOUT;
+        } else {
+            if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
+            m.plies++;
+            m.rplies++;
+            m.cur = (m.cur + 1) & 3;
+            if (m.plies >= a.cfg.max_rollout_moves)
+                mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
+        }
+    }
+}
+
+__global__ __launch_bounds__(COOP_WAVES * WAVE) void k_mcts_coop(MctsArgs a) { mcts_coop_body<false>(a); }
+__global__ __launch_bounds__(COOP_WAVES * WAVE) void k_mcts_coop_h(MctsArgs a) { mcts_coop_body<true>(a); }
+
+// ------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------
 struct bk_handle_s {
@@ -3666,19 +4021,24 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     }
     // persistent grid: every resident slot pulls whole searches from the counter
     const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;
-    const int blk = heur ? HBLOCK : BLOCK;
-    int blocks = h->num_cu * (heur ? 3 : h->mcts_blocks_per_cu);
+    // one wave per search (k_mcts_coop) when the batch cannot fill the chip with one
+    // search per lane: up to one search per SIMD (config 4's arena rounds, single calls)
+    bool coop = (int64_t)n_games <= 4 * (int64_t)h->num_cu;
+    if (const char* env = getenv("BK_MCTS_COOP")) coop = atoi(env) != 0;  // tuning / test override
+    const int blk = coop ? COOP_WAVES * WAVE : heur ? HBLOCK : BLOCK;
+    int blocks = h->num_cu * (coop ? 2 : heur ? 3 : h->mcts_blocks_per_cu);
     // k_mcts is latency-bound at one wave per SIMD (config 5: 65,536 searches fill one
     // 256-lane block per CU): when the resident slots allow, every other lane takes a
     // search, so twice the waves hide each other's latency (11.14 vs 10.84 M sims/s,
     // profiles/r03/sweeps/mcts_spread.jsonl; 4 measured slower)
-    int spread = (!heur && (int64_t)n_games * 2 <= (int64_t)blocks * blk) ? 2 : 1;
+    int spread = (!heur && !coop && (int64_t)n_games * 2 <= (int64_t)blocks * blk) ? 2 : 1;
     if (const char* env = getenv("BK_MCTS_SPREAD")) spread = atoi(env);  // tuning override
-    if (spread < 1 || spread > WAVE || (spread & (spread - 1))) spread = 1;
-    const int need = (int)(((int64_t)n_games * spread + blk - 1) / blk);
+    if (spread < 1 || spread > WAVE || (spread & (spread - 1)) || coop) spread = 1;
+    const int per_block = coop ? COOP_WAVES : blk;  // searches a block holds at once
+    const int need = (int)(((int64_t)n_games * spread + per_block - 1) / per_block);
     if (blocks > need) blocks = need;
     if (blocks < 1) blocks = 1;
-    const uint32_t nslots = (uint32_t)blocks * blk;
+    const uint32_t nslots = (uint32_t)blocks * per_block;
     rc = grow(h, &h->d_slab, &h->d_slab_cap, sizeof(uint32_t) * SLAB_WORDS * (size_t)nslots);
     if (rc) return rc;
     rc = grow(h, &h->d_mclane, &h->d_mclane_cap, sizeof(McLane) * (size_t)nslots);
@@ -3701,7 +4061,11 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    if (heur)
+    if (coop && heur)
+        hipLaunchKernelGGL(k_mcts_coop_h, dim3(blocks), dim3(blk), 0, h->cur, a);
+    else if (coop)
+        hipLaunchKernelGGL(k_mcts_coop, dim3(blocks), dim3(blk), 0, h->cur, a);
+    else if (heur)
         hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
     else
         hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
