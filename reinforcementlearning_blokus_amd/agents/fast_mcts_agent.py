@@ -123,7 +123,7 @@ class FastMCTSAgent:
         return np.array(words, dtype=np.uint32)
 
     def _set_rng_words(self, words: np.ndarray) -> None:
-        self.rng.setstate((3, tuple(int(x) for x in words), None))
+        self.rng.setstate((3, tuple(np.asarray(words, dtype=np.uint32).tolist()), None))
 
     # ------------------------------------------------------------------ reference helpers
     def _get_cached_legal_moves(self, board: Board, player: Player) -> List[Move]:

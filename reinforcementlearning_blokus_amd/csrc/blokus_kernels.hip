@@ -4022,8 +4022,10 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     // persistent grid: every resident slot pulls whole searches from the counter
     const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;
     // one wave per search (k_mcts_coop) when the batch cannot fill the chip with one
-    // search per lane: up to one search per SIMD (config 4's arena rounds, single calls)
-    bool coop = (int64_t)n_games <= 4 * (int64_t)h->num_cu;
+    // search per lane: a cooperative search runs ~6x faster than a lane's (config 4: MCTS
+    // phase 53 -> 8.6 s at ~500 searches per launch), so it wins while the searches take
+    // fewer than ~6 rounds of the resident waves (config 4's arena rounds, single calls)
+    bool coop = (int64_t)n_games <= 16 * (int64_t)h->num_cu;
     if (const char* env = getenv("BK_MCTS_COOP")) coop = atoi(env) != 0;  // tuning / test override
     const int blk = coop ? COOP_WAVES * WAVE : heur ? HBLOCK : BLOCK;
     int blocks = h->num_cu * (coop ? 2 : heur ? 3 : h->mcts_blocks_per_cu);

@@ -107,6 +107,33 @@ def order_moves(rows: np.ndarray, frontier: Optional[Sequence] = None):
     return g[order], r[order], c[order]
 
 
+def order_moves_many(rows: np.ndarray, frontiers: Sequence[Sequence]):
+    """order_moves for m board-players at once: rows uint32[m,91,20], frontiers[i] the
+    iteration-order (row, col) list of board-player i's frontier set.  Returns a list of
+    m (g, r, c) tuples, each in the reference's frontier list order (the key of
+    order_moves: piece asc, orientation asc, min over the move's cells on a frontier cell
+    of (rank, cell index))."""
+    rows = np.ascontiguousarray(rows, dtype="<u4")
+    m = rows.shape[0]
+    if m == 0:
+        return []
+    bits = np.unpackbits(rows.view(np.uint8).reshape(m, 91, 20, 4), axis=3, bitorder="little")
+    gi, g, r, c = np.nonzero(bits)  # game-major, then naive order
+    rank = np.full((m, 400), _BIG, dtype=np.int64)
+    for i, fr in enumerate(frontiers):
+        for j, (a, b) in enumerate(fr):
+            if rank[i, a * 20 + b] == _BIG:
+                rank[i, a * 20 + b] = j
+    cells = (r[:, None] + _DR[g]) * 20 + (c[:, None] + _DC[g])
+    valid = np.arange(5)[None, :] < _NCELLS[g][:, None]
+    cells = np.where(valid, np.clip(cells, 0, 399), 0)
+    key = np.where(valid, rank[gi[:, None], cells] * 8 + np.arange(5)[None, :], _BIG * 8).min(axis=1)
+    order = np.lexsort((key, g, gi))
+    gi, g, r, c = gi[order], g[order], r[order], c[order]
+    cuts = np.searchsorted(gi, np.arange(1, m))
+    return [(gg, rr, cc) for gg, rr, cc in zip(np.split(g, cuts), np.split(r, cuts), np.split(c, cuts))]
+
+
 class LegalMoveGenerator:
     """Drop-in for engine.move_generator.LegalMoveGenerator, GPU-backed."""
 

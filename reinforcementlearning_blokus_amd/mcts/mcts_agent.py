@@ -263,7 +263,7 @@ class MCTSAgent:
                 tabs.append(flat_keys(a.zobrist_hash))
                 zidx.append(len(tabs) - 1)
             zob = np.stack(tabs)
-            rh = np.array([hash_states(rts[j:j + 1], zob[j])[0] for j in range(len(idx))], np.uint64)
+            rh = hash_states(rts, zob)  # one table per search
             mt = np.zeros((len(idx), 625), np.uint32)
             rng_states = [a.rollout_agent.rng.get_state() for a in ags]
             for j, st in enumerate(rng_states):
@@ -271,10 +271,20 @@ class MCTSAgent:
                 mt[j, 624] = st[2]
             tt = None
             if use_tt:
-                tt = MctsTT(len(idx), cap=max([a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12]))
+                # the batch's tables: the agents' own open-addressing rows (same capacity:
+                # copied as they are; smaller: re-inserted), grown for this search's inserts
+                caps = [a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12]
+                need = max([int(a._gpu_tt.count[0]) for a in ags if a._gpu_tt is not None] or [0]) + iters + 2
+                cap = max(caps)
+                while 2 * need > cap:
+                    cap *= 2
+                tt = MctsTT(len(idx), cap=cap)
                 for j, a in enumerate(ags):
                     if a._gpu_tt is not None and a._gpu_tt.count[0]:
-                        tt.load(j, *a._gpu_tt.items(0))
+                        if a._gpu_tt.cap == cap:
+                            tt.keys[j], tt.vals[j], tt.count[j] = a._gpu_tt.keys[0], a._gpu_tt.vals[0], a._gpu_tt.count[0]
+                        else:
+                            tt.load(j, *a._gpu_tt.items(0))
             t0 = time.time()
             r = gpu.mcts(rts, sts, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
                          mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us,
@@ -303,7 +313,7 @@ class MCTSAgent:
                 a.stats["rollout_rewards"].extend(float(x) for x in rew[hits == 0])
                 if use_tt:
                     a._gpu_tt = MctsTT(1, cap=tt.cap)
-                    a._gpu_tt.load(0, *tt.items(j))
+                    a._gpu_tt.keys[0], a._gpu_tt.vals[0], a._gpu_tt.count[0] = tt.keys[j], tt.vals[j], tt.count[j]
                     t = a.transposition_table
                     t.access_count += int(o["tt_hits"]) + int(o["rollouts"])
                     t.hit_count += int(o["tt_hits"])

@@ -21,15 +21,16 @@ class ZobristHash:
         self._generate_hash_values()
 
     def _generate_hash_values(self):
+        # the reference draws one randint(0, 2**64, dtype=uint64) per key, cell x value,
+        # then turn, then player x piece (mcts/zobrist.py:41-68); a full-range uint64 draw
+        # is next_uint64 per element whether drawn one at a time or as one array, so one
+        # vector draw in that order gives the same keys (tests/golden/zobrist.json)
         n, k = self.board_size, self.num_players
-        draw = lambda: self.rng.randint(0, 2**64, dtype=np.uint64)  # noqa: E731
-        self.position_player_hashes = np.zeros((n, n, k + 1), dtype=np.uint64)
-        for r in range(n):
-            for c in range(n):
-                for v in range(k + 1):
-                    self.position_player_hashes[r, c, v] = draw()
-        self.player_turn_hashes = np.array([draw() for _ in range(k)], dtype=np.uint64)
-        self.piece_used_hashes = np.array([[draw() for _ in range(21)] for _ in range(k)], dtype=np.uint64)
+        vals = self.rng.randint(0, 2**64, size=n * n * (k + 1) + k + k * 21, dtype=np.uint64)
+        m = n * n * (k + 1)
+        self.position_player_hashes = vals[:m].reshape(n, n, k + 1).copy()
+        self.player_turn_hashes = vals[m:m + k].copy()
+        self.piece_used_hashes = vals[m + k:].reshape(k, 21).copy()
         # flat view used for vectorised hashing: index cell * (k+1) + value
         self._flat = self.position_player_hashes.reshape(-1)
 
@@ -96,9 +97,14 @@ def flat_keys(z: ZobristHash) -> np.ndarray:
 
 def hash_states(states: np.ndarray, keys: np.ndarray) -> np.ndarray:
     """ZobristHash.hash_board (mcts/zobrist.py:70-99) of packed bk_state records,
-    vectorised: XOR of the 400 cell keys, the side-to-move key and the used-piece keys."""
+    vectorised: XOR of the 400 cell keys, the side-to-move key and the used-piece keys.
+    keys: one 2088-word table (flat_keys) for every state, or one table per state
+    ([n, 2088])."""
     states = np.atleast_1d(states)
-    keys = np.asarray(keys, dtype=np.uint64).reshape(-1)
+    keys = np.asarray(keys, dtype=np.uint64)
+    per_state = keys.ndim == 2 and keys.shape[0] == len(states) and keys.shape[1] == 2088
+    if not per_state:
+        keys = keys.reshape(-1)
     n = len(states)
     cells = np.arange(400)
     word, bit = cells // 64, (cells % 64).astype(np.uint64)
@@ -106,11 +112,18 @@ def hash_states(states: np.ndarray, keys: np.ndarray) -> np.ndarray:
     for p in range(4):
         occ = (states["planes"][:, p, word] >> bit) & np.uint64(1)
         grid += occ.astype(np.int64) * (p + 1)
-    h = np.bitwise_xor.reduce(keys[cells * 5 + grid], axis=1)
-    h ^= keys[2000 + states["current_player"].astype(np.int64)]
-    for p in range(4):
-        used = states["used"][:, p].astype(np.int64)
-        for pid in range(21):
-            on = (used >> pid) & 1 == 1
-            h[on] ^= keys[2004 + p * 21 + pid]
+    # used-piece keys: [n, 4, 21] on/off
+    used = states["used"].astype(np.int64)  # [n, 4]
+    pidx = 2004 + np.arange(4)[:, None] * 21 + np.arange(21)[None, :]  # [4, 21]
+    pon = ((used[:, :, None] >> np.arange(21)[None, None, :]) & 1) == 1  # [n, 4, 21]
+    if per_state:
+        cellk = np.take_along_axis(keys, cells * 5 + grid, axis=1)
+        h = np.bitwise_xor.reduce(cellk, axis=1)
+        h ^= keys[np.arange(n), 2000 + states["current_player"].astype(np.int64)]
+        pk = np.where(pon, keys[:, pidx.reshape(-1)].reshape(n, 4, 21), np.uint64(0))
+    else:
+        h = np.bitwise_xor.reduce(keys[cells * 5 + grid], axis=1)
+        h ^= keys[2000 + states["current_player"].astype(np.int64)]
+        pk = np.where(pon, keys[pidx][None, :, :], np.uint64(0))
+    h ^= np.bitwise_xor.reduce(pk.reshape(n, -1), axis=1)
     return h.astype(np.uint64)

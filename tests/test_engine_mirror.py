@@ -217,3 +217,20 @@ def test_debug_compare_bitboard_vs_grid_report(capsys, monkeypatch):
     # offsets, so at an interior anchor they miss the up/left neighbours (as in the reference)
     assert "shifted orientation shape coords: [(5, 5)]\n  MATCH: True" in out
     assert "RESULT: grid_legal=" in out and "MISMATCH" not in out
+
+
+def test_order_moves_many_equals_order_moves():
+    """The batched orderer (config-4 FastMCTS seats) equals order_moves board by board,
+    including boards with no legal move and empty frontier lists."""
+    from reinforcementlearning_blokus_amd.engine.move_generator import order_moves, order_moves_many
+    rng = np.random.RandomState(3)
+    m = 9
+    rows = (rng.randint(0, 1 << 20, size=(m, 91, 20)) & rng.randint(0, 1 << 20, size=(m, 91, 20))
+            & rng.randint(0, 1 << 20, size=(m, 91, 20))).astype(np.uint32)
+    rows[4] = 0
+    frs = [[(int(a), int(b)) for a, b in rng.randint(0, 20, size=(rng.randint(0, 30), 2))] for _ in range(m)]
+    frs[2] = []
+    got = order_moves_many(rows, frs)
+    for i in range(m):
+        ref = order_moves(rows[i], frs[i])
+        assert all(np.array_equal(x, y) for x, y in zip(got[i], ref)), i
