@@ -529,14 +529,18 @@ def run_config4(args, world, rank, local, dist):
             print(f"config4 rank {rank}: round {rnd}, {left} games in play, mcts {prof['mcts_s']:.1f} s",
                   file=sys.stderr, flush=True)
 
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import SEARCH_TOTALS
     for _ in range(args.warmup):
         run_games_batched(cfg, mine[:64], device=local)
     barrier_sync(dist)
+    for k in SEARCH_TOTALS:
+        SEARCH_TOTALS[k] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         recs = run_games_batched(cfg, mine, device=local, progress=progress)
     barrier_sync(dist)
     elapsed = time.perf_counter() - t0
+    st = dict(SEARCH_TOTALS)
     from reinforcementlearning_blokus_amd.arena.runner import LAST_BATCH_PROFILE
     phases = dict(LAST_BATCH_PROFILE)
     sims = sum(int(r["agent_move_stats"]["mcts"]["total_simulations"] or 0) for r in recs)
@@ -549,7 +553,13 @@ def run_config4(args, world, rank, local, dist):
         dist.all_gather_object(gathered, [(r["game_index"], r["final_scores"]) for r in recs])
     if rank != 0:
         return None
-    return {
+    # roofline of the dominant kernel, bk_mcts (k_mcts_coop_h for these batch sizes): SURVEY
+    # 8(d) bytes, 256 B state read + write per rollout ply, plus 120 B per simulation (result,
+    # TT probe, node write, path update), over the launches' HIP-event time
+    kms = st["kernel_ms"] or float("nan")
+    mcts_bytes = 2.0 * STATE_B * st["rollout_plies"] + (RESULT_B + 16 + 24 + 48) * st["sims"]
+    achieved = mcts_bytes / (kms * 1e-3) / 1e9
+    line = {
         "metric": "arena games/sec (Random/Heuristic/MCTS/FastMCTS round-robin, reference-exact records)",
         "value": games / elapsed, "unit": "games/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
@@ -561,10 +571,53 @@ def run_config4(args, world, rank, local, dist):
                    "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
                    "rank0_phase_seconds": phases,
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for("k_mcts_coop_h")[0],
+                     "kernel": "k_mcts_coop_h", "kernel_ms": kms, "launches": st["launches"],
+                     "mcts_sims": st["sims"], "rollout_plies_per_sim": st["rollout_plies"] / max(st["sims"], 1)},
         "reference_python": {"value": 1.0 / 20.3, "unit": "games/s/core",
                              "what": "a 4-random-agent game with the reference's default telemetry (20.3 s), "
                                      "measured in the build container (SURVEY.md 6); MCTS seats are slower"},
     }
+    if not args.no_cpu_baseline and world == 1:
+        cb = cpu_baseline_config4(cfg, args.cpu_seconds)
+        cb["gpu_over_cpu"] = line["value"] / cb["value"]
+        line["cpu_baseline"] = cb
+    return line
+
+
+def cpu_baseline_config4(cfg, seconds):
+    """oracle/blokus_oracle.c or_arena4_game on this host's cores: the first games of the
+    same run (seat assignment and agent seeds of game i from the run config, as the GPU
+    run derives them), one game per thread at a time, as many as fit in about `seconds`."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import pyoracle as O
+    from reinforcementlearning_blokus_amd.arena.config import (agent_seed, game_seed_from_run_seed,
+                                                               seat_assignment_for_game)
+    cpu = host_cpu()
+    threads = cpu["cores"]
+    kinds = {a.name: {"random": 0, "heuristic": 1, "mcts": 2, "fast_mcts": 3}[a.type] for a in cfg.agents}
+
+    def game(gi):
+        seats = seat_assignment_for_game(cfg.agent_names, gi, game_seed_from_run_seed(cfg.seed, gi), cfg.seat_policy)
+        names = [seats[str(p + 1)] for p in range(4)]
+        return O.arena4_game([kinds[n] for n in names], [agent_seed(cfg.seed, gi, n) for n in names],
+                             CONFIG4_AGENTS[2]["params"]["iterations"], 1000)[0]
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside or_arena4_game
+        list(ex.map(game, range(threads)))
+    dt1 = time.perf_counter() - t0
+    n = max(threads, int(threads * seconds / max(dt1, 1e-3)) // threads * threads)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        plies = sum(ex.map(game, range(n)))
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "games/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+            "host": cpu, "sample": f"the run's first {n} games ({plies} plies), oracle/blokus_oracle.c "
+                                   f"or_arena4_game (MCTS 64 iterations with HeuristicAgent rollouts, FastMCTS 1,000 "
+                                   f"iterations), {threads} threads, {dt:.1f} s"}
 
 
 # ------------------------------------------------------------------ config 2

@@ -904,14 +904,84 @@ static int tt_find(const uint64_t* keys, const double* vals, int cap, uint64_t h
     return 0;
 }
 
+/* HeuristicAgent._evaluate_move (agents/heuristic_agent.py:68-199) of move = g * 400 +
+ * anchor for player p, in the reference's double-precision operation order (as
+ * pyoracle.heuristic_score, which tests/golden/heuristic.json pins) */
+static double heur_score_c(const or_board* b, int p, int move) {
+    const or_orient_t* o = &g_or[move / 400];
+    const int ar = (move % 400) / 20, ac = move % 20, pv = p + 1;
+    double score = 0.0;
+    score += 1.0 * o->n;
+    int corners = 0, edge = 0;
+    for (int k = 0; k < o->n; ++k) {
+        const int r = ar + o->r[k], c = ac + o->c[k];
+        static const int DR[4] = {-1, -1, 1, 1}, DC[4] = {-1, 1, -1, 1};
+        for (int d = 0; d < 4; ++d) {
+            const int nr = r + DR[d], nc = c + DC[d];
+            if (!inb(nr, nc) || b->grid[nr * 20 + nc] != 0) continue;
+            int safe = 1;
+            if (nr > 0 && b->grid[(nr - 1) * 20 + nc] == pv) safe = 0;
+            if (nr < 19 && b->grid[(nr + 1) * 20 + nc] == pv) safe = 0;
+            if (nc > 0 && b->grid[nr * 20 + nc - 1] == pv) safe = 0;
+            if (nc < 19 && b->grid[nr * 20 + nc + 1] == pv) safe = 0;
+            corners += safe;
+        }
+        int m = r < c ? r : c;
+        m = m < 19 - r ? m : 19 - r;
+        m = m < 19 - c ? m : 19 - c;
+        edge += m <= 2;
+    }
+    score += 2.0 * corners;
+    const double edge_score = b->move_count / 100.0 < 0.3 ? (double)edge : edge * 0.5;
+    score += -1.5 * edge_score;
+    const double distance = sqrt((ar - 9.5) * (ar - 9.5) + (ac - 9.5) * (ac - 9.5));
+    score += 0.5 * (1.0 - distance / sqrt(2 * (9.5 * 9.5)));
+    return score;
+}
+
+double or_heuristic_score(const or_board* b, int p, int move) { or_init(); return heur_score_c(b, p, move); }
+
+/* HeuristicAgent.select_action (:40-65): softmax of the scores (:223-244) and
+ * rng.choice(n, p) -- one random_sample() u, the first index whose cumulative probability
+ * exceeds u.  For the CPU baseline's timing (sums in sequence; numpy's pairwise sum and
+ * exp can round differently, so near-tie choices are not pinned -- pyoracle's numpy
+ * restatement is the parity checker). */
+static int heur_choice_c(const or_board* b, int p, or_mt* rng, int32_t* scratch, double* sc) {
+    const int n = or_legal_moves(b, p, BK_ORDER_FRONTIER, scratch, BK_ORIENTS * 400);
+    if (n == 0) return -1;
+    double mx = -INFINITY;
+    for (int i = 0; i < n; ++i) { sc[i] = heur_score_c(b, p, scratch[i]); mx = sc[i] > mx ? sc[i] : mx; }
+    double tot = 0.0;
+    for (int i = 0; i < n; ++i) { sc[i] = exp(sc[i] - mx); tot += sc[i]; }
+    uint32_t a = or_mt_next(rng) >> 5, c = or_mt_next(rng) >> 6;
+    const double u = (a * 67108864.0 + c) * (1.0 / 9007199254740992.0);
+    double cum = 0.0;
+    for (int i = 0; i < n; ++i) {
+        cum += sc[i] / tot;
+        if (cum > u) return scratch[i];
+    }
+    return scratch[n - 1];
+}
+
+/* 0: RandomAgent rollouts; 1: HeuristicAgent rollouts (MCTSAgent's default) */
+static __thread int g_rollout_policy = 0;
+
 static double or_rollout_mt(const or_board* b, int player, or_mt* rng, int max_moves, int32_t* scratch) {
     or_board* sim = (or_board*)malloc(sizeof(or_board));
     or_board_copy(sim, b);
+    static __thread double sc[BK_ORIENTS * 400];
     int initial = or_board_score(sim, player), made = 0, cur = player;
     while (made < max_moves) {
-        int n = or_legal_moves(sim, cur, BK_ORDER_FRONTIER, scratch, BK_ORIENTS * 400);
-        if (n == 0) break;
-        or_place_move(sim, cur, scratch[or_np_randint(rng, n)]);
+        int mv;
+        if (g_rollout_policy) {
+            mv = heur_choice_c(sim, cur, rng, scratch, sc);
+            if (mv < 0) break;
+        } else {
+            int n = or_legal_moves(sim, cur, BK_ORDER_FRONTIER, scratch, BK_ORIENTS * 400);
+            if (n == 0) break;
+            mv = scratch[or_np_randint(rng, n)];
+        }
+        or_place_move(sim, cur, mv);
         cur = (cur + 1) & 3;
         ++made;
     }
@@ -1030,4 +1100,84 @@ done:
     free(ch); free(nodes); free(scratch);
     return rc;
 #undef NEW_NODE
+}
+
+/* ---------------------------------------------------------------------------------
+ * One config-4 arena game on the CPU (the bench's cpu_baseline for that line): the
+ * arena loop (analytics/tournament/arena_runner.py:652-697) with seat kinds
+ * 0 RandomAgent, 1 HeuristicAgent, 2 MCTSAgent (mcts_iters iterations, HeuristicAgent
+ * rollouts of <= 50 plies, TT kept across the seat's moves), 3 FastMCTSAgent
+ * (fast_iters iterations, the deterministic arena budget); seeds[p] seeds seat p's
+ * agent.  Returns the plies played; scores4 gets get_game_result's scores.
+ * --------------------------------------------------------------------------------- */
+int or_arena4_game(const int32_t* kinds4, const uint32_t* seeds4, int mcts_iters, int fast_iters, int32_t* scores4) {
+    or_init();
+    or_board* b = (or_board*)malloc(sizeof(or_board));
+    or_board_init(b);
+    or_mt rng[4];
+    uint64_t* ztab[4] = {0, 0, 0, 0};
+    uint64_t* tkeys[4] = {0, 0, 0, 0};
+    double* tvals[4] = {0, 0, 0, 0};
+    int32_t tcount[4] = {0, 0, 0, 0};
+    const int tcap = 1 << 16;
+    for (int p = 0; p < 4; ++p) {
+        or_mt_seed_numpy(&rng[p], seeds4[p]);
+        if (kinds4[p] == 2) {
+            ztab[p] = (uint64_t*)malloc(sizeof(uint64_t) * 2088);
+            or_zobrist_table(seeds4[p], ztab[p]);
+            tkeys[p] = (uint64_t*)calloc(tcap, sizeof(uint64_t));
+            tvals[p] = (double*)malloc(sizeof(double) * tcap);
+            for (int i = 0; i < tcap; ++i) tvals[p][i] = NAN;
+        }
+    }
+    double* lt = (double*)malloc(sizeof(double) * (size_t)(mcts_iters + 2));
+    lt[0] = 0.0;
+    for (int i = 1; i < mcts_iters + 2; ++i) lt[i] = log((double)i);
+    int32_t* moves = (int32_t*)malloc(sizeof(int32_t) * BK_ORIENTS * 400);
+    double* sc = (double*)malloc(sizeof(double) * BK_ORIENTS * 400);
+    double* rw = (double*)malloc(sizeof(double) * (size_t)(mcts_iters + 1));
+    uint8_t* hf = (uint8_t*)malloc((size_t)(mcts_iters + 1));
+    int32_t cm[1], cv[1];
+    double ct[1];
+    int plies = 0, turns = 0;
+    while (!game_over(b) && turns < 2500) {
+        const int p = b->cur;
+        ++turns;
+        int mv = -1;
+        const int n = or_legal_moves(b, p, BK_ORDER_FRONTIER, moves, BK_ORIENTS * 400);
+        if (n > 0) {
+            if (kinds4[p] == 0) {
+                mv = moves[or_np_randint(&rng[p], n)];
+            } else if (kinds4[p] == 1) {
+                mv = heur_choice_c(b, p, &rng[p], moves, sc);
+            } else if (kinds4[p] == 2) {
+                if (n == 1) { mv = moves[0]; }
+                else {
+                    int32_t best, hits, nch;
+                    g_rollout_policy = 1;
+                    if (tcount[p] * 2 + 2 * (mcts_iters + 1) > tcap) {  /* reference clears at 500k */
+                        for (int i = 0; i < tcap; ++i) tvals[p][i] = NAN;
+                        tcount[p] = 0;
+                    }
+                    or_mcts(b, p, mcts_iters, 1.414, 50, lt, mcts_iters + 2, ztab[p], &rng[p], 1, tkeys[p],
+                            tvals[p], tcap, &tcount[p], &best, &hits, rw, hf, cm, cv, ct, 1, &nch);
+                    g_rollout_policy = 0;
+                    mv = best;
+                }
+            } else {
+                int32_t nodes, tm[1], tv[1];
+                double tq[1];
+                or_fastmcts(b, p, (int64_t)seeds4[p] + turns, fast_iters, BK_ORDER_FRONTIER, &mv, &nodes, tm, tv, tq, 1);
+            }
+        }
+        if (mv < 0) { b->cur = (b->cur + 1) & 3; continue; }
+        or_place_move(b, p, mv);
+        b->cur = (p + 1) & 3;
+        ++plies;
+    }
+    int32_t wm;
+    or_game_scores(b, scores4, &wm);
+    for (int p = 0; p < 4; ++p) { free(ztab[p]); free(tkeys[p]); free(tvals[p]); }
+    free(lt); free(moves); free(sc); free(rw); free(hf); free(b);
+    return plies;
 }

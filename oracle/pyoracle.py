@@ -103,6 +103,8 @@ def lib():
             "or_philox_stream": (C.c_uint32, [C.c_uint64, C.c_uint32, C.c_uint32]),
             "or_playout_arena_philox": (C.c_int, [P(Board), C.c_uint64, C.c_uint32, C.c_int, C.c_int, C.c_int,
                                                   P(Result), P(C.c_int32), C.c_int]),
+            "or_heuristic_score": (C.c_double, [P(Board), C.c_int, C.c_int]),
+            "or_arena4_game": (C.c_int, [P(C.c_int32), P(C.c_uint32), C.c_int, C.c_int, P(C.c_int32)]),
             "or_set_frontier_table": (C.c_int, [P(Board), C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
             "or_mcts": (C.c_int, [P(Board), C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int,
                                   C.c_void_p, P(MT), C.c_int, C.c_void_p, C.c_void_p, C.c_int,
@@ -459,3 +461,14 @@ def heuristic_rollout_a(b, player, rng, max_moves=50):
         cur = (cur + 1) & 3
         plies += 1
     return board_score(sim, player) - start, plies
+
+
+def arena4_game(kinds, seeds, mcts_iters=64, fast_iters=1000):
+    """One config-4 arena game in C (seat kinds 0 random, 1 heuristic, 2 MCTS with
+    heuristic rollouts, 3 FastMCTS): (plies, scores).  The CPU baseline of bench.py's
+    config-4 line (ctypes releases the GIL, so threads run games in parallel)."""
+    k = (C.c_int32 * 4)(*kinds)
+    sd = (C.c_uint32 * 4)(*[int(x) & 0xFFFFFFFF for x in seeds])
+    sc = (C.c_int32 * 4)()
+    plies = lib().or_arena4_game(k, sd, mcts_iters, fast_iters, sc)
+    return plies, list(sc)

@@ -117,8 +117,12 @@ def order_moves_many(rows: np.ndarray, frontiers: Sequence[Sequence]):
     m = rows.shape[0]
     if m == 0:
         return []
-    bits = np.unpackbits(rows.view(np.uint8).reshape(m, 91, 20, 4), axis=3, bitorder="little")
-    gi, g, r, c = np.nonzero(bits)  # game-major, then naive order
+    # only the nonzero row words are unpacked (most of the 91 x 20 rows hold no anchor)
+    gi, g, r = np.nonzero(rows)
+    words = rows[gi, g, r]
+    bits = np.unpackbits(words.view(np.uint8).reshape(-1, 4), axis=1, bitorder="little")
+    w, c = np.nonzero(bits)  # word-major (game, g, r ascending), columns ascending
+    gi, g, r = gi[w], g[w], r[w]
     rank = np.full((m, 400), _BIG, dtype=np.int64)
     for i, fr in enumerate(frontiers):
         for j, (a, b) in enumerate(fr):

@@ -60,6 +60,10 @@ def _positions(move: Move) -> List[Position]:
     return [Position(move.anchor_row + int(r), move.anchor_col + int(c)) for r, c in zip(*np.nonzero(shape))]
 
 
+# search_packed's running totals (bench / arena profiling): launches, their kernel time
+# (HIP events around bk_mcts), simulations and rollout plies
+SEARCH_TOTALS: Dict[str, float] = {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0}
+
 # Timed searches (time_limit): iteration bound per second of limit, and overall.  One
 # search runs ~100-1,000 iterations/s on the GPU (a lane of a persistent wave), so the
 # bound is not reached in practice; if it is, stats say so and a warning is issued.
@@ -290,6 +294,10 @@ class MCTSAgent:
                          mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us,
                          rollout_policy=policy)
             dt = time.time() - t0
+            SEARCH_TOTALS["launches"] += 1
+            SEARCH_TOTALS["kernel_ms"] += gpu.last_kernel_ms()
+            SEARCH_TOTALS["sims"] += int(r["out"]["iterations_run"].sum())
+            SEARCH_TOTALS["rollout_plies"] += int(r["out"]["rollout_plies"].astype(np.int64).sum())
             for j, (i, a) in enumerate(zip(idx, ags)):
                 o = r["out"][j]
                 st = rng_states[j]

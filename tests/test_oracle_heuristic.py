@@ -65,3 +65,24 @@ def test_full_games(game):
     assert trace == g["trace"]
     assert list(scores) == g["scores"] and (passes, turns) == (g["passes"], g["turns"])
     assert [p + 1 for p in range(4) if wm >> p & 1] == g["winner_ids"]
+
+
+def test_c_heuristic_score_equals_pinned_restatement():
+    """or_heuristic_score (the C _evaluate_move behind the config-4 CPU baseline) equals
+    pyoracle.heuristic_score, which tests/golden/heuristic.json pins to the reference."""
+    from tests.helpers import POS, replay
+    n = 0
+    for rec in POS[:24]:
+        b = replay(rec)
+        for p in range(4):
+            for mv in O.legal_moves(b, p, O.ORDER_FRONTIER)[::3]:
+                assert O.lib().or_heuristic_score(O.C.byref(b), p, mv) == O.heuristic_score(b, p, mv)
+                n += 1
+    assert n > 1000
+
+
+def test_c_arena4_game_runs_and_is_deterministic():
+    """or_arena4_game (config-4 CPU baseline): a full mixed-seat game, reproducible."""
+    a = O.arena4_game([0, 1, 2, 3], [5, 6, 7, 8], 8, 50)
+    b = O.arena4_game([0, 1, 2, 3], [5, 6, 7, 8], 8, 50)
+    assert a == b and a[0] > 40 and sum(a[1]) > 150
