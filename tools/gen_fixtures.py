@@ -39,6 +39,10 @@ What is recorded (all reference behaviour, nothing re-implemented here):
                           self-play, full 4-heuristic games, MCTSAgent searches with its
                           default HeuristicAgent rollouts, and run_single_game records of
                           mixed random/heuristic/mcts/fast_mcts arenas
+* ``arena_bench.json`` -- run_single_game records of bench.py's config-4 seats (MCTS 64
+                          iterations with 50-ply heuristic rollouts, FastMCTS 1,000
+                          iterations), games 0..3 of run seed 20260301 (``arena_bench``
+                          only, not part of ``all``)
 """
 from __future__ import annotations
 
@@ -557,6 +561,31 @@ def _heur_arena_game(gi):
     return {k: rec[k] for k in keep}
 
 
+# bench.py's config-4 seats (CONFIG4_AGENTS, run seed 20260301): MCTS 64 iterations with
+# 50-ply HeuristicAgent rollouts, FastMCTS 20 iterations/ms x 50 ms deterministic budget
+ARENA_BENCH = {"agents": [{"name": "random", "type": "random"}, {"name": "heuristic", "type": "heuristic"},
+                          {"name": "mcts", "type": "mcts", "params": {"iterations": 64, "max_rollout_moves": 50}},
+                          {"name": "fast_mcts", "type": "fast_mcts", "thinking_time_ms": 50,
+                           "params": {"deterministic_time_budget": True, "iterations_per_ms": 20.0}}],
+               "num_games": 4, "seed": 20260301, "seat_policy": "round_robin", "output_root": "/tmp/arena_fx4"}
+
+
+def _bench_arena_game(gi):
+    _setup()
+    from analytics.tournament.arena_runner import (RunConfig, _seat_assignment_for_game, game_seed_from_run_seed,
+                                                   run_single_game)
+    cfg = RunConfig.from_dict(ARENA_BENCH)
+    gs = game_seed_from_run_seed(cfg.seed, gi)
+    seats = _seat_assignment_for_game([a.name for a in cfg.agents], gi, gs, cfg.seat_policy)
+    rec, _ = run_single_game(run_id="fx4", game_index=gi, game_seed=gs, run_config=cfg, seat_assignment=seats,
+                             agent_configs={a.name: a for a in cfg.agents})
+    keep = ("game_index", "game_seed", "seat_assignment", "winner_ids", "final_scores", "moves_made",
+            "turn_count", "passes", "invalid_actions", "is_tie", "error")
+    out = {k: rec[k] for k in keep}
+    out["mcts_total_simulations"] = rec["agent_move_stats"]["mcts"]["total_simulations"]
+    return out
+
+
 def gen_heuristic():
     with Pool(8) as pool:
         cases = pool.map(_heur_case, HEUR_CASES)
@@ -635,6 +664,9 @@ def main():
             dump("mcts.json", pool.map(gen_mcts_case, MCTS_CASES))
     if what in ("all", "heuristic"):
         dump("heuristic.json", gen_heuristic())
+    if what == "arena_bench":  # ~30 min: MCTS seats with heuristic rollouts in Python
+        with Pool(4) as pool:
+            dump("arena_bench.json", {"config": ARENA_BENCH, "games": pool.map(_bench_arena_game, range(4))})
 
 
 if __name__ == "__main__":
