@@ -330,6 +330,62 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
     return total;
 }
 
+// Tuning variant (BK_STENCIL_LITERAL): every stencil-table entry as its own
+// straight-line code with literal column shifts (code = t | shift << 8), piece and
+// orientation as constants -- no scalar table loads, no shift amounts moved from SGPRs.
+template <int H, int... CODES>
+struct StencilEntry {
+    static constexpr int NT = sizeof...(CODES);
+    static constexpr int NR = 21 - H;
+    static constexpr int cs[NT] = {CODES...};
+    template <int K>
+    __device__ __forceinline__ static uint64_t tv(const Planes& P, int r) {
+        constexpr int d = (cs[K] & 0xFF) >> 2, kind = cs[K] & 3, sh = cs[K] >> 8;
+        const uint64_t v = kind == 1 ? P.BCP[r + d] : kind == 2 ? P.BCV[r + d] : P.BC[r + d];
+        return sh == 0 ? v : v >> sh;
+    }
+    template <int K>
+    __device__ __forceinline__ static uint32_t fold(const Planes& P, int r, uint32_t b, uint32_t c) {
+        if constexpr (K + 2 <= NT - 1) {
+            const uint64_t t0 = tv<K>(P, r), t1 = tv<K + 1>(P, r);
+            b = BITOP3(b, (uint32_t)t0, (uint32_t)t1, LUT_OR3);
+            c = BITOP3(c, (uint32_t)(t0 >> 32), (uint32_t)(t1 >> 32), LUT_OR3);
+            return fold<K + 2>(P, r, b, c);
+        } else if constexpr (K + 2 == NT) {
+            const uint64_t t0 = tv<K>(P, r), t1 = tv<K + 1>(P, r);
+            b = BITOP3(b, (uint32_t)t0, (uint32_t)t1, LUT_OR3);
+            c = c | (uint32_t)(t0 >> 32);
+            return BITOP3(c, (uint32_t)(t1 >> 32), b, LUT_OR2_ANDN);
+        } else if constexpr (K + 1 == NT) {
+            const uint64_t t0 = tv<K>(P, r);
+            b = b | (uint32_t)t0;
+            return BITOP3(c, (uint32_t)(t0 >> 32), b, LUT_OR2_ANDN);
+        } else {
+            return BITOP3(c, b, b, LUT_ANDN);
+        }
+    }
+    __device__ __forceinline__ static uint32_t count(const Planes& P) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint64_t t0 = tv<0>(P, r);
+            acc = bcnt_acc(fold<1>(P, r, (uint32_t)t0, (uint32_t)(t0 >> 32)), acc);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        return acc;
+    }
+};
+
+template <bool STORE, int PIECE, int G, int H, int... CODES>
+__device__ __forceinline__ uint32_t count_entry(const Planes& P, uint32_t avail, uint32_t* cl) {
+    const bool av = (avail >> (PIECE - 1)) & 1u;
+    if (__builtin_amdgcn_ballot_w64(av) == 0ull) return 0u;
+    uint32_t c = StencilEntry<H, CODES...>::count(P);
+    c = av ? c : 0u;
+    if constexpr (STORE) atomicAdd(cl + (G / 3) * WAVE, c << (10 * (G % 3)));
+    return c;
+}
+
 template <bool STORE>
 __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane) {
     uint32_t t = 0;
@@ -345,9 +401,16 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     int tb0 = 0;
     asm volatile("" : "+s"(tb0));
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
+#ifdef BK_STENCIL_LITERAL
+    (void)tb0;
+#define BK_COUNT_ENTRY(PIECE, G, H, ...) t += count_entry<STORE, PIECE, G, H, __VA_ARGS__>(P, avail, cl);
+    BK_ENTRY_LIST(BK_COUNT_ENTRY)
+#undef BK_COUNT_ENTRY
+#else
 #define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl);
     BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
+#endif
     return t;
 }
 
