@@ -475,6 +475,12 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                 for i, a, p, lg in by_kind["mcts"]:
                     if len(lg) == 1:
                         chosen[i] = lg[0]
+                        # select_action returns the only move without a search (mcts_agent.py
+                        # :319-320), and the arena reads the agent's stats as they are: the
+                        # previous search's iterations_run (0 before any) counts again
+                        e = per_agent[i][seats[i][str(p + 1)]]
+                        e["total_simulations"] += a.agent.stats["iterations_run"]
+                        e["moves_with_simulations"] += 1
                 if todo:
                     ti = np.array([t[0] for t in todo])
                     tm = time.perf_counter()

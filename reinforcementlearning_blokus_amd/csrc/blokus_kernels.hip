@@ -30,7 +30,6 @@
 //     counter, keeps its board in a lane-strided scratch slab (L2-resident rows),
 //     and never returns to the host between plies.
 #include <hip/hip_runtime.h>
-#include <initializer_list>
 
 #include <math.h>
 #include <stdint.h>
@@ -806,7 +805,6 @@ struct MovegenArgs {
     uint8_t* out_mask4;      // has_moves mode
     int32_t groups;          // k_movegen_g: orientation groups per board-player
     uint64_t* out_mask;      // k_movegen_m: n x 91 x 7 (bit 20 r + c of the 400-bit mask) or NULL
-    const int32_t* gsplit;   // k_movegen_m: group g covers orientations [gsplit[g], gsplit[g + 1])
 };
 
 __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&own)[4][20], uint32_t (&occ)[20]) {
@@ -897,31 +895,10 @@ __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
 // XCD's L2 (not once per XCD) and the partial 128-B lines of one board's mask, written by
 // different group waves, merge in the same L2.
 #define MG_XCDS 8
-// Dense rows of the class's entries whose orientation lies in [g0, g1) (k_movegen_m)
-template <int H, int... T, typename F>
-__device__ __forceinline__ void rows_class_range(int i0, int i1, int g0, int g1, const Planes& P, F&& f) {
-#pragma unroll 1
-    for (int i = i0; i < i1; ++i) {
-        const uint32_t w0 = kClass[i][0], w1 = kClass[i][1];
-        const int g = (int)(w0 >> 8);
-        if (g < g0 || g >= g1) continue;
-        uint32_t ok[20];
-#pragma unroll
-        for (int r = 0; r < 20; ++r) ok[r] = 0u;
-        StencilClass<H, T...>::scan(P, w1, [&](int r, uint32_t v) { ok[r] = v; });
-        f(g, w0 & 0xFFu, ok);
-    }
-}
-
-// Group grp of a board set covers the CONTIGUOUS orientations [a.gsplit[grp],
-// a.gsplit[grp + 1]) -- split on the host into equal stencil work -- so each lane writes
-// one contiguous span of its board's mask (whole 128-B lines, not 56-B pieces interleaved
-// with other waves' writes).
 __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
     const int G = a.groups;
     const int xcd = blockIdx.x % MG_XCDS, j = blockIdx.x / MG_XCDS;
     const int set = xcd + MG_XCDS * (j / G), grp = j % G;
-    const int g0 = a.gsplit[grp], g1 = a.gsplit[grp + 1];
     const int i = set * WAVE + threadIdx.x;
     const bool live = i < a.n;
     const int idx = live ? i : 0;
@@ -962,9 +939,9 @@ __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
         }
     };
     if (set * WAVE < a.n) {  // a grid rounded up to a multiple of 8 sets has idle blocks
-#define BK_ROWS_RANGE(i0, i1, H, ...) rows_class_range<H, __VA_ARGS__>(i0, i1, g0, g1, P, emit);
-        BK_CLASS_LIST(BK_ROWS_RANGE)
-#undef BK_ROWS_RANGE
+#define BK_ROWS_GROUP(i0, i1, H, ...) rows_class_group<H, __VA_ARGS__>(i0, i1, grp, G, P, emit);
+        BK_CLASS_LIST(BK_ROWS_GROUP)
+#undef BK_ROWS_GROUP
     }
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
 }
@@ -3324,7 +3301,6 @@ struct bk_handle_s {
     void* d_out = nullptr; size_t d_out_cap = 0;
     void* d_aux = nullptr; size_t d_aux_cap = 0;
     void* d_aux2 = nullptr; size_t d_aux2_cap = 0;
-    void* d_mg_split = nullptr; int mg_split_groups = 0;  // k_movegen_m orientation ranges
     void* d_slab = nullptr; size_t d_slab_cap = 0;
     void* d_fin = nullptr; size_t d_fin_cap = 0;     // frontier: root tables
     void* d_fout = nullptr; size_t d_fout_cap = 0;   // frontier: advanced tables
@@ -3426,7 +3402,7 @@ int bk_destroy(bk_handle h) {
     (void)hipSetDevice(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_mc, h->d_mclane, h->d_counter, h->d_mg_split};
+                    h->d_mc, h->d_mclane, h->d_counter};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -3535,8 +3511,7 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
     if (groups < 1) groups = 1;
     if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
-    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups, nullptr,
-                  nullptr};
+    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups, nullptr};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     const int grid = waves * groups;
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
@@ -3583,38 +3558,7 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     if (groups < 1) groups = 1;
     if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
     const int sets = ((waves + MG_XCDS - 1) / MG_XCDS) * MG_XCDS;
-    // contiguous orientation ranges of equal stencil work ((21 - height) rows x terms)
-    int32_t split[MG_GROUPS_MAX + 1];
-    {
-        static const uint32_t cls[BK_NUM_ORIENTS][2] = BK_CLASS_TABLE_INIT;
-        double cost[BK_NUM_ORIENTS] = {0}, tot = 0.0;
-#define BK_COST(i0, i1, H, ...)                                                           \
-        for (int i_ = i0; i_ < i1; ++i_) {                                                 \
-            const int nt_ = std::initializer_list<int>{__VA_ARGS__}.size();                \
-            cost[cls[i_][0] >> 8] = (double)(21 - H) * (nt_ + 1);                          \
-        }
-        BK_CLASS_LIST(BK_COST)
-#undef BK_COST
-        for (int g = 0; g < BK_NUM_ORIENTS; ++g) tot += cost[g];
-        double run = 0.0;
-        int k = 1;
-        split[0] = 0;
-        for (int g = 0; g < BK_NUM_ORIENTS && k < groups; ++g) {
-            run += cost[g];
-            while (k < groups && run >= tot * k / groups) split[k++] = g + 1;
-        }
-        while (k < groups) split[k++] = BK_NUM_ORIENTS;
-        split[groups] = BK_NUM_ORIENTS;
-    }
-    if (h->mg_split_groups != groups) {  // a per-handle device copy, rebuilt when G changes
-        if (!h->d_mg_split) HIPCHK(h, hipMalloc(&h->d_mg_split, sizeof(int32_t) * (MG_GROUPS_MAX + 1)));
-        HIPCHK(h, hipStreamSynchronize(h->cur));
-        HIPCHK(h, hipMemcpy(h->d_mg_split, split, sizeof(int32_t) * (size_t)(groups + 1), hipMemcpyHostToDevice));
-        h->mg_split_groups = groups;
-    }
-    const void* d_split = h->d_mg_split;
-    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, nullptr, d_count, nullptr, groups, d_mask,
-                  (const int32_t*)d_split};
+    MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, nullptr, d_count, nullptr, groups, d_mask};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);
@@ -3643,7 +3587,7 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
         if (rc) return rc;
         d_mask = (uint8_t*)h->d_out;
     }
-    MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask, 0, nullptr, nullptr};
+    MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask, 0, nullptr};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     hipLaunchKernelGGL(k_has_moves, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
