@@ -1556,6 +1556,10 @@ struct RolloutArgs {
     FsLane* fslab;             // frontier order: one record per slot
     const uint8_t* seat_masks; // bk_arena_advance: per game, bits 0-3 heuristic seats, 4-7 stop seats
     uint32_t* rng_io;          // bk_arena_advance: per game 4 seats x MT cursor, in/out
+    int32_t handout;           // 0: every lane pulls playouts from the counter; 1: slot s plays
+                               // s, s + nslots, ...; 2: slot s plays s, then only slots
+                               // < long_slots pull the rest from the counter (whole waves)
+    uint32_t long_slots;
 };
 
 // four per-player scalars (kept as separate SSA values: an array indexed by a
@@ -1916,13 +1920,24 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     Game g;
     g.pid = -1;
     bool done = false;
+    uint32_t handed = 0;  // playouts this slot has taken (handout 1, 2)
     SECT_DECL
     for (uint32_t iter = 0;; ++iter) {
         SECT(0);
         // ---- make sure this lane has a game whose current player may still move
         for (int guard = 0; guard < 3 && !done; ++guard) {
             if (g.pid < 0) {
-                const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
+                int32_t next;
+                if (a.handout == 0) {
+                    next = (int32_t)atomicAdd(&a.counter[0], 1u);
+                } else if (handed == 0u) {
+                    next = (int32_t)slot;
+                } else if (a.handout == 1) {
+                    next = (int32_t)(slot + handed * a.nslots);
+                } else {
+                    next = slot < a.long_slots ? (int32_t)(a.nslots + atomicAdd(&a.counter[0], 1u)) : a.n_playouts;
+                }
+                ++handed;
                 if (next >= a.n_playouts) { done = true; break; }
                 start_game<FR>(a, g, slab, slot, next, htab);
             }
@@ -3689,13 +3704,27 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     HIPCHK(h, hipMemsetAsync(h->d_counter, 0, 2 * sizeof(uint32_t), h->cur));  // [2] is sticky
     const uint64_t per_lane = ((uint64_t)n_playouts + nslots - 1) / nslots + 1;
     const uint64_t per_game = (cfg->semantics == BK_SEM_ROLLOUT ? (uint64_t)cfg->max_plies + 2u : 100u);
-    uint64_t iters = per_lane * per_game + 64u;
+    uint64_t iters = 2 * per_lane * per_game + 64u;  // 2x: uneven hand-outs (handout 2)
     if (const char* dbg = getenv("BK_DEBUG_MAX_ITERS")) iters = strtoull(dbg, nullptr, 10);  // tests: force the guard
     RolloutArgs a{(const bk_state*)d_roots, n_roots, (const int32_t*)d_idx, n_playouts, *cfg,
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
                   (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr,
-                  (const uint8_t*)d_masks, (uint32_t*)d_rng};
+                  (const uint8_t*)d_masks, (uint32_t*)d_rng, 2, 0u};
+    // Playout hand-out.  Config 3 has 1.33 playouts per resident slot: pulled per lane
+    // from one counter (handout 0), the extra third lands on lanes of EVERY wave, and each
+    // wave then runs a second playout length with a third of its lanes; given to whole
+    // waves (2: slot s plays s first, then only the first slots -- whole waves, one per
+    // SIMD -- pull the rest), the other waves finish and free their SIMD time.  57.0 M ->
+    // 60.2 M playouts/s (profiles/r03/sweeps/handout.jsonl).  Results depend only on the
+    // playout id, not on the slot (tests/test_gpu_parity.py slot independence).
+    if (const char* env = getenv("BK_HANDOUT")) a.handout = atoi(env);  // tuning override
+    if (a.handout < 0 || a.handout > 2) a.handout = 0;
+    {
+        const int64_t rest = (int64_t)n_playouts - (int64_t)nslots;
+        int64_t ls = rest <= 0 ? 0 : rest >= (int64_t)nslots ? (int64_t)nslots : ((rest + WAVE - 1) / WAVE) * WAVE;
+        a.long_slots = (uint32_t)ls;
+    }
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (heur)
         hipLaunchKernelGGL(k_rollout_fr_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
