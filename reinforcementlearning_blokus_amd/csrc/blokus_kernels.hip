@@ -3710,13 +3710,14 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
                   (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr,
-                  (const uint8_t*)d_masks, (uint32_t*)d_rng, 2, 0u};
+                  (const uint8_t*)d_masks, (uint32_t*)d_rng, fr ? 0 : 2, 0u};
     // Playout hand-out.  Config 3 has 1.33 playouts per resident slot: pulled per lane
     // from one counter (handout 0), the extra third lands on lanes of EVERY wave, and each
     // wave then runs a second playout length with a third of its lanes; given to whole
     // waves (2: slot s plays s first, then only the first slots -- whole waves, one per
     // SIMD -- pull the rest), the other waves finish and free their SIMD time.  57.0 M ->
-    // 60.2 M playouts/s (profiles/r03/sweeps/handout.jsonl).  Results depend only on the
+    // 60.2 M playouts/s (profiles/r03/sweeps/handout.jsonl).  The frontier-order kernels
+    // keep 0 (22.4 vs 21.5 M: their playout lengths vary more).  Results depend only on the
     // playout id, not on the slot (tests/test_gpu_parity.py slot independence).
     if (const char* env = getenv("BK_HANDOUT")) a.handout = atoi(env);  // tuning override
     if (a.handout < 0 || a.handout > 2) a.handout = 0;
