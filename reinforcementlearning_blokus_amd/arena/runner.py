@@ -329,6 +329,28 @@ def run_games_gpu(run_config: RunConfig, game_indices: Sequence[int], *, run_id:
 
 _SEARCH_KINDS = ("mcts", "fast_mcts", "gameplay_fast_mcts", "gameplay_mcts")
 
+_MOVE_TABLES = None
+
+
+def _move_tables():
+    """(uint64[91 * 400, 7] plane words of each move int g * 400 + anchor (0 for off-board
+    anchors), int64[91] piece index 0..20 of each orientation), built once."""
+    global _MOVE_TABLES
+    if _MOVE_TABLES is None:
+        from ..engine.pieces import ORIENT_CELLS, ORIENT_LIST
+        masks = np.zeros((91 * 400, 7), np.uint64)
+        for g, cells in enumerate(ORIENT_CELLS):
+            for a in range(400):
+                ar, ac = divmod(a, 20)
+                cs = [(ar + dr, ac + dc) for dr, dc in cells]
+                if all(0 <= r < 20 and 0 <= c < 20 for r, c in cs):
+                    for r, c in cs:
+                        k = r * 20 + c
+                        masks[g * 400 + a, k // 64] |= np.uint64(1) << np.uint64(k % 64)
+        pieces = np.array([pid - 1 for pid, _o in ORIENT_LIST], np.int64)
+        _MOVE_TABLES = (masks, pieces)
+    return _MOVE_TABLES
+
 
 def _batchable(run_config: RunConfig, seats: Mapping[str, str]) -> bool:
     """run_games_batched can play this seating: random / default-weight heuristic seats
@@ -515,23 +537,27 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                     if len(g) > 1:
                         e["total_simulations"] += it
                         e["moves_with_simulations"] += 1
-            for i in stopped:  # place the search moves (Board.place_piece, engine/board.py:515-555)
-                p = int(states["current_player"][i]) & 3
-                m = chosen.get(i)
-                states["reserved"][i, 0] += 1  # turn_count
-                if m is None:  # agent returned no move: the reference passes (arena_runner.py:683-687)
-                    states["reserved"][i, 1] += 1
-                    states["current_player"][i] = (p + 1) & 3
-                    continue
-                g, a = divmod(int(m), 400)
-                cells = [(a // 20 + dr) * 20 + a % 20 + dc for dr, dc in ORIENT_CELLS[g]]
-                for c in cells:
-                    states["planes"][i, p, c // 64] |= np.uint64(1) << np.uint64(c % 64)
-                states["used"][i, p] |= np.uint32(1 << (ORIENT_LIST[g][0] - 1))
-                states["first_move"][i] &= np.uint8(~(1 << p) & 0xFF)
-                states["move_count"][i] += 1
-                states["current_player"][i] = (p + 1) & 3
-                N.fset_place(sets[i:i + 1], states[i:i + 1], p, cells)
+            # place the search moves (Board.place_piece, engine/board.py:515-555), all games
+            # of the round at once; the frontier tables per game (CPython set order)
+            th = time.perf_counter()
+            sp = (states["current_player"][stopped] & 3).astype(np.int64)
+            mv = np.array([-1 if chosen.get(i) is None else int(chosen[i]) for i in stopped], np.int64)
+            states["reserved"][stopped, 0] += 1  # turn_count
+            passed = mv < 0  # agent returned no move: the reference passes (arena_runner.py:683-687)
+            states["reserved"][stopped[passed], 1] += 1
+            pm, pp, mm = stopped[~passed], sp[~passed], mv[~passed]
+            if len(pm):
+                masks_, pieces_ = _move_tables()
+                states["planes"][pm, pp, :] |= masks_[mm]
+                states["used"][pm, pp] |= (np.uint32(1) << pieces_[mm // 400].astype(np.uint32))
+                states["first_move"][pm] &= (~(np.uint8(1) << pp.astype(np.uint8))).astype(np.uint8)
+                states["move_count"][pm] += 1
+                for i, p, m in zip(pm.tolist(), pp.tolist(), mm.tolist()):
+                    g, a = divmod(m, 400)
+                    N.fset_place(sets[i:i + 1], states[i:i + 1], p,
+                                 [(a // 20 + dr) * 20 + a % 20 + dc for dr, dc in ORIENT_CELLS[g]])
+            states["current_player"][stopped] = ((sp + 1) & 3).astype(np.uint8)
+            prof["place_s"] = prof.get("place_s", 0.0) + time.perf_counter() - th
         active = np.array([i for i in active if results[i] is None], dtype=np.int64)
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
