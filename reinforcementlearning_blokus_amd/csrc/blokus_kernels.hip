@@ -3127,7 +3127,11 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     Mc m;
     m.game = -1;
     m.mode = MC_SELECT;
+    // section timers (-DBK_SECTION_PROF): 0 tree, 1 derive + rows, 2 lane orientations +
+    // scan, 3 draw + pick, 4 locate / heuristic walk, 5 frontier ops + place + expansion
+    SECT_DECL
     for (uint64_t step = 0;; ++step) {
+        SECT(5);
         // ---- tree work until the search needs a movegen (uniform over the wave)
         bool done = false;
         while (m.mode == MC_SELECT) {
@@ -3147,6 +3151,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             mc_replay(a, m, slab, L, htab);
             m.mode = MC_EXPAND;
         }
+        SECT(0);
         if (done) break;
         if (step > a.max_steps) {  // safety valve: never spin forever
             if (lane == 0) { atomicOr(&a.counter[1], 1u); atomicOr(&a.counter[2], BK_STICKY_GUARD); }
@@ -3170,12 +3175,14 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         // Board.move_count of the rollout board: placements on the way from the root
         const int edge_w = (int)(a.roots[m.game].move_count + m.depth + m.plies) < 30 ? 6 : 3;
+        SECT(1);
         uint32_t cnt[2];
         double es[2];
         if (hroll) coop_orients<true>(rows_lds, avail, lane, hs, edge_w, cnt, es);
         else coop_orients<false>(rows_lds, avail, lane, hs, edge_w, cnt, es);
         const CoopScan sc = coop_scan(cnt, lane);
         const uint32_t total = sc.total;
+        SECT(2);
         bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
         uint32_t k = 0;
         if (m.mode == MC_EXPAND) {
@@ -3233,6 +3240,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         }
         FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
         int ar, ac;
+        SECT(3);
         if (hroll) {
             if (gs < 0) {
                 ar = -1;
@@ -3250,6 +3258,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             m.mode = MC_SELECT;
             continue;
         }
+        SECT(4);
         uint32_t pm[5];
         int32_t cells[5];
         piece_cells(gs, ar, ac, pm, cells);
@@ -3296,6 +3305,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
                 mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
         }
     }
+    SECT_FLUSH;
 }
 
 __global__ __launch_bounds__(COOP_WAVES * WAVE) void k_mcts_coop(MctsArgs a) { mcts_coop_body<false>(a); }

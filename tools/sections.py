@@ -111,9 +111,41 @@ def run_mcts():
              {"games": games, "iterations": f"{iters - 64}..{iters}", "kernel_ms": gpu.last_kernel_ms()})
 
 
+def run_coop():
+    """k_mcts_coop(_h) sections (one wave per search): 512 searches x 64 iterations with
+    heuristic rollouts (a config-4 arena round) and with random rollouts."""
+    os.environ["BK_LIB_PATH"] = LIB
+    os.environ["BK_MCTS_COOP"] = "1"
+    sys.path.insert(0, ROOT)
+    import ctypes as C
+
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    gpu = BlokusGPU(0)
+    L = N.load()
+    buf = (C.c_uint64 * 16)()
+    names = {0: "tree", 1: "derive+rows", 2: "lane orientations+scan", 3: "draw+pick",
+             4: "locate / heuristic walk", 5: "frontier ops+place+expand"}
+    for policy in (N.MCTS_ROLLOUT_HEURISTIC, N.MCTS_ROLLOUT_RANDOM):
+        roots, sets = frontier_roots(gpu, 512, 24, seed=11)
+        b = MctsBatch(gpu, roots, sets, iterations=64, seed0=3)
+        L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
+        b.run(rollout_policy=policy)
+        rc = L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
+        assert rc == 0, rc
+        tot = sum(buf)
+        rows = {names.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
+        print(json.dumps({"run": "k_mcts_coop_h" if policy == N.MCTS_ROLLOUT_HEURISTIC else "k_mcts_coop",
+                          "searches": 512, "iterations": 64, "kernel_ms": gpu.last_kernel_ms(), "cycles": tot,
+                          "share": rows}), flush=True)
+
+
 if __name__ == "__main__":
     if "--build" in sys.argv:
         build()
+    elif "--coop" in sys.argv:
+        run_coop()
     elif "--mcts" in sys.argv:
         run_mcts()
     else:
