@@ -572,6 +572,34 @@ __device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2
 // anchors of gs over the B half of each LDS row.  Pass 2 walks the mover's frontier set
 // in slot order and the orientation's cells in order; an anchor counts at its first
 // (frontier cell, cell k) hit, and its bit is cleared when it is counted.
+// Pass 1 of locate_move_frontier alone: the legal anchors of gs over the C half of each
+// LDS row (rows[r].y; the B half stays)
+__device__ __forceinline__ void locate_pass1(int gs, uint2* rows) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    const int rlim = 20 - (int)((info >> 16) & 0xFFu);
+    const uint2* base[5];
+    uint32_t sh[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        base[k] = rows + (cell >> 8) * WAVE;
+        sh[k] = cell & 0xFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        const int rr = r < rlim ? r : rlim;
+        uint2 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = base[k][rr * WAVE];
+        uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
+        uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
+        ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
+        ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
+        rows[r * WAVE].y = r <= rlim ? (ac & ~ab) : 0u;
+    }
+}
+
 __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2* rows, const int16_t* key,
                                                      int mask, int& out_r, int& out_c) {
     const uint32_t info = kInfo[gs];
@@ -2376,6 +2404,7 @@ struct MctsArgs {
     uint64_t limit_ticks;  // cfg.time_limit_us in wall-clock (s_memrealtime) ticks
     int32_t tree_batch;    // tree phase once this many lanes of a wave wait for it (or no lane is busy)
     int32_t spread;        // only lanes with lane % spread == 0 take searches (more waves, fewer lanes each)
+    int32_t coop_walk;     // k_mcts_coop(_h): frontier walk split over the wave (coop_walk), else serial
 };
 
 struct Mc {
@@ -3104,12 +3133,134 @@ __device__ __forceinline__ int coop_heur_pick(const double* es, const double* ps
     return gstar;
 }
 
+__device__ __forceinline__ double wave_incl_scan_f64(double v, int lane) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const double u = __shfl_up(v, o);
+        v += lane >= o ? u : 0.0;
+    }
+    return v;
+}
+
+// Cooperative pass 2 of locate_move_frontier / heur_walk_frontier (one wave = one search;
+// the legal anchors of gs in rows[r * WAVE].y, identical in every lane's column).  Lane j
+// takes the table's slots j and j + 64.  The anchor a = f - cell_k of the key f at slot s
+// is NEW there -- the serial walk counts it at s -- iff no key of an earlier slot is
+// another cell of the piece placed at a: rank[a + cell_q] > s for every q != k, where
+// rank holds each key's slot (0x7FFF elsewhere; wave-private LDS).  Count mode (E =
+// false): the kk-th new anchor in (slot, cell) order.  E: the anchor whose cumulative e
+// from R first exceeds target, certified as in heur_walk_frontier (the prefix sums differ
+// from the serial ones by rounding only, far inside the margin).  Tables of more than 128
+// slots return false: the caller walks serially.
+template <bool E>
+__device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows, const int16_t* key, int mask,
+                                          int16_t* rank, int lane, const HeurShared* hs, int edge_w, double target,
+                                          double R, double total, int& out_r, int& out_c, bool& uncertain) {
+    if (mask > 2 * WAVE - 1) return false;
+    int n;
+    uint32_t cd[5], cc[5];
+    orient_cells(gs, n, cd, cc);
+#pragma unroll
+    for (int t = 0; t < 7; ++t)
+        if (lane + WAVE * t < BK_CELLS) rank[lane + WAVE * t] = 0x7FFF;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int f[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int sl = lane + WAVE * h;
+        f[h] = sl <= mask ? (int)key[sl] : -1;
+        if (f[h] >= 0) rank[f[h]] = (int16_t)sl;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t cnt[2] = {0u, 0u}, newk[2] = {0u, 0u};  // newk bit k: cell k's anchor is new here
+    double es[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (f[h] < 0) continue;
+        const int sl = lane + WAVE * h, fr = f[h] / 20, fc = f[h] - 20 * (f[h] / 20);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k >= n) continue;
+            const int ar = fr - (int)cd[k], acl = fc - (int)cc[k];
+            if (ar < 0 || acl < 0 || !((rows[ar * WAVE].y >> acl) & 1u)) continue;
+            bool fresh = true;
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                if (q < n && q != k && rank[(ar + (int)cd[q]) * 20 + acl + (int)cc[q]] < sl) fresh = false;
+            if (!fresh) continue;
+            newk[h] |= 1u << k;
+            ++cnt[h];
+            if constexpr (E) es[h] += heur_e(n, cd, cc, ar, acl, rows, hs, edge_w);
+        }
+    }
+    // the slot holding the answer, then the anchor inside it in cell order
+    int hit = -1, hh = 0;
+    uint32_t before = 0;
+    double lo = R;
+    if constexpr (!E) {
+        const CoopScan sc = coop_scan(cnt, lane);
+        const uint64_t b0 = __ballot(kk < sc.i0 && kk >= sc.i0 - sc.c0);
+        const uint64_t b1 = __ballot(kk < sc.i1 && kk >= sc.i1 - sc.c1);
+        if (b0) { hit = __ffsll((unsigned long long)b0) - 1; before = __shfl(sc.i0 - sc.c0, hit); }
+        else if (b1) { hit = __ffsll((unsigned long long)b1) - 1; hh = 1; before = __shfl(sc.i1 - sc.c1, hit); }
+    } else {
+        const double i0 = wave_incl_scan_f64(es[0], lane);
+        const double i1 = wave_incl_scan_f64(es[1], lane) + __shfl(i0, WAVE - 1);
+        const uint64_t b0 = __ballot(es[0] > 0.0 && R + i0 > target);
+        const uint64_t b1 = __ballot(es[1] > 0.0 && R + i1 > target);
+        if (b0) { hit = __ffsll((unsigned long long)b0) - 1; }
+        else if (b1) { hit = __ffsll((unsigned long long)b1) - 1; hh = 1; }
+        else {  // rounding put the target past the last anchor: the last one, uncertified
+            uncertain = true;
+            target = 1e300;
+            const uint64_t l1 = __ballot(newk[1] != 0u), l0 = __ballot(newk[0] != 0u);
+            if (l1) { hit = 63 - __clzll((unsigned long long)l1); hh = 1; }
+            else if (l0) { hit = 63 - __clzll((unsigned long long)l0); }
+        }
+        if (hit >= 0) lo = R + __shfl(hh ? i1 - es[1] : i0 - es[0], hit);
+    }
+    if (hit < 0) { out_r = -1; out_c = 0; return true; }
+    // every lane resolves the chosen slot (identical work and result)
+    const int fh = __shfl(hh ? f[1] : f[0], hit);
+    const uint32_t nk = __shfl(hh ? newk[1] : newk[0], hit);
+    const int fr = fh / 20, fc = fh - 20 * (fh / 20);
+    int found_r = -1, found_c = 0, last_r = -1, last_c = 0;
+    uint32_t rem = kk - before;
+    double acc = lo, last_lo = lo, last_e = 0.0;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        if (found_r >= 0 || !((nk >> k) & 1u)) continue;
+        const int ar = fr - (int)cd[k], acl = fc - (int)cc[k];
+        if constexpr (!E) {
+            if (rem == 0u) { found_r = ar; found_c = acl; } else { --rem; }
+        } else {
+            const double e = heur_e(n, cd, cc, ar, acl, rows, hs, edge_w);
+            last_r = ar; last_c = acl; last_lo = acc; last_e = e;
+            if (acc + e > target) { found_r = ar; found_c = acl; } else { acc += e; }
+        }
+    }
+    if constexpr (E) {
+        if (found_r < 0) { uncertain = true; found_r = last_r; found_c = last_c; }
+        if (!(target - last_lo > HEUR_MARGIN * total && last_lo + last_e - target > HEUR_MARGIN * total))
+            uncertain = true;
+    }
+    out_r = found_r;
+    out_c = found_c;
+    return true;
+}
+
 template <bool HEUR>
 __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     constexpr int BLK = COOP_WAVES * WAVE;
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
     __shared__ __attribute__((aligned(16))) uint32_t lds[COOP_AREA * COOP_WAVES + 2 * BK_CELLS + HS_WORDS];
     __shared__ double coop_sh[COOP_WAVES][COOP_SHARED];
+    __shared__ int16_t coop_rank[COOP_WAVES][448];  // coop_walk: slot of each frontier key
+    const bool coop_walk_on = a.coop_walk != 0;
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint32_t* my = lds + wv * COOP_AREA;
     uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
@@ -3241,17 +3392,32 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
         int ar, ac;
         SECT(3);
+        int16_t* rank = coop_rank[wv];
         if (hroll) {
             if (gs < 0) {
                 ar = -1;
                 ac = 0;
+            } else if (coop_walk_on) {
+#pragma unroll
+                for (int r = 0; r < 20; ++r) rows_lds[r * WAVE].y = h_ok[r];
+                if (!coop_walk<true>(gs, 0u, rows_lds, T->s.key[p], T->s.mask[p], rank, lane, hs, edge_w, h_target,
+                                     h_R, h_total, ar, ac, h_unc))
+                    heur_walk_frontier(gs, h_ok, rows_lds, T->s.key[p], T->s.mask[p], hs, edge_w, h_target, h_R,
+                                       h_total, ar, ac, h_unc);
             } else {
                 heur_walk_frontier(gs, h_ok, rows_lds, T->s.key[p], T->s.mask[p], hs, edge_w, h_target, h_R, h_total,
                                    ar, ac, h_unc);
             }
             if (h_unc) m.status |= BK_MCTS_EUNCERT;
         } else {
-            locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+            bool walked = false;
+            if (coop_walk_on && T->s.mask[p] <= 2 * WAVE - 1) {
+                bool unc_unused = false;
+                locate_pass1(gs, rows_lds);
+                walked = coop_walk<false>(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], rank, lane, hs, 0, 0.0, 0.0,
+                                          0.0, ar, ac, unc_unused);
+            }
+            if (!walked) locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
         }
         if (ar < 0) {  // the table does not list the move: counts and tables disagree
             m.status |= BK_MCTS_EINTERNAL;
@@ -4168,7 +4334,8 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (int32_t*)sec[9].dev, (const double*)sec[10].dev, log_len, (bk_mcts_node*)sec[11].dev,
                (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
-               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread};
+               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1};
+    if (const char* env = getenv("BK_COOP_WALK")) a.coop_walk = atoi(env);  // tuning / test override
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (coop && heur)
         hipLaunchKernelGGL(k_mcts_coop_h, dim3(blocks), dim3(blk), 0, h->cur, a);
