@@ -3022,7 +3022,6 @@ __global__ __launch_bounds__(HBLOCK, 2) void k_mcts_h(MctsArgs a) { mcts_body<tr
 #define COOP_H_WAVES_PER_SIMD 1                  // k_mcts_coop_h waves per SIMD (2: <= 256 registers, spills)
 #endif
 #define COOP_AREA ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS)  // per-wave per-lane area (rows / staged table)
-#define COOP_SHARED (BK_NUM_ORIENTS + BK_PIECES)  // per-wave doubles: e per orientation, per piece
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 #pragma unroll
@@ -3053,6 +3052,15 @@ __device__ __forceinline__ void coop_orients(const uint2* rows, uint32_t avail, 
             if constexpr (E) es[h] = lane_orient_sum(g, ok, rows, hs, edge_w);
         }
     }
+}
+
+__device__ __forceinline__ double wave_incl_scan_f64(double v, int lane) {
+#pragma unroll
+    for (int o = 1; o < WAVE; o <<= 1) {
+        const double u = __shfl_up(v, o);
+        v += lane >= o ? u : 0.0;
+    }
+    return v;
 }
 
 struct CoopScan {
@@ -3091,55 +3099,42 @@ __device__ __forceinline__ int coop_find(const CoopScan& s, uint32_t k, uint32_t
     return g;
 }
 
-// heur_pick_orient from the wave-shared sums: piece, then orientation (list order: piece
-// asc, orientation asc) whose cumulative e crosses target; R = cumulative e before it.
-// Uncertain when no crossing is found (rounding at the total), as heur_pick_orient.
-__device__ __forceinline__ int coop_heur_pick(const double* es, const double* psum, const HeurShared* hs,
-                                              double target, double& R, bool& uncertain) {
-    int pstar = -1;
-    R = 0.0;
-#pragma unroll 1
-    for (int p = 0; p < BK_PIECES; ++p) {
-        const double sp = psum[p];
-        if (pstar < 0 && sp > 0.0) {
-            if (R + sp > target) pstar = p;
-            else R += sp;
-        }
+// heur_pick_orient for the wave's search from the lanes' e sums (es[h] of orientation
+// lane + 64 h): the orientation (list order: g ascending) whose cumulative e crosses
+// target, by a wave scan; R = cumulative e before it, total = the sum of all.  The sums
+// differ from the per-piece serial ones by rounding only (the walk certifies the draw
+// against HEUR_MARGIN).  Uncertain when no crossing is found (rounding at the total).
+__device__ __forceinline__ int coop_heur_pick(const double (&es)[2], int lane, const uint32_t* st, uint32_t& pos,
+                                              uint32_t pre0, uint32_t pre1, double& target, double& R,
+                                              double& total, bool& uncertain) {
+    const double i0 = wave_incl_scan_f64(es[0], lane);
+    const double i1 = wave_incl_scan_f64(es[1], lane) + __shfl(i0, WAVE - 1);
+    total = __shfl(i1, WAVE - 1);
+    // HeuristicAgent's draw (random_sample): the two words were loaded ahead (pre) when
+    // the state holds them without a twist
+    double u;
+    if (pos + 2u <= (uint32_t)FM_N) {
+        u = ((double)(mc_temper(pre0) >> 5) * 67108864.0 + (double)(mc_temper(pre1) >> 6)) *
+            (1.0 / 9007199254740992.0);
+        pos += 2u;
+    } else {
+        u = mc_random_sample(const_cast<uint32_t*>(st), pos);
     }
-    if (pstar < 0) {
+    target = u * total;
+    const uint64_t b0 = __ballot(es[0] > 0.0 && i0 > target);
+    const uint64_t b1 = __ballot(es[1] > 0.0 && i1 > target);
+    int L = -1, h = 0;
+    if (b0) { L = __ffsll((unsigned long long)b0) - 1; }
+    else if (b1) { L = __ffsll((unsigned long long)b1) - 1; h = 1; }
+    else {
         uncertain = true;
-        R = 0.0;
-        for (int p = 0; p < BK_PIECES; ++p)
-            if (psum[p] > 0.0) pstar = p;
-#pragma unroll 1
-        for (int p = 0; p < pstar; ++p) R += psum[p];
+        const uint64_t l1 = __ballot(es[1] > 0.0), l0 = __ballot(es[0] > 0.0);
+        if (l1) { L = 63 - __clzll((unsigned long long)l1); h = 1; }
+        else if (l0) { L = 63 - __clzll((unsigned long long)l0); }
     }
-    int gstar = -1;
-    double Rstar = R;
-    bool found = false;
-    const int g1 = hs->first[pstar + 1];
-#pragma unroll 1
-    for (int g = hs->first[pstar]; g < g1 && !found; ++g) {
-        const double sg = es[g];
-        if (sg > 0.0) {
-            gstar = g;
-            Rstar = R;
-            found = R + sg > target;
-            R += sg;
-        }
-    }
-    if (!found) uncertain = true;
-    R = Rstar;
-    return gstar;
-}
-
-__device__ __forceinline__ double wave_incl_scan_f64(double v, int lane) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const double u = __shfl_up(v, o);
-        v += lane >= o ? u : 0.0;
-    }
-    return v;
+    if (L < 0) { R = 0.0; return -1; }
+    R = __shfl(h ? i1 - es[1] : i0 - es[0], L);
+    return L + WAVE * h;
 }
 
 // Cooperative pass 2 of locate_move_frontier / heur_walk_frontier (one wave = one search;
@@ -3258,7 +3253,6 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     constexpr int BLK = COOP_WAVES * WAVE;
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
     __shared__ __attribute__((aligned(16))) uint32_t lds[COOP_AREA * COOP_WAVES + 2 * BK_CELLS + HS_WORDS];
-    __shared__ double coop_sh[COOP_WAVES][COOP_SHARED];
     __shared__ int16_t coop_rank[COOP_WAVES][448];  // coop_walk: slot of each frontier key
     const bool coop_walk_on = a.coop_walk != 0;
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
@@ -3267,8 +3261,6 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     int16_t* lk = reinterpret_cast<int16_t*>(my) + 2 * lane;
     uint64_t* htab = reinterpret_cast<uint64_t*>(lds + COOP_AREA * COOP_WAVES);
     HeurShared* hs = reinterpret_cast<HeurShared*>(lds + COOP_AREA * COOP_WAVES + 2 * BK_CELLS);
-    double* es_sh = coop_sh[wv];                      // e sum per orientation
-    double* ps_sh = coop_sh[wv] + BK_NUM_ORIENTS;     // e sum per piece
     for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab[i] = kCellHash[i];
     if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
     __syncthreads();
@@ -3326,6 +3318,12 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         // Board.move_count of the rollout board: placements on the way from the root
         const int edge_w = (int)(a.roots[m.game].move_count + m.depth + m.plies) < 30 ? 6 : 3;
+        uint32_t h_pre0 = 0u, h_pre1 = 0u;  // the heuristic draw's two MT words, loaded early
+        if (hroll && m.mt_pos + 2u <= (uint32_t)FM_N) {
+            const uint32_t* st = a.mt + (size_t)m.game * (FM_N + 1);
+            h_pre0 = st[m.mt_pos];
+            h_pre1 = st[m.mt_pos + 1u];
+        }
         SECT(1);
         uint32_t cnt[2];
         double es[2];
@@ -3368,23 +3366,8 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         uint32_t h_ok[20];
         bool h_unc = false;
         if (hroll) {
-            // per-orientation e to the wave-shared array, per-piece sums in orientation order
-            if (lane < BK_NUM_ORIENTS) es_sh[lane] = es[0];
-            if (lane + WAVE < BK_NUM_ORIENTS) es_sh[lane + WAVE] = es[1];
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            if (lane < BK_PIECES) {
-                double sp = 0.0;
-#pragma unroll 1
-                for (int g = hs->first[lane]; g < hs->first[lane + 1]; ++g) sp += es_sh[g];
-                ps_sh[lane] = sp;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-#pragma unroll 1
-            for (int q = 0; q < BK_PIECES; ++q) h_total += ps_sh[q];
-            h_target = mc_random_sample(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos) * h_total;
-            gs = coop_heur_pick(es_sh, ps_sh, hs, h_target, h_R, h_unc);
+            gs = coop_heur_pick(es, lane, a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, h_pre0, h_pre1, h_target,
+                                h_R, h_total, h_unc);
             if (gs >= 0) lane_ok_rows(gs, rows_lds, h_ok);
         } else {
             gs = coop_find(sc, k, kk);

@@ -394,7 +394,7 @@ class BlokusGPU:
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
                     hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
                     on_chunk=None, stop_after: int | None = None, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM,
-                    resume_from: int | None = None):
+                    resume_from: int | None = None, time_limit_us: int = 0):
         """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
@@ -405,8 +405,9 @@ class BlokusGPU:
         rewards float64 / hit_flags uint8 [n, iterations] (optional).  chunk > 0 splits
         the searches into launches of `chunk` iterations; on_chunk(done_iterations) is
         called after each; stop_after: run only the first stop_after iterations (they
-        can be resumed by no caller here: a warm-up).  Raises if any search reports a
-        nonzero status."""
+        can be resumed by no caller here: a warm-up).  time_limit_us: stop each search at
+        the first iteration boundary past it (no chunking).  Raises if any search reports
+        a nonzero status."""
         import torch
         n = roots.shape[0]
         use_tt = tt_keys is not None
@@ -429,6 +430,7 @@ class BlokusGPU:
         _check_device_tensor(log_table, "log_table", torch.float64, (log_table.shape[0],), self.device)
         self._stream_from_torch()
         d = lambda t: t.data_ptr() if t is not None else 0  # noqa: E731
+        assert not ((chunk or stop_after or resume_from) and time_limit_us), "timed searches run in one launch"
         stops = mcts_chunks(iterations, chunk)
         if stop_after is not None and 0 < stop_after < iterations:
             stops = [x for x in stops if 0 < x < stop_after] + [stop_after]
@@ -437,7 +439,8 @@ class BlokusGPU:
         for j, stop in enumerate(stops):
             resume = int(j > 0 or resume_from is not None)
             cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
-                              tt_keys.shape[1] if use_tt else 0, 0, stop, resume, int(rollout_policy), 0)
+                              tt_keys.shape[1] if use_tt else 0, int(time_limit_us), stop, resume,
+                              int(rollout_policy), 0)
             self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
                              d(zobrist_index), d(mt_state), d(tt_keys), d(tt_vals), d(tt_count), d(log_table),
                              log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)
@@ -543,6 +546,86 @@ class MctsTT:
         for g in range(n):
             _insert(keys[g], vals[g], *self.items(g))
         self.keys, self.vals = keys, vals
+
+
+class TTPool:
+    """Device-resident transposition tables of one capacity (the MctsTT layout in HBM:
+    keys int64 / vals float64 [rows, cap], NaN = empty, count int32 [rows]).  An agent
+    leases one row (TTRow) and keeps it across select_action calls, so a search never
+    moves its table between host and device (mcts/mcts_agent.py:304-341 keeps the TT
+    across moves; mcts/zobrist.py:155-220).  One pool per (device, cap): pools()."""
+
+    _pools: dict = {}
+
+    def __init__(self, device: int, cap: int, rows: int = 64):
+        import torch
+        assert cap >= 2 and cap & (cap - 1) == 0
+        self.device, self.cap = device, cap
+        dev = f"cuda:{device}"
+        self.keys = torch.zeros((rows, cap), dtype=torch.int64, device=dev)
+        self.vals = torch.full((rows, cap), float("nan"), dtype=torch.float64, device=dev)
+        self.count = torch.zeros(rows, dtype=torch.int32, device=dev)
+        self.free = list(range(rows - 1, -1, -1))
+
+    @classmethod
+    def get(cls, device: int, cap: int) -> "TTPool":
+        key = (device, cap)
+        if key not in cls._pools:
+            cls._pools[key] = TTPool(device, cap)
+        return cls._pools[key]
+
+    def lease(self) -> "TTRow":
+        import torch
+        if not self.free:  # double the rows (new rows empty)
+            n = self.keys.shape[0]
+            self.keys = torch.cat([self.keys, torch.zeros_like(self.keys)])
+            self.vals = torch.cat([self.vals, torch.full_like(self.vals, float("nan"))])
+            self.count = torch.cat([self.count, torch.zeros_like(self.count)])
+            self.free = list(range(2 * n - 1, n - 1, -1))
+        return TTRow(self, self.free.pop())
+
+    def release(self, row: int):
+        self.keys[row] = 0
+        self.vals[row] = float("nan")
+        self.count[row] = 0
+        self.free.append(row)
+
+
+class TTRow:
+    """One agent's table: a row of a TTPool.  count mirrors the device count after
+    each search; items(0) / cap match MctsTT's single-table accessors."""
+
+    def __init__(self, pool: TTPool, row: int):
+        import weakref
+        self.pool, self.row, self.count = pool, row, np.zeros(1, np.int32)
+        self._fin = weakref.finalize(self, pool.release, row)
+        self._fin.atexit = False  # no device work while the interpreter shuts down
+
+    @property
+    def cap(self) -> int:
+        return self.pool.cap
+
+    def items(self, g: int = 0):
+        assert g == 0
+        keys = self.pool.keys[self.row].cpu().numpy().view(np.uint64)
+        vals = self.pool.vals[self.row].cpu().numpy()
+        live = ~np.isnan(vals)
+        return keys[live], vals[live]
+
+    def load(self, keys, vals):
+        """Replace the row's contents with the given (key, reward) entries."""
+        import torch
+        tk = np.zeros(self.cap, np.uint64)
+        tv = np.full(self.cap, np.nan)
+        _insert(tk, tv, np.asarray(keys, np.uint64), np.asarray(vals, np.float64))
+        dev = self.pool.keys.device
+        self.pool.keys[self.row] = torch.from_numpy(tk.view(np.int64)).to(dev)
+        self.pool.vals[self.row] = torch.from_numpy(tv).to(dev)
+        self.pool.count[self.row] = len(keys)
+        self.count[0] = len(keys)
+
+    def release(self):
+        self._fin()
 
 
 def _insert(tkeys: np.ndarray, tvals: np.ndarray, k: np.ndarray, v: np.ndarray) -> None:

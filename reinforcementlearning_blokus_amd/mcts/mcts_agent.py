@@ -41,6 +41,62 @@ from ..engine.pieces import PieceGenerator
 from .zobrist import TranspositionTable, ZobristHash
 
 
+def _search_on_device(gpu, ags, rts, sts, pl, rh, zob, zidx, mt, iters, max_roll, c, use_tt, tl_us, policy):
+    """One bk_mcts launch for search_packed with every buffer in HBM (BK_MEM_DEVICE).
+    The agents' TTs stay on the device between calls (TTPool rows, gathered into the
+    launch's [n, cap] block and scattered back); only the roots, streams and per-search
+    outputs cross PCIe.  mt (uint32[n, 625]) is advanced in place.  Returns dict(out,
+    rewards, hit_flags) as host arrays."""
+    import torch
+
+    from .. import _native as N
+    from ..gpu import TTPool, mcts_log_table, mcts_node_cap
+    n = len(ags)
+    dev = f"cuda:{gpu.device}"
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    lts = gpu.__dict__.setdefault("_log_tables", {})
+    if iters not in lts:
+        lts[iters] = up(mcts_log_table(iters))
+    cap_nodes = mcts_node_cap(iters)
+    d_mt = up(mt.view(np.int32))
+    d_out = torch.zeros((n, N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    d_rew = torch.empty((n, iters), dtype=torch.float64, device=dev)
+    d_flags = torch.empty((n, iters), dtype=torch.uint8, device=dev)
+    tk = tv = tc = rows = pool = None
+    if use_tt:
+        cap = max([a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12])
+        need = max([int(a._gpu_tt.count[0]) for a in ags if a._gpu_tt is not None] or [0]) + iters + 2
+        while 2 * need > cap:
+            cap *= 2
+        pool = TTPool.get(gpu.device, cap)
+        for a in ags:
+            row = a._gpu_tt
+            if row is None:
+                a._gpu_tt = pool.lease()
+            elif row.pool is not pool:  # grown: re-insert into a row of the larger pool
+                nr = pool.lease()
+                nr.load(*row.items(0))
+                row.release()
+                a._gpu_tt = nr
+        rows = torch.tensor([a._gpu_tt.row for a in ags], dtype=torch.int64, device=dev)
+        tk, tv, tc = (pool.keys.index_select(0, rows), pool.vals.index_select(0, rows),
+                      pool.count.index_select(0, rows))
+    gpu.mcts_device(up(rts.view(np.uint8).reshape(n, 256)), up(sts.view(np.uint8).reshape(n, -1)), up(pl),
+                    up(rh.view(np.int64)), up(zob.view(np.int64)), up(zidx), d_mt, lts[iters],
+                    torch.empty((n, cap_nodes * N.MCTS_NODE_DTYPE.itemsize), dtype=torch.uint8, device=dev), d_out,
+                    iterations=iters, tt_keys=tk, tt_vals=tv, tt_count=tc, rewards=d_rew, hit_flags=d_flags,
+                    max_rollout_moves=max_roll, exploration=c, rollout_policy=policy, time_limit_us=tl_us)
+    if use_tt:
+        pool.keys.index_copy_(0, rows, tk)
+        pool.vals.index_copy_(0, rows, tv)
+        pool.count.index_copy_(0, rows, tc)
+        for a, cnt in zip(ags, tc.cpu().numpy()):
+            a._gpu_tt.count[0] = cnt
+    mt[:] = d_mt.cpu().numpy().view(np.uint32)
+    return {"out": d_out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(n), "rewards": d_rew.cpu().numpy(),
+            "hit_flags": d_flags.cpu().numpy()}
+
+
 def _search_policy(agent) -> Optional[int]:
     """bk_mcts rollout policy replaying this rollout agent on the GPU, or None:
     RandomAgent, or HeuristicAgent with the reference's default weights (the kernel's
@@ -230,7 +286,7 @@ class MCTSAgent:
         FSET_DTYPE frontier tables, players 0..3), each with >= 2 legal moves; one
         bk_mcts launch per parameter group.  Returns move ints (g * 400 + cell)."""
         from .. import _native as N
-        from ..gpu import BlokusGPU, MctsTT
+        from ..gpu import BlokusGPU
         from .zobrist import flat_keys, hash_states
         assert len({id(a) for a in agents}) == len(agents), "one search per agent per launch"
         out: List[Optional[int]] = [None] * len(agents)
@@ -273,26 +329,9 @@ class MCTSAgent:
             for j, st in enumerate(rng_states):
                 mt[j, :624] = st[1]
                 mt[j, 624] = st[2]
-            tt = None
-            if use_tt:
-                # the batch's tables: the agents' own open-addressing rows (same capacity:
-                # copied as they are; smaller: re-inserted), grown for this search's inserts
-                caps = [a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12]
-                need = max([int(a._gpu_tt.count[0]) for a in ags if a._gpu_tt is not None] or [0]) + iters + 2
-                cap = max(caps)
-                while 2 * need > cap:
-                    cap *= 2
-                tt = MctsTT(len(idx), cap=cap)
-                for j, a in enumerate(ags):
-                    if a._gpu_tt is not None and a._gpu_tt.count[0]:
-                        if a._gpu_tt.cap == cap:
-                            tt.keys[j], tt.vals[j], tt.count[j] = a._gpu_tt.keys[0], a._gpu_tt.vals[0], a._gpu_tt.count[0]
-                        else:
-                            tt.load(j, *a._gpu_tt.items(0))
             t0 = time.time()
-            r = gpu.mcts(rts, sts, pl, rh, iterations=iters, zobrist=zob, zobrist_index=np.array(zidx, np.int32),
-                         mt_state=mt, tt=tt, max_rollout_moves=max_roll, exploration=c, time_limit_us=tl_us,
-                         rollout_policy=policy)
+            r = _search_on_device(gpu, ags, rts, sts, pl, rh, zob, np.array(zidx, np.int32), mt, iters, max_roll, c,
+                                  use_tt, tl_us, policy)
             dt = time.time() - t0
             SEARCH_TOTALS["launches"] += 1
             SEARCH_TOTALS["kernel_ms"] += gpu.last_kernel_ms()
@@ -302,9 +341,10 @@ class MCTSAgent:
                 o = r["out"][j]
                 st = rng_states[j]
                 a.rollout_agent.rng.set_state((st[0], mt[j, :624].copy(), int(mt[j, 624]), st[3], st[4]))
-                hits = r["hit_flags"][j, :int(o["iterations_run"])]
-                rew = r["rewards"][j, :int(o["iterations_run"])]
-                a.stats["iterations_run"] = int(o["iterations_run"])
+                n_it = int(o["iterations_run"])
+                hits = r["hit_flags"][j, :n_it]
+                rew = r["rewards"][j, :n_it]
+                a.stats["iterations_run"] = n_it
                 # HeuristicAgent rollouts: a draw within 2^-40 of a probability boundary
                 # (BK_MCTS_EUNCERT; the kernel flags the search, it does not count draws)
                 unc = bool(int(o["status"]) & N.MCTS_EUNCERT)
@@ -312,22 +352,21 @@ class MCTSAgent:
                 a.stats["uncertified_searches"] = a.stats.get("uncertified_searches", 0) + int(unc)
                 if tl_us:
                     a.stats["iteration_bound"] = iters
-                    a.stats["iteration_bound_reached"] = int(o["iterations_run"]) >= iters
+                    a.stats["iteration_bound_reached"] = n_it >= iters
                     if a.stats["iteration_bound_reached"]:
                         warnings.warn(f"MCTSAgent: a {a.time_limit} s search stopped at its {iters}-iteration "
                                       "bound before the time ran out", RuntimeWarning, stacklevel=2)
                 a.stats["time_elapsed"] = dt
                 a.stats["transposition_hits"] += int(o["tt_hits"])
-                a.stats["rollout_rewards"].extend(float(x) for x in rew[hits == 0])
+                a.stats["rollout_rewards"].extend(rew[hits == 0].tolist())
                 if use_tt:
-                    a._gpu_tt = MctsTT(1, cap=tt.cap)
-                    a._gpu_tt.keys[0], a._gpu_tt.vals[0], a._gpu_tt.count[0] = tt.keys[j], tt.vals[j], tt.count[j]
                     t = a.transposition_table
                     t.access_count += int(o["tt_hits"]) + int(o["rollouts"])
                     t.hit_count += int(o["tt_hits"])
                     t.gpu_size = int(a._gpu_tt.count[0])
                     if t.gpu_size > 500000:  # mcts_agent.py:338-339
                         t.clear()
+                        a._gpu_tt.release()
                         a._gpu_tt = None
                 out[i] = int(o["best_move"]) if o["best_move"] >= 0 else None
         return out
@@ -416,6 +455,8 @@ class MCTSAgent:
         self.stats = self._fresh_stats()
         if self.transposition_table:
             self.transposition_table.clear()
+        if self._gpu_tt is not None:
+            self._gpu_tt.release()
         self._gpu_tt = None
 
     def set_seed(self, seed: int):
