@@ -712,6 +712,9 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
 // 7 x 7 bits, rows ar - 1 .. ar + 5 and columns ac - 1 .. ac + 5 (bit 7 i + j).
 // rows[R * WAVE].x = the mover's blocked rows BEFORE the move; slab = own planes before
 // or after the move (the piece's cells m are masked out).
+// FROM_SLAB: the blocked rows are derived from the slab (occupancy and own rows before
+// the move) instead of read from the LDS rows (MCTS replay, where no movegen ran).
+template <bool FROM_SLAB = false>
 __device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& slab, int p, bool first, int gs,
                                                  int ar, int ac, const uint32_t (&m)[5]) {
     uint32_t o[9];  // own rows ar - 2 .. ar + 6 before the move
@@ -733,7 +736,8 @@ __device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& 
         const uint32_t orth = own | (own << 1) | (own >> 1) | up | dn;
         const uint32_t vd = up | dn;
         const uint32_t diag = ((vd << 1) | (vd >> 1)) & ROWMASK;
-        const uint32_t b = inb ? rows[(R < 0 ? 0 : R > 19 ? 19 : R) * WAVE].x : ~0u;
+        const int Rc = R < 0 ? 0 : R > 19 ? 19 : R;
+        const uint32_t b = !inb ? ~0u : FROM_SLAB ? (slab.at(4, Rc) | orth | OFFBOARD) : rows[Rc * WAVE].x;
         const uint32_t pr = (i >= 1 && i <= 5) ? m[i - 1] : 0u;
         const uint32_t pu = (i >= 2) ? m[i - 2] : 0u, pd = (i <= 4) ? m[i] : 0u;
         const uint32_t addable = ~(b | pr | (pr << 1) | (pr >> 1) | pu | pd) & ROWMASK;
@@ -1230,7 +1234,102 @@ struct FsLane {
 // WAVE): one ds_write_b32 / ds_read_b32 per slot pair, and a probe of ANY slot by each
 // lane hits bank `lane` (conflict-free).  A larger table (or a move that grows one past
 // the stage) is updated in place.  false: table overflow.
-template <int STAGE>
+// Occupancy of a table of <= 256 slots in registers: set_insert_clean's probe sequence
+// on a fresh table needs only "is slot i unused", so a clean re-insert never reads the
+// destination back.
+struct SlotBits {
+    uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    __device__ __forceinline__ bool test(uint32_t i) const {
+        const uint32_t q = i >> 6;
+        const uint64_t w = q == 0u ? w0 : q == 1u ? w1 : q == 2u ? w2 : w3;
+        return ((w >> (i & 63u)) & 1ull) != 0ull;
+    }
+    __device__ __forceinline__ void set(uint32_t i) {
+        const uint64_t b = 1ull << (i & 63u);
+        const uint32_t q = i >> 6;
+        w0 |= q == 0u ? b : 0ull;
+        w1 |= q == 1u ? b : 0ull;
+        w2 |= q == 2u ? b : 0ull;
+        w3 |= q == 3u ? b : 0ull;
+    }
+};
+
+// fs_insert_clean's slot for key hash h in a fresh table of mask + 1 slots whose used
+// slots are `o` (marks the slot used)
+__device__ __forceinline__ uint32_t fs_clean_slot(uint64_t h, uint32_t mask, SlotBits& o) {
+    uint64_t perturb = h;
+    uint32_t i = (uint32_t)(h & mask);
+#pragma unroll 1
+    for (;;) {
+        if (!o.test(i)) break;
+        bool hit = false;
+        if (i + FS_PROBES <= mask) {
+#pragma unroll 1
+            for (int j = 0; j < FS_PROBES; ++j) {
+                ++i;
+                if (!o.test(i)) { hit = true; break; }
+            }
+        }
+        if (hit) break;
+        perturb >>= FS_SHIFT;
+        i = (uint32_t)(((uint64_t)i * 5u + 1u + perturb) & mask);
+    }
+    o.set(i);
+    return i;
+}
+
+// fs_copy_dev's size rule: the copy of a table with `used` active keys has newsize
+// slots; the copy is slot-for-slot the source when the size is unchanged and the source
+// has no dummies (set_merge's same-size path)
+__device__ __forceinline__ uint32_t fs_copy_size(uint32_t used) {
+    uint32_t newsize = 8;
+    if (used * 5 >= 7u * 3u)
+        while (newsize <= used * 2) newsize <<= 1;
+    return newsize;
+}
+
+// Board.copy() of table q of fl in place (the copy replaces the table): the source keys
+// go to fl->tmp, the destination is cleared and the keys re-inserted in slot order with
+// their slots chosen from a register bitmap.  Equal to fs_copy_dev into another record.
+// false: the copy would not fit the storage (table left empty, as fs_copy_dev).
+__device__ __forceinline__ bool fs_recopy_global(FsLane* fl, int q, const uint64_t* htab) {
+    bk_fset* s = &fl->s;
+    const uint32_t smask = s->mask[q], sfill = s->fill[q], sused = s->used[q];
+    const uint32_t newsize = fs_copy_size(sused);
+    if (newsize - 1 == smask && sfill == sused) return true;  // a copy of a copy
+    if (newsize > BK_FSET_SLOTS) {
+        fs_clear(fs_ref(s, q, htab));
+        return false;
+    }
+    bk_u4_alias* k4 = reinterpret_cast<bk_u4_alias*>(s->key[q]);
+    bk_u4_alias* t4 = reinterpret_cast<bk_u4_alias*>(fl->tmp);
+#pragma unroll 1
+    for (uint32_t i = 0; i <= smask / 8; ++i) t4[i] = k4[i];
+    const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+#pragma unroll 1
+    for (uint32_t i = 0; i < newsize / 8; ++i) k4[i] = unused;
+    s->mask[q] = (uint16_t)(newsize - 1);
+    s->fill[q] = (uint16_t)sused;
+    s->used[q] = (uint16_t)sused;
+    SlotBits o;
+#pragma unroll 1
+    for (uint32_t i = 0; i <= smask / 8; ++i) {
+        const uint4 v = t4[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int16_t k = (int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            if (k >= 0) s->key[q][fs_clean_slot(htab[k], newsize - 1, o)] = k;
+        }
+    }
+    return true;
+}
+
+// RECOPY: the table after the ops is replaced by its Board.copy() (MCTSNode boards are
+// copies of copies, mcts_agent.py:113-145): from the LDS stage, the keys are re-inserted
+// straight into the global table (slots from a register bitmap), so the copy costs no
+// second record and no reads of global memory.
+template <int STAGE, bool RECOPY = false>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
                                                const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
@@ -1252,17 +1351,36 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab};
         if (fs_run_ops(t, fl->tmp, cells, real)) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
+            const uint32_t newsize = fs_copy_size(u);
+            if (!RECOPY || (newsize - 1 == m && f == u)) {  // (a copy of a clean table is the table)
 #pragma unroll
-            for (int i = 0; i < STAGE / 8; ++i) {
-                if ((uint32_t)(8 * i) <= m)
-                    dst4[i] = make_uint4(lw[(4 * i + 0) * WAVE], lw[(4 * i + 1) * WAVE], lw[(4 * i + 2) * WAVE],
-                                         lw[(4 * i + 3) * WAVE]);
+                for (int i = 0; i < STAGE / 8; ++i) {
+                    if ((uint32_t)(8 * i) <= m)
+                        dst4[i] = make_uint4(lw[(4 * i + 0) * WAVE], lw[(4 * i + 1) * WAVE],
+                                             lw[(4 * i + 2) * WAVE], lw[(4 * i + 3) * WAVE]);
+                }
+                gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+                return true;
             }
-            gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+            // the copy: newsize <= 2 * STAGE <= BK_FSET_SLOTS (u < STAGE * 3 / 5)
+            const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+#pragma unroll 1
+            for (uint32_t i = 0; i < newsize / 8; ++i) dst4[i] = unused;
+            gfs->mask[p] = (uint16_t)(newsize - 1); gfs->fill[p] = u; gfs->used[p] = u;
+            SlotBits o;
+            int16_t* dk = gfs->key[p];
+#pragma unroll 1
+            for (uint32_t j = 0; j <= m / 2; ++j) {
+                const uint32_t w = lw[j * WAVE];
+                const int16_t k0 = (int16_t)(w & 0xFFFFu), k1 = (int16_t)(w >> 16);
+                if (k0 >= 0) dk[fs_clean_slot(htab[k0], newsize - 1, o)] = k0;
+                if (k1 >= 0) dk[fs_clean_slot(htab[k1], newsize - 1, o)] = k1;
+            }
             return true;
         }
     }
-    return fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real);
+    if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real)) return false;
+    return RECOPY ? fs_recopy_global(fl, p, htab) : true;
 }
 
 // ------------------------------------------------------------------------------------
@@ -2371,8 +2489,7 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts_select(const uint32_t* visits
 #define MC_TREE_BATCH WAVE
 
 struct McLane {          // per-lane scratch record in HBM
-    FsLane A;            // node.board tables of the node being worked on
-    FsLane B;            // copy target; the rollout's sim board
+    FsLane A;            // node.board tables of the node being worked on; the rollout's sim board
     bk_fset root;        // root.board (= board.copy(), made once per search)
     int32_t path[MC_PATH];
 };
@@ -2469,33 +2586,6 @@ __device__ __forceinline__ bool mc_copy_tables(bk_fset* d, const bk_fset* s, con
     return ok;
 }
 
-// Board.place_piece(validate=False) of orientation gs at (ar, ac) for player p: rows,
-// used / cells / first, and the player's frontier table in T (engine/board.py:515-555)
-__device__ __forceinline__ bool mc_place(Mc& m, const Slab& slab, int p, int gs, int ar, int ac, FsLane* T, const uint64_t* htab) {
-    const uint32_t info = kInfo[gs];
-    const int n = (int)((info >> 8) & 0xFFu);
-    int32_t cells[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-        const uint32_t cell = kCells[gs][q < n ? q : 0];
-        const int r = ar + (int)(cell >> 8), c = ac + (int)(cell & 0xFFu);
-        cells[q] = r * 20 + c;
-        if (q < n) {
-            slab.at(p, r) |= 1u << c;
-            slab.at(4, r) |= 1u << c;
-        }
-    }
-    const uint32_t* occ_rows = slab.base + 4 * 20;
-    const uint32_t* own_rows = slab.base + p * 20;
-    auto occ = [&](int r, int c) { return ((occ_rows[r] >> c) & 1u) != 0u; };
-    auto own = [&](int r, int c) { return ((own_rows[r] >> c) & 1u) != 0u; };
-    const bool ok = fs_place(fs_ref(&T->s, p, htab), T->tmp, cells, n, occ, own);
-    m.cells.set(p, m.cells.get(p) + (uint32_t)n);
-    m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
-    m.first &= ~(1u << p);
-    return ok;
-}
-
 // The placed piece's row masks (pm[d] = cells in row ar + d) and cell indices.
 __device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&pm)[5], int32_t (&cells)[5]) {
     const int n = (int)((kInfo[gs] >> 8) & 0xFFu);
@@ -2516,6 +2606,9 @@ __device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&p
 // cells from piece_cells, real from frontier_ops -- computed by EVERY lane of the wave
 // before any lane stages a table: the staged tables of some lanes overlay the LDS rows
 // of others.
+// RECOPY: the table then becomes its Board.copy() in place (expansion and replay edges:
+// node boards are copies).
+template <bool RECOPY>
 __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
                                                 const uint64_t* htab, const uint32_t (&pm)[5],
                                                 const int32_t (&cells)[5], uint64_t real, int16_t* lk) {
@@ -2528,7 +2621,7 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
             slab.at(4, ar + d) |= pm[d];
         }
     }
-    const bool ok = place_frontier<BK_FS_STAGE_MCTS>(T, p, lk, htab, cells, real);
+    const bool ok = place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
     m.first &= ~(1u << p);
@@ -2716,6 +2809,46 @@ __device__ __forceinline__ void mc_sim_terminal(const MctsArgs& a, Mc& m, McLane
     mc_complete(a, m, L, reward, hit);
 }
 
+// best_child (mcts_agent.py:68-111): index of the first child with the largest UCB1
+// total/visits + c * sqrt(log(parent visits) / visits) (unvisited: inf) among the n
+// children at cb.  The (total, visits) pairs are loaded MC_UCB_BATCH children at a time
+// before any is used, so a scan waits on ~n / MC_UCB_BATCH memory round trips instead of
+// two dependent loads per child (a fully expanded root has hundreds of children, and a
+// lane's child block is not cache-resident).  Same operations, same order: the argmax is
+// the reference's.
+#define MC_UCB_BATCH 16
+__device__ __forceinline__ int mc_ucb_best(const bk_mcts_node* cb, int n, double lg, double c_explore) {
+    int best = 0;
+    double bv = 0.0;
+#pragma unroll 1
+    for (int k0 = 0; k0 < n; k0 += MC_UCB_BATCH) {
+        double tot[MC_UCB_BATCH];
+        uint32_t vis[MC_UCB_BATCH];
+#pragma unroll
+        for (int j = 0; j < MC_UCB_BATCH; ++j) {
+            const int k = k0 + j < n ? k0 + j : n - 1;  // in bounds; unused past n
+            tot[j] = cb[k].total;
+            vis[j] = cb[k].visits;
+        }
+#pragma unroll
+        for (int j = 0; j < MC_UCB_BATCH; ++j) {
+            if (k0 + j < n) {
+                double v;
+                if (vis[j] == 0u) {
+                    v = __builtin_inf();
+                } else {
+                    const double vd = (double)vis[j];
+                    const double exploit = tot[j] / vd;
+                    const double explore = c_explore * __builtin_sqrt(lg / vd);
+                    v = exploit + explore;
+                }
+                if (k0 + j == 0 || v > bv) { bv = v; best = k0 + j; }
+            }
+        }
+    }
+    return best;
+}
+
 // selection (mcts_agent.py:384-406, UCB1 :68-111) from the root; leaves m.node at the
 // node to expand or simulate, m.depth / path / m.hash for it.  Returns true when that
 // node is evaluated terminal (no untried move, no child).
@@ -2731,21 +2864,7 @@ __device__ __forceinline__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, c
         if ((int32_t)nd.visits >= a.log_len) { m.status |= BK_MCTS_ELOG; break; }
         if (depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; break; }
         const double lg = a.log_table[nd.visits];
-        int best = nd.child0;
-        double bv = 0.0;
-        for (int k = 0; k < (int)nd.n_exp; ++k) {
-            const bk_mcts_node c = pool[nd.child0 + k];
-            double v;
-            if (c.visits == 0u) {
-                v = __builtin_inf();
-            } else {
-                const double vis = (double)c.visits;
-                const double exploit = c.total / vis;
-                const double explore = a.cfg.exploration * __builtin_sqrt(lg / vis);
-                v = exploit + explore;
-            }
-            if (k == 0 || v > bv) { bv = v; best = nd.child0 + k; }
-        }
+        const int best = nd.child0 + mc_ucb_best(pool + nd.child0, (int)nd.n_exp, lg, a.cfg.exploration);
         int gs, ar, ac;
         mc_move_split(pool[best].move, gs, ar, ac);
         h = mc_hash_step(Z, h, (m.root_player + depth) & 3, (m.root_cp + depth) & 3, gs, ar, ac);
@@ -2761,22 +2880,26 @@ __device__ __forceinline__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, c
 // node.board of path[depth] into the lane (slab rows + table A): root, then per edge
 // new_board = board.copy(); place; MCTSNode(new_board) copies again (mcts_agent.py:113-145).
 // Every node board is a copy, and a copy of a copy is slot-for-slot the same table
-// (set_merge's same-size path), so the first copy is skipped: place on the node table
-// itself and copy into the other record, alternating A and B.
-__device__ __forceinline__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L, const uint64_t* htab) {
+// (set_merge's same-size path), so the first copy is skipped and the second only
+// changes the mover's table: place on A (the ops that change the set, frontier_ops from
+// the slab, on the LDS-staged table) and replace that table by its copy in place.  lk:
+// this lane's LDS column (free in the tree phase: every lane of the wave is at the same
+// point of this loop, and the rows of a step are rebuilt after it).
+__device__ __forceinline__ void mc_replay(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L, const uint64_t* htab,
+                                          int16_t* lk) {
     mc_load_root(a, m, slab, L);
     const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
-    FsLane* X = &L->A;
-    FsLane* Y = &L->B;
     bool ok = true;
     for (int d = 1; d <= m.depth; ++d) {
         int gs, ar, ac;
         mc_move_split(pool[L->path[d]].move, gs, ar, ac);
-        ok &= mc_place(m, slab, (m.root_player + d - 1) & 3, gs, ar, ac, X, htab);
-        ok &= mc_copy_tables(&Y->s, &X->s, htab);
-        FsLane* t = X; X = Y; Y = t;
+        const int p = (m.root_player + d - 1) & 3;
+        uint32_t pm[5];
+        int32_t cells[5];
+        piece_cells(gs, ar, ac, pm, cells);
+        const uint64_t real = frontier_ops<true>(nullptr, slab, p, (m.first >> p) & 1u, gs, ar, ac, pm);
+        ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
     }
-    if (X != &L->A) ok &= mc_copy_tables(&L->A.s, &X->s, htab);  // same-shape copy
     if (!ok) m.status |= BK_MCTS_EFSET;
 }
 
@@ -2836,9 +2959,13 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             const bool chunk_end = a.cfg.iter_stop > 0 && m.it >= a.cfg.iter_stop;
             if (m.it >= a.cfg.iterations || chunk_end || timed_out || MC_FATAL(m.status)) { mc_finish_game(a, m); continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
-            if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
+            SECT(2);
+            const bool term = mc_select(a, m, L, Z);
+            SECT(0);
+            if (term) { mc_sim_terminal(a, m, L); continue; }
             if (MC_FATAL(m.status)) continue;
-            mc_replay(a, m, slab, L, htab);
+            mc_replay(a, m, slab, L, htab, lk);
+            SECT(1);
             m.mode = MC_EXPAND;
         }
         if (__ballot(!done) == 0ull) break;
@@ -2920,7 +3047,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         }
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
-        FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
+        FsLane* T = &L->A;  // the node board at expansion, the rollout's sim board after it
         int ar, ac;
         SECT(10);
         if (hroll) {
@@ -2964,10 +3091,12 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             pool[c] = ch;
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
         }
-        // expand: new_board = board.copy() is table A itself (A is a copy, see mc_replay)
-        ok &= mc_place_staged(m, slab, p, gs, ar, expand ? &L->A : &L->B, htab, pm, cells, real, lk);
+        // expand: new_board = board.copy() is table A itself (A is a copy, see mc_replay),
+        // and MCTSNode(new_board)'s copy replaces the mover's table in place; the rollout's
+        // sim = node.board.copy() is that copy again (A), and its plies place on A
+        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
+        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
         if (expand) {
-            ok &= mc_copy_tables(&L->B.s, &L->A.s, htab);  // MCTSNode(new_board): board.copy()
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             m.hash = mc_hash_step(Z, m.hash, p, (m.root_cp + m.depth) & 3, gs, ar, ac);
@@ -3291,7 +3420,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
             if (MC_FATAL(m.status)) continue;
-            mc_replay(a, m, slab, L, htab);
+            mc_replay(a, m, slab, L, htab, lk);
             m.mode = MC_EXPAND;
         }
         SECT(0);
@@ -3372,7 +3501,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         } else {
             gs = coop_find(sc, k, kk);
         }
-        FsLane* T = m.mode == MC_EXPAND ? &L->A : &L->B;
+        FsLane* T = &L->A;  // the node board at expansion, the rollout's sim board after it
         int ar, ac;
         SECT(3);
         int16_t* rank = coop_rank[wv];
@@ -3428,9 +3557,9 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             pool[c] = ch;
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
         }
-        ok &= mc_place_staged(m, slab, p, gs, ar, expand ? &L->A : &L->B, htab, pm, cells, real, lk);
+        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
+        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
         if (expand) {
-            ok &= mc_copy_tables(&L->B.s, &L->A.s, htab);  // MCTSNode(new_board): board.copy()
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             m.hash = mc_hash_step(Z, m.hash, p, (m.root_cp + m.depth) & 3, gs, ar, ac);

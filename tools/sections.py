@@ -107,6 +107,8 @@ def run_mcts():
         gpu.mcts_device(b.roots, b.sets, b.players, b.root_hash, b.zobrist, b.zidx, b.mt, b.log_table, b.nodes,
                         b.out, iterations=iters, tt_keys=b.tt_keys, tt_vals=b.tt_vals, tt_count=b.tt_count,
                         chunk=64, resume_from=iters - 64, rollout_policy=policy)
+        # k_mcts splits its tree phase: 0 select, 1 replay, 2 game start/finish/complete
+        NAMES.update({0: "mcts tree: select", 1: "mcts tree: replay", 2: "mcts tree: start/finish/terminal"})
         read("k_mcts" if policy == N.MCTS_ROLLOUT_RANDOM else "k_mcts_h",
              {"games": games, "iterations": f"{iters - 64}..{iters}", "kernel_ms": gpu.last_kernel_ms()})
 
