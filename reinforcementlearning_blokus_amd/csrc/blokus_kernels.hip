@@ -241,7 +241,8 @@ struct StencilClass {
             return BITOP3(c, b, b, LUT_ANDN);
         }
     }
-    template <typename F>
+    // LANE_W1: w1 differs per lane (the lane-pair split of count_class_pair)
+    template <bool LANE_W1 = false, typename F>
     __device__ __forceinline__ static void scan(const Planes& P, uint32_t w1, F&& f) {
         // Shift amounts go to VGPRs: a VALU op reading an SGPR is never dual-issued on
         // gfx950 (tools/valu_probe2.hip).  NOTE: the v_bcnt below keeps
@@ -251,7 +252,8 @@ struct StencilClass {
 #pragma unroll
         for (int k = 1; k < NT; ++k) {
             const uint32_t v = (w1 >> (3 * (k - 1))) & 7u;
-            asm("v_mov_b32 %0, %1" : "=v"(sh[k]) : "s"(v));
+            if constexpr (LANE_W1) sh[k] = v;
+            else asm("v_mov_b32 %0, %1" : "=v"(sh[k]) : "s"(v));
         }
         // row by row: without the barriers the scheduler interleaves all rows for ILP
         // and the live set no longer fits 3 waves per SIMD (other waves hide latency)
@@ -330,6 +332,36 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
     return total;
 }
 
+// count_class for a lane PAIR that shares one board-player (k_mcts_pair): the even lane
+// counts the class's entries i0, i0 + 2, ..., the odd lane i0 + 1, i0 + 3, ... (both
+// entries of a pair run in the same instructions, with per-lane shift amounts, piece and
+// orientation), so a class of n entries costs ceil(n / 2) scans instead of n.  Each
+// orientation's count lands in the column of the lane that counted it; the other lane's
+// field stays 0, so the two columns add up to the full count vector (pick_orient<true>).
+template <bool STORE, int H, int... T>
+__device__ __forceinline__ uint32_t count_class_pair(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl,
+                                                     bool odd) {
+    uint32_t total = 0;
+#pragma unroll 1
+    for (int ia = i0; ia < i1; ia += 2) {
+        const bool has_b = ia + 1 < i1;  // uniform
+        const int ib = has_b ? ia + 1 : ia;
+        const uint32_t a0 = kClass[ia][0], a1 = kClass[ia][1], b0 = kClass[ib][0], b1 = kClass[ib][1];
+        const uint32_t w0 = odd ? b0 : a0, w1 = odd ? b1 : a1;
+        const uint32_t piece = w0 & 0xFFu;
+        const int g = (int)(w0 >> 8);
+        const bool av = ((avail >> (piece - 1u)) & 1u) && (has_b || !odd);
+        if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
+            uint32_t c = 0;
+            StencilClass<H, T...>::template scan<true>(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); });
+            c = av ? c : 0u;
+            if constexpr (STORE) atomicAdd(cl + (g / 3) * WAVE, c << (10 * (g % 3)));
+            total += c;
+        }
+    }
+    return total;
+}
+
 // Tuning variant (BK_STENCIL_LITERAL): every stencil-table entry as its own
 // straight-line code with literal column shifts (code = t | shift << 8), piece and
 // orientation as constants -- no scalar table loads, no shift amounts moved from SGPRs.
@@ -386,7 +418,9 @@ __device__ __forceinline__ uint32_t count_entry(const Planes& P, uint32_t avail,
     return c;
 }
 
-template <bool STORE>
+// PAIR: lanes 2j and 2j + 1 hold the same board-player and split the entries
+// (count_class_pair); each returns its share of the total.
+template <bool STORE, bool PAIR = false>
 __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane) {
     uint32_t t = 0;
     uint32_t* cl = cnt + lane;  // this lane's dwords; the orientation part is uniform
@@ -407,9 +441,16 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     BK_ENTRY_LIST(BK_COUNT_ENTRY)
 #undef BK_COUNT_ENTRY
 #else
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl);
-    BK_CLASS_LIST(BK_COUNT_CLASS)
+    if constexpr (PAIR) {
+        const bool odd = (lane & 1) != 0;
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd);
+        BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
+    } else {
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl);
+        BK_CLASS_LIST(BK_COUNT_CLASS)
+#undef BK_COUNT_CLASS
+    }
 #endif
     return t;
 }
@@ -435,7 +476,9 @@ __device__ __forceinline__ void all_rows(const Planes& P, F&& f) {
 #undef BK_ROWS_CLASS
 }
 
-// orientation holding the k-th legal move (naive order: g ascending) and its rank in it
+// orientation holding the k-th legal move (naive order: g ascending) and its rank in it.
+// PAIR: the counts are split over this lane's column and the next one (movegen_counts<.., true>)
+template <bool PAIR = false>
 __device__ __forceinline__ int pick_orient(const uint32_t* cnt, int lane, uint32_t k, uint32_t& kk) {
     // dword level first (the three 10-bit fields summed), then the field inside the
     // dword that holds index k
@@ -446,7 +489,9 @@ __device__ __forceinline__ int pick_orient(const uint32_t* cnt, int lane, uint32
     for (int h0 = 0; h0 < CNT_DWORDS; h0 += 8) {  // 8 LDS reads in flight per batch
         uint32_t v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (h0 + j < CNT_DWORDS) ? cnt[(h0 + j) * WAVE + lane] : 0u;
+        for (int j = 0; j < 8; ++j)
+            v[j] = (h0 + j < CNT_DWORDS) ? cnt[(h0 + j) * WAVE + lane] + (PAIR ? cnt[(h0 + j) * WAVE + lane + 1] : 0u)
+                                         : 0u;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const uint32_t s = (v[j] & 0x3FFu) + ((v[j] >> 10) & 0x3FFu) + (v[j] >> 20);
@@ -2914,8 +2959,11 @@ __device__ __forceinline__ double mc_random_sample(uint32_t* st, uint32_t& pos) 
 
 // HEUR: rollouts play HeuristicAgent (MCTSAgent's default rollout_agent,
 // mcts/mcts_agent.py:275-281) instead of RandomAgent
-template <bool HEUR>
+// PAIR (k_mcts_pair, spread 2, random rollouts): the idle odd lane of each pair counts
+// half of the even lane's stencil entries (count_class_pair).
+template <bool HEUR, bool PAIR = false>
 __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
+    static_assert(!(HEUR && PAIR), "the heuristic pass is not split");
     constexpr int BLK = HEUR ? HBLOCK : BLOCK;
     constexpr int AREA = HEUR ? HEUR_WORDS : ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS);
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
@@ -2977,19 +3025,34 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         // ---- one movegen per busy lane (uniform work)
         const bool idle = done || m.mode == MC_SELECT;
         const int p = idle ? 0 : (m.mode == MC_EXPAND ? ((m.root_player + m.depth) & 3) : m.cur);
+        // the board-player this lane counts: its own, or (PAIR, odd lane) its even neighbour's
+        bool c_idle = idle;
+        int cp = p;
+        uint32_t c_first = (m.first >> p) & 1u, c_used = m.used.get(p);
+        uint32_t* c_base = slab.base;
+        if constexpr (PAIR) {
+            const int o = lane & ~1;
+            c_idle = __shfl((int)idle, o) != 0;
+            cp = __shfl(p, o);
+            c_first = (uint32_t)__shfl((int)c_first, o);
+            c_used = (uint32_t)__shfl((int)c_used, o);
+            c_base = a.slab + (size_t)(slot & ~1u) * SLAB_WORDS;
+        }
+        const Slab cslab{c_base};
         Planes P;
         {
             uint32_t own[20], occ[20];
 #pragma unroll
             for (int R = 0; R < 20; ++R) {
-                own[R] = idle ? 0u : slab.at(p, R);
-                occ[R] = idle ? 0u : slab.at(4, R);
+                own[R] = c_idle ? 0u : cslab.at(cp, R);
+                occ[R] = c_idle ? 0u : cslab.at(4, R);
             }
-            derive_rows(own, occ, (m.first >> p) & 1u, p, P);
+            derive_rows(own, occ, c_first, cp, P);
         }
         make_pairs(P);
-        const uint32_t avail = idle ? 0u : (~m.used.get(p) & 0x1FFFFFu);
-        const uint32_t total = movegen_counts<true>(P, avail, my, lane);
+        const uint32_t avail = c_idle ? 0u : (~c_used & 0x1FFFFFu);
+        uint32_t total = movegen_counts<true, PAIR>(P, avail, my, lane);
+        if constexpr (PAIR) total += (uint32_t)__shfl_xor((int)total, 1);
         SECT(9);
         if (idle) continue;
         bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
@@ -3021,7 +3084,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             k = HEUR ? 0u : mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
         }
         uint32_t kk;
-        int gs = pick_orient(my, lane, k, kk);
+        int gs = pick_orient<PAIR>(my, lane, k, kk);
         // HEUR: a rollout ply's move is HeuristicAgent.select_action's (heur_* above)
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         double h_target = 0.0, h_R = 0.0, h_total = 0.0;
@@ -3128,6 +3191,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
 }
 
 __global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
+__global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts_pair(MctsArgs a) { mcts_body<false, true>(a); }
 __global__ __launch_bounds__(HBLOCK, 2) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
 
 // ------------------------------------------------------------------------------------
@@ -4448,6 +4512,9 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1};
     if (const char* env = getenv("BK_COOP_WALK")) a.coop_walk = atoi(env);  // tuning / test override
+    // spread 2: the idle odd lane of each pair splits the even lane's stencil (k_mcts_pair)
+    bool pair = true;
+    if (const char* env = getenv("BK_MCTS_PAIR")) pair = atoi(env) != 0;  // tuning / test override
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (coop && heur)
         hipLaunchKernelGGL(k_mcts_coop_h, dim3(blocks), dim3(blk), 0, h->cur, a);
@@ -4455,6 +4522,8 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         hipLaunchKernelGGL(k_mcts_coop, dim3(blocks), dim3(blk), 0, h->cur, a);
     else if (heur)
         hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
+    else if (spread == 2 && pair)
+        hipLaunchKernelGGL(k_mcts_pair, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     else
         hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());

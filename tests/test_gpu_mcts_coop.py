@@ -22,11 +22,13 @@ def gpu():
     return BlokusGPU(0)
 
 
-def _run(gpu, roots, sets, iters, policy, max_roll, coop, monkeypatch, seed0=100, time_limit_us=0):
+def _run(gpu, roots, sets, iters, policy, max_roll, coop, monkeypatch, seed0=100, time_limit_us=0, env=None):
     from reinforcementlearning_blokus_amd.gpu import MctsTT
     from reinforcementlearning_blokus_amd.mcts.zobrist import ZobristHash, flat_keys, hash_states
     from reinforcementlearning_blokus_amd.workloads import numpy_mt_states
     monkeypatch.setenv("BK_MCTS_COOP", "1" if coop else "0")
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
     n = len(roots)
     zob = np.stack([flat_keys(ZobristHash(seed=t)) for t in range(3)])
     zi = (np.arange(n) % 3).astype(np.int32)
@@ -57,6 +59,27 @@ def test_coop_equals_per_lane(gpu, monkeypatch, policy, n, iters, max_roll):
     assert np.array_equal(mta, mtb)
     assert np.array_equal(tta.keys, ttb.keys) and np.array_equal(tta.count, ttb.count)
     assert a["nodes"].tobytes() == b["nodes"].tobytes()
+
+
+@pytest.mark.parametrize("n,iters,max_roll", [(70, 160, 50), (333, 96, 50), (9, 400, 20)])
+def test_pair_split_equals_single_lane(gpu, monkeypatch, n, iters, max_roll):
+    """k_mcts_pair (spread 2: the odd lane of each pair counts half of the even lane's
+    stencil entries, count_class_pair) against k_mcts with one lane per search (spread 1)
+    and against k_mcts at spread 2 without the split: every output bit-identical."""
+    from reinforcementlearning_blokus_amd.workloads import frontier_roots
+    roots, sets = frontier_roots(gpu, n, 10 + n % 13, seed=4242 + n)
+    pol = N.MCTS_ROLLOUT_RANDOM
+    a, mta, tta = _run(gpu, roots, sets, iters, pol, max_roll, False, monkeypatch,
+                       env={"BK_MCTS_SPREAD": "2", "BK_MCTS_PAIR": "1"})
+    for env in ({"BK_MCTS_SPREAD": "1", "BK_MCTS_PAIR": "0"}, {"BK_MCTS_SPREAD": "2", "BK_MCTS_PAIR": "0"}):
+        b, mtb, ttb = _run(gpu, roots, sets, iters, pol, max_roll, False, monkeypatch, env=env)
+        assert (a["out"]["status"] == 0).all()
+        assert (a["out"]["iterations_run"] == iters).all()
+        assert a["out"].tobytes() == b["out"].tobytes()
+        assert np.array_equal(a["rewards"], b["rewards"]) and np.array_equal(a["hit_flags"], b["hit_flags"])
+        assert np.array_equal(mta, mtb)
+        assert np.array_equal(tta.keys, ttb.keys) and np.array_equal(tta.count, ttb.count)
+        assert a["nodes"].tobytes() == b["nodes"].tobytes()
 
 
 def test_coop_time_limit_stops(gpu, monkeypatch):
