@@ -422,7 +422,7 @@ def run_config5(args, world, rank, local, dist):
     sims_rank0 = int(res["iterations_run"].sum())
     bytes_rank0 = 2.0 * STATE_B * plies_local + (RESULT_B + 16 + 24 + 48) * sims_rank0
     achieved = bytes_rank0 / (kernel_ms * 1e-3) / 1e9
-    kname = "k_mcts_h" if heur else "k_mcts"
+    kname = gpu.last_kernel() or ("k_mcts_h" if heur else "k_mcts")  # bk_mcts picks it by batch size
     traffic, valu_insts = traffic_for(kname)
     line = {
         "metric": METRIC if not heur else "MCTSAgent (default HeuristicAgent rollouts) simulations/sec",

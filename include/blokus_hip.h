@@ -415,6 +415,10 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
 /* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
    stream, measured with HIP events around that launch. */
 int bk_last_kernel_ms(bk_handle h, float* ms);
+/* Name of the kernel the last timed call on h launched ("" before any), e.g. "k_mcts_pair"
+   or "k_mcts_coop_h" for bk_mcts, which picks its kernel from the batch size: lets a
+   profiler's per-kernel counters be matched to the call.  Owned by the library.          */
+const char* bk_last_kernel(bk_handle h);
 
 /* Diagnostics (no reference counterpart): per-section shader-clock cycles summed over
    waves since the last reset, from a library built with -DBK_SECTION_PROF

@@ -29,7 +29,7 @@ STREAM_OWN = (1 << 64) - 1  # BK_STREAM_OWN
 EXPORTS = (
     "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream",
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_movegen_mask", "bk_has_moves",
-    "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms",
+    "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms", "bk_last_kernel",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
     "bk_mt_cursor_init",
@@ -162,6 +162,7 @@ def load():
             "bk_debug_fastmcts_select": (C.c_int, [vp, C.c_int32, vp, vp, C.c_uint32, vp, C.c_int32, vp, vp,
                                                    C.c_int32, C.c_double, P(C.c_int32)]),
             "bk_last_kernel_ms": (C.c_int, [vp, P(C.c_float)]),
+            "bk_last_kernel": (C.c_char_p, [vp]),
             "bk_fset_init": (C.c_int, [vp]),
             "bk_fset_place": (C.c_int, [vp, vp, C.c_int32, vp, C.c_int32]),
             "bk_fset_copy": (C.c_int, [vp, vp]),
@@ -326,6 +327,10 @@ class Handle:
         ms = C.c_float()
         self.check(self._L.bk_last_kernel_ms(self._h, C.byref(ms)), "bk_last_kernel_ms")
         return float(ms.value)
+
+    def last_kernel(self) -> str:
+        """Name of the kernel the last timed call launched (bk_last_kernel)."""
+        return (self._L.bk_last_kernel(self._h) or b"").decode()
 
     # -- hot path -------------------------------------------------------------------
     def movegen(self, states_ptr, players_ptr, n, rows_ptr, count_ptr, mem):

@@ -3679,6 +3679,7 @@ struct bk_handle_s {
     int rollout_blocks_per_cu = 0;
     int fr_blocks_per_cu = 0;    // k_rollout_fr
     int mcts_blocks_per_cu = 0;  // k_mcts
+    const char* last_kernel = "";  // name of the kernel the last timed call launched
 };
 
 static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
@@ -3825,6 +3826,8 @@ int bk_debug_sections(bk_handle h, uint64_t* out, int32_t n, int32_t reset) {
 #endif
 }
 
+const char* bk_last_kernel(bk_handle h) { return h ? h->last_kernel : ""; }
+
 int bk_last_kernel_ms(bk_handle h, float* ms) {
     if (!h || !ms) return BK_EINVAL;
     if (!h->timed) return set_err(h, BK_EINVAL, "no timed kernel on this handle%s", "");
@@ -3882,6 +3885,7 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     const int grid = waves * groups;
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    h->last_kernel = "k_movegen_g";
     hipLaunchKernelGGL(k_movegen_g, dim3(grid), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
@@ -3928,6 +3932,7 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, nullptr, d_count, nullptr, groups, d_mask};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    h->last_kernel = "k_movegen_m";
     hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
@@ -3956,6 +3961,7 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
     }
     MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask, 0, nullptr};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    h->last_kernel = "k_has_moves";
     hipLaunchKernelGGL(k_has_moves, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
@@ -4079,14 +4085,19 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         a.long_slots = (uint32_t)ls;
     }
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    if (heur)
+    if (heur) {
+        h->last_kernel = "k_rollout_fr_h";
         hipLaunchKernelGGL(k_rollout_fr_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
-    else if (fr)
+    } else if (fr) {
+        h->last_kernel = "k_rollout_fr";
         hipLaunchKernelGGL(k_rollout_fr, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
-    else if (cfg->semantics == BK_SEM_ADVANCE)
+    } else if (cfg->semantics == BK_SEM_ADVANCE) {
+        h->last_kernel = "k_advance";
         hipLaunchKernelGGL(k_advance, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
-    else
+    } else {
+        h->last_kernel = "k_rollout";
         hipLaunchKernelGGL(k_rollout, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
+    }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;
@@ -4379,6 +4390,7 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
                    d_out, d_vis,
                    h->d_counter + 1};
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    h->last_kernel = "k_fastmcts";
     hipLaunchKernelGGL(k_fastmcts, dim3(n_games), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
@@ -4516,16 +4528,22 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     bool pair = true;
     if (const char* env = getenv("BK_MCTS_PAIR")) pair = atoi(env) != 0;  // tuning / test override
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    if (coop && heur)
+    if (coop && heur) {
+        h->last_kernel = "k_mcts_coop_h";
         hipLaunchKernelGGL(k_mcts_coop_h, dim3(blocks), dim3(blk), 0, h->cur, a);
-    else if (coop)
+    } else if (coop) {
+        h->last_kernel = "k_mcts_coop";
         hipLaunchKernelGGL(k_mcts_coop, dim3(blocks), dim3(blk), 0, h->cur, a);
-    else if (heur)
+    } else if (heur) {
+        h->last_kernel = "k_mcts_h";
         hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
-    else if (spread == 2 && pair)
+    } else if (spread == 2 && pair) {
+        h->last_kernel = "k_mcts_pair";
         hipLaunchKernelGGL(k_mcts_pair, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
-    else
+    } else {
+        h->last_kernel = "k_mcts";
         hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
+    }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;

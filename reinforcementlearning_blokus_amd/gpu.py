@@ -42,6 +42,9 @@ class BlokusGPU:
     def last_kernel_ms(self) -> float:
         return self.handle.last_kernel_ms()
 
+    def last_kernel(self) -> str:
+        return self.handle.last_kernel()
+
     def synchronize(self):
         """Wait for this handle's launches; raises if a device-path launch tripped its
         iteration guard or read a bad root_index (bk_synchronize)."""

@@ -12,7 +12,7 @@ from tests.conftest import ROOT, load_golden
 
 def declared_symbols():
     text = open(os.path.join(ROOT, "include", "blokus_hip.h")).read()
-    return sorted(set(re.findall(r"^int\s+(bk_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|const char\s*\*)\s*(bk_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_header_and_binding_agree():
