@@ -645,6 +645,9 @@ __device__ __forceinline__ void locate_pass1(int gs, uint2* rows) {
     }
 }
 
+// RS: uint4 distance between 16-slot runs of the table (2: a plain array; 64: the lane
+// pair's LDS-DMA stage of k_mcts_pair)
+template <int RS = 2>
 __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2* rows, const int16_t* key,
                                                      int mask, int& out_r, int& out_c) {
     const uint32_t info = kInfo[gs];
@@ -696,7 +699,7 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
 #pragma unroll 1
     for (int b0 = 0; b0 <= mask && hit_f < 0; b0 += 16) {
         const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
-        const uint4 na = k4[nb0 >> 3], nb = k4[(nb0 >> 3) + 1];
+        const uint4 na = k4[(nb0 >> 4) * RS], nb = k4[(nb0 >> 4) * RS + 1];
         const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -1066,16 +1069,18 @@ static const uint64_t kCellHashHost[BK_CELLS] = BK_CELL_HASH_INIT;
 #define FS_UNUSED ((int16_t)-1)
 #define FS_DUMMY ((int16_t)-2)
 
-struct FsetRef {  // one player's table: slots 2j, 2j + 1 at key[j * stride], key[j * stride + 1]
+struct FsetRef {  // one player's table: runs of 2^sh slots, run j at key[j * stride]
     int16_t* key;
-    int stride;       // 2: a plain array; 2 * WAVE: slot pairs of one lane interleaved in LDS
+    int stride;       // 2: a plain array; 2 * WAVE: slot pairs of one lane interleaved in LDS;
+                      // 512 (sh 4): 16-slot runs of a lane pair's LDS-DMA stage (k_mcts_pair)
     uint16_t* mask;
     uint16_t* fill;
     uint16_t* used;
     uint32_t cap;     // largest table this storage holds (power of 2)
     const uint64_t* hash;  // hash((r, c)) by cell
+    int sh = 1;       // log2 of the run length
     __host__ __device__ __forceinline__ int16_t& at(uint64_t i) const {
-        return key[(i >> 1) * (uint64_t)stride + (i & 1u)];
+        return key[(i >> sh) * (uint64_t)stride + (i & ((1u << sh) - 1u))];
     }
 };
 
@@ -1423,6 +1428,59 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
             }
             return true;
         }
+    }
+    if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real)) return false;
+    return RECOPY ? fs_recopy_global(fl, p, htab) : true;
+}
+
+// k_mcts_pair's LDS-DMA stage of the mover's table: the lane pair (2q, 2q + 1) loads run
+// k (slots 16k .. 16k + 15, 32 bytes) of pair q's table with one global_load_lds_dwordx4
+// per lane, so run k of pair q sits at dwords DMA_BASE + 256 k + 8 q of the wave's area.
+#define DMA_RUNS 8                       // tables of <= 128 slots are staged
+#define DMA_RUN_DWORDS (WAVE * 4)        // one wave-instruction: 64 lanes x 16 bytes
+#define DMA_RUN_I16 (2 * DMA_RUN_DWORDS)
+
+// place_frontier on the DMA stage (stage_q = pair q's slot 0; mask / fill / used as
+// loaded): the ops in LDS, then the table (or, RECOPY, its copy) written to fl.  Falls
+// back to the global table when the ops outgrow the stage.
+template <bool RECOPY>
+__device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* stage_q, const uint64_t* htab,
+                                                   const int32_t (&cells)[5], uint64_t real) {
+    bk_fset* gfs = &fl->s;
+    uint16_t m = gfs->mask[p], f = gfs->fill[p], u = gfs->used[p];
+    FsetRef t{stage_q, DMA_RUN_I16, &m, &f, &u, 16u * DMA_RUNS, htab, 4};
+    if (fs_run_ops(t, fl->tmp, cells, real)) {
+        bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
+        const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(stage_q);
+        const uint32_t newsize = fs_copy_size(u);
+        if (!RECOPY || (newsize - 1 == m && f == u)) {  // (a copy of a clean table is the table)
+#pragma unroll
+            for (int r = 0; r < DMA_RUNS; ++r) {
+                if ((uint32_t)(16 * r) <= m) {
+                    dst4[2 * r] = src4[r * (DMA_RUN_DWORDS / 4)];
+                    dst4[2 * r + 1] = src4[r * (DMA_RUN_DWORDS / 4) + 1];
+                }
+            }
+            gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+            return true;
+        }
+        const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+#pragma unroll 1
+        for (uint32_t i = 0; i < newsize / 8; ++i) dst4[i] = unused;
+        gfs->mask[p] = (uint16_t)(newsize - 1); gfs->fill[p] = u; gfs->used[p] = u;
+        SlotBits o;
+        int16_t* dk = gfs->key[p];
+#pragma unroll 1
+        for (uint32_t i = 0; i <= m; i += 8) {
+            const uint4 v = src4[(i >> 4) * (DMA_RUN_DWORDS / 4) + ((i >> 3) & 1u)];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int16_t k = (int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+                if (k >= 0) dk[fs_clean_slot(htab[k], newsize - 1, o)] = k;
+            }
+        }
+        return true;
     }
     if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real)) return false;
     return RECOPY ? fs_recopy_global(fl, p, htab) : true;
@@ -2653,10 +2711,12 @@ __device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&p
 // of others.
 // RECOPY: the table then becomes its Board.copy() in place (expansion and replay edges:
 // node boards are copies).
+// stage_q (k_mcts_pair): the mover's table is already in the LDS-DMA stage at stage_q.
 template <bool RECOPY>
 __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
                                                 const uint64_t* htab, const uint32_t (&pm)[5],
-                                                const int32_t (&cells)[5], uint64_t real, int16_t* lk) {
+                                                const int32_t (&cells)[5], uint64_t real, int16_t* lk,
+                                                int16_t* stage_q = nullptr) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
 #pragma unroll
@@ -2666,7 +2726,8 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
             slab.at(4, ar + d) |= pm[d];
         }
     }
-    const bool ok = place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
+    const bool ok = stage_q ? place_frontier_dma<RECOPY>(T, p, stage_q, htab, cells, real)
+                            : place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
     m.first &= ~(1u << p);
@@ -2965,12 +3026,18 @@ template <bool HEUR, bool PAIR = false>
 __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     static_assert(!(HEUR && PAIR), "the heuristic pass is not split");
     constexpr int BLK = HEUR ? HBLOCK : BLOCK;
-    constexpr int AREA = HEUR ? HEUR_WORDS : ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS);
+    // PAIR: + the LDS-DMA stage of the pairs' mover tables after the 40 dwords per lane of
+    // counts / rows (2 blocks of 77 KB per CU)
+    constexpr int AREA = HEUR ? HEUR_WORDS : PAIR ? 40 * WAVE + DMA_RUNS * DMA_RUN_DWORDS
+                                                  : ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS);
+    static_assert(AREA >= ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS) || HEUR, "the replay's 128-slot stage fits");
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
     // per wave: counts / B,C rows (+ HEUR: per-piece e sums) / the staged frontier table
     __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + 2 * BK_CELLS + HS_WORDS];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint32_t* my = lds + wv * AREA;
+    uint32_t* dstage = my + 40 * WAVE;  // PAIR: run r of pair q at dstage + r * DMA_RUN_DWORDS + 8 q
+    int16_t* stage_q = reinterpret_cast<int16_t*>(dstage + 8 * (lane >> 1));
     uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
     int16_t* lk = reinterpret_cast<int16_t*>(my) + 2 * lane;
     uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
@@ -3030,6 +3097,8 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         int cp = p;
         uint32_t c_first = (m.first >> p) & 1u, c_used = m.used.get(p);
         uint32_t* c_base = slab.base;
+        const bk_fset* ofs = nullptr;  // PAIR: the pair's node / sim tables and the mover's mask
+        uint32_t omask = 0xFFFFu;
         if constexpr (PAIR) {
             const int o = lane & ~1;
             c_idle = __shfl((int)idle, o) != 0;
@@ -3037,6 +3106,8 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             c_first = (uint32_t)__shfl((int)c_first, o);
             c_used = (uint32_t)__shfl((int)c_used, o);
             c_base = a.slab + (size_t)(slot & ~1u) * SLAB_WORDS;
+            ofs = &a.lanes[slot & ~1u].A.s;
+            omask = ofs->mask[cp];
         }
         const Slab cslab{c_base};
         Planes P;
@@ -3050,6 +3121,22 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             derive_rows(own, occ, c_first, cp, P);
         }
         make_pairs(P);
+        // PAIR: the mover's table (<= 128 slots) goes to the pair's LDS-DMA stage while the
+        // stencil runs: the lanes of a pair load alternate 16-byte halves of each 16-slot run
+        bool staged = false;
+        if constexpr (PAIR) {
+            staged = !c_idle && omask < 16u * DMA_RUNS;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the table's last stores have landed
+            const int16_t* src = ofs->key[cp] + 8 * (lane & 1);
+#pragma unroll
+            for (int r = 0; r < DMA_RUNS; ++r) {
+                const bool need = staged && omask >= 16u * (uint32_t)r;
+                if (__builtin_amdgcn_ballot_w64(need) == 0ull) break;
+                if (need)
+                    __builtin_amdgcn_global_load_lds((const void*)(src + 16 * r), (void*)(dstage + r * DMA_RUN_DWORDS),
+                                                     16, 0, 0);
+            }
+        }
         const uint32_t avail = c_idle ? 0u : (~c_used & 0x1FFFFFu);
         uint32_t total = movegen_counts<true, PAIR>(P, avail, my, lane);
         if constexpr (PAIR) total += (uint32_t)__shfl_xor((int)total, 1);
@@ -3122,6 +3209,10 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
                                    ar, ac, h_unc);
             }
             if (h_unc) m.status |= BK_MCTS_EUNCERT;
+        } else if (PAIR) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
+            if (staged) locate_move_frontier<DMA_RUN_DWORDS / 4>(gs, kk, rows_lds, stage_q, (int)omask, ar, ac);
+            else locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
         } else {
             locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
         }
@@ -3157,8 +3248,9 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         // expand: new_board = board.copy() is table A itself (A is a copy, see mc_replay),
         // and MCTSNode(new_board)'s copy replaces the mover's table in place; the rollout's
         // sim = node.board.copy() is that copy again (A), and its plies place on A
-        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
-        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
+        int16_t* sq = (PAIR && staged) ? stage_q : nullptr;
+        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
+        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
         if (expand) {
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
