@@ -448,19 +448,24 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
         prof["advance_s"] += time.perf_counter() - ta
         states[active], sets[active], rng[active] = sub_st, sub_fs, sub_rng
         stopped = []
-        for j, i in enumerate(active):
+        status = res["status"].astype(np.int64)
+        prof["uncertified_heuristic"] += int(np.count_nonzero(status & N.STATUS_UNCERT))
+        bad = status & ~(N.STATUS_CAP | N.STATUS_STOP | N.STATUS_UNCERT)
+        if bad.any():
+            j = int(np.flatnonzero(bad)[0])
+            raise RuntimeError(f"game {idx[int(active[j])]}: kernel status {int(status[j])}")
+        stop = (status & N.STATUS_STOP) != 0
+        stopped = active[stop].tolist()
+        # finished games (the rest): record results, turns and passes as whole arrays
+        fin = np.flatnonzero(~stop)
+        f_turns = (before[fin, 0].astype(np.int64) + res["turns"][fin].astype(np.int64)).tolist()
+        f_passes = (before[fin, 1].astype(np.int64) + res["passes"][fin].astype(np.int64)).tolist()
+        f_cap = ((status[fin] & N.STATUS_CAP) != 0).tolist()
+        for j, turns, passes, cap in zip(fin.tolist(), f_turns, f_passes, f_cap):
+            i = int(active[j])
             r = res[j]
-            if int(r["status"]) & N.STATUS_UNCERT:
-                prof["uncertified_heuristic"] += 1
-            if int(r["status"]) & N.STATUS_STOP:
-                stopped.append(i)
-                continue
-            if int(r["status"]) & ~(N.STATUS_CAP | N.STATUS_STOP | N.STATUS_UNCERT):
-                raise RuntimeError(f"game {idx[i]}: kernel status {int(r['status'])}")
-            turns = int(before[j, 0]) + int(r["turns"])
-            passes = int(before[j, 1]) + int(r["passes"])
             truncated = False
-            if int(r["status"]) & N.STATUS_CAP:  # cut by max_turns: over or not (arena_runner.py:702)
+            if cap:  # cut by max_turns: over or not (arena_runner.py:702)
                 if int(gpu.has_moves(states[i:i + 1])[0]) != 0:
                     truncated = True
                 else:

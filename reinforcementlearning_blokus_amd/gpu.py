@@ -30,9 +30,21 @@ def _as_host(x, dtype):
 class BlokusGPU:
     """Owns one bk_handle (one HIP stream + scratch) on `device`."""
 
+    _shared: dict = {}
+
     def __init__(self, device: int = 0):
         self.handle = N.Handle(device)
         self.device = device
+
+    @classmethod
+    def shared(cls, device: int = 0) -> "BlokusGPU":
+        """One engine per device for batched callers (MCTSAgent.search_packed): the
+        agents of an arena share its handle and scratch instead of each allocating its
+        own.  Each native call takes the handle's lock."""
+        eng = cls._shared.get(device)
+        if eng is None:
+            eng = cls._shared.setdefault(device, cls(device))
+        return eng
 
     # ------------------------------------------------------------------ helpers
     def _stream_from_torch(self):

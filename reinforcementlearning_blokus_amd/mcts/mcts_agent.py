@@ -313,7 +313,7 @@ class MCTSAgent:
             groups.setdefault(key, []).append(i)
         for (iters, max_roll, c, use_tt, tl_us, policy), idx in groups.items():
             ags = [agents[i] for i in idx]
-            gpu = ags[0]._gpu = ags[0]._gpu or BlokusGPU(ags[0].device)
+            gpu = BlokusGPU.shared(ags[0].device)
             rts = np.ascontiguousarray(roots[idx])
             sts = np.ascontiguousarray(sets[idx])
             pl = np.array([players[i] for i in idx], np.uint8)
@@ -337,17 +337,19 @@ class MCTSAgent:
             SEARCH_TOTALS["kernel_ms"] += gpu.last_kernel_ms()
             SEARCH_TOTALS["sims"] += int(r["out"]["iterations_run"].sum())
             SEARCH_TOTALS["rollout_plies"] += int(r["out"]["rollout_plies"].astype(np.int64).sum())
+            ro = r["out"]  # per-search fields as Python ints (structured-scalar access is slow)
+            f_it, f_hits, f_roll = ro["iterations_run"].tolist(), ro["tt_hits"].tolist(), ro["rollouts"].tolist()
+            f_status, f_best = ro["status"].tolist(), ro["best_move"].tolist()
             for j, (i, a) in enumerate(zip(idx, ags)):
-                o = r["out"][j]
                 st = rng_states[j]
                 a.rollout_agent.rng.set_state((st[0], mt[j, :624].copy(), int(mt[j, 624]), st[3], st[4]))
-                n_it = int(o["iterations_run"])
+                n_it = f_it[j]
                 hits = r["hit_flags"][j, :n_it]
                 rew = r["rewards"][j, :n_it]
                 a.stats["iterations_run"] = n_it
                 # HeuristicAgent rollouts: a draw within 2^-40 of a probability boundary
                 # (BK_MCTS_EUNCERT; the kernel flags the search, it does not count draws)
-                unc = bool(int(o["status"]) & N.MCTS_EUNCERT)
+                unc = bool(f_status[j] & N.MCTS_EUNCERT)
                 a.stats["last_search_uncertified"] = unc
                 a.stats["uncertified_searches"] = a.stats.get("uncertified_searches", 0) + int(unc)
                 if tl_us:
@@ -357,18 +359,18 @@ class MCTSAgent:
                         warnings.warn(f"MCTSAgent: a {a.time_limit} s search stopped at its {iters}-iteration "
                                       "bound before the time ran out", RuntimeWarning, stacklevel=2)
                 a.stats["time_elapsed"] = dt
-                a.stats["transposition_hits"] += int(o["tt_hits"])
+                a.stats["transposition_hits"] += f_hits[j]
                 a.stats["rollout_rewards"].extend(rew[hits == 0].tolist())
                 if use_tt:
                     t = a.transposition_table
-                    t.access_count += int(o["tt_hits"]) + int(o["rollouts"])
-                    t.hit_count += int(o["tt_hits"])
+                    t.access_count += f_hits[j] + f_roll[j]
+                    t.hit_count += f_hits[j]
                     t.gpu_size = int(a._gpu_tt.count[0])
                     if t.gpu_size > 500000:  # mcts_agent.py:338-339
                         t.clear()
                         a._gpu_tt.release()
                         a._gpu_tt = None
-                out[i] = int(o["best_move"]) if o["best_move"] >= 0 else None
+                out[i] = f_best[j] if f_best[j] >= 0 else None
         return out
 
     def _get_move_positions(self, move: Move) -> List[Position]:
