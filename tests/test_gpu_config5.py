@@ -141,3 +141,23 @@ def test_config5_full_scale(gpu):
     t1 = time.perf_counter()
     _check_against_oracle(batch, list(range(0, n, n // 16)))
     _progress(f"config5 oracle sample checked in {time.perf_counter() - t1:.1f} s")
+
+
+def test_late_game_tt_hits_at_scale(gpu):
+    """The TT-hit path at scale (config 5's own 20-ply roots see almost no hits): 16,384
+    searches x 512 iterations from 52-ply positions, whose trees reach terminal positions
+    that every later visit re-simulates through the TT (mcts_agent.py:408-437,
+    mcts/zobrist.py:155-220).  Properties on every search; bit-exact against or_mcts on a
+    strided sample plus the searches with the most hits."""
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    n, iters = 16384, 512
+    roots, sets = frontier_roots(gpu, n, 52, seed=777)
+    batch = MctsBatch(gpu, roots, sets, iterations=iters, seed0=90_000, want_rewards=True)
+    batch.run(chunk=256)
+    _check_properties(batch)
+    res = batch.results()
+    hits = res["tt_hits"].astype(np.int64)
+    _progress(f"late-game TT: {int(hits.sum())} hits, {(hits > 0).mean():.3f} of searches with one")
+    assert (hits > 0).mean() > 0.05
+    top = np.argsort(-hits, kind="stable")[:12].tolist()
+    _check_against_oracle(batch, sorted(set(list(range(0, n, n // 12)) + top)))
