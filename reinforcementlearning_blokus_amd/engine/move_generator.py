@@ -162,10 +162,20 @@ class LegalMoveGenerator:
             self._gpu.engine = eng
         return eng
 
+    @staticmethod
+    def _legality_key(state) -> bytes:
+        """The packed fields a legal set depends on: planes, used pieces, first-move flags."""
+        return state["planes"].tobytes() + state["used"].tobytes() + state["first_move"].tobytes()
+
     def _masks(self, boards: Sequence[Board], players: Sequence[Player]):
         from .board import pack_states
         states = pack_states(boards)
         pl = np.array([p.value - 1 for p in players], dtype=np.uint8)
+        if len(boards) == 1:  # the rows players_with_moves fetched for this very position
+            last = getattr(self._gpu, "last_rows", None)
+            if last is not None and last[0] == self._legality_key(states[0]):
+                k = int(pl[0])
+                return last[1][k:k + 1], last[2][k:k + 1]
         return self._engine().movegen(states, pl, rows=True)
 
     @staticmethod
@@ -207,9 +217,14 @@ class LegalMoveGenerator:
         return self.get_move_count(board, player) > 0
 
     def players_with_moves(self, board: Board) -> List[bool]:
-        """has_legal_moves for all four players in ONE launch (BlokusGame._check_game_over)."""
+        """has_legal_moves for all four players in ONE launch (BlokusGame._check_game_over).
+        The launch also returns the four legal sets, kept (per thread, keyed by the packed
+        position) for the next get_legal_moves on the same position -- the next player's
+        turn in a game loop -- so a ply costs one launch, not two."""
         from .board import pack_states
-        cnt, _ = self._engine().movegen(pack_states([board] * 4), np.arange(4, dtype=np.uint8), rows=False)
+        st = pack_states([board])
+        cnt, rows = self._engine().movegen(np.repeat(st, 4), np.arange(4, dtype=np.uint8), rows=True)
+        self._gpu.last_rows = (self._legality_key(st[0]), cnt, rows)
         return [int(c) > 0 for c in cnt]
 
     def _has_any_legal_move_frontier(self, board: Board, player: Player) -> bool:
