@@ -6,6 +6,7 @@ implementation behind any of these functions.
 """
 from __future__ import annotations
 
+import threading
 import warnings
 
 import numpy as np
@@ -30,7 +31,7 @@ def _as_host(x, dtype):
 class BlokusGPU:
     """Owns one bk_handle (one HIP stream + scratch) on `device`."""
 
-    _shared: dict = {}
+    _shared = threading.local()
 
     def __init__(self, device: int = 0):
         self.handle = N.Handle(device)
@@ -38,13 +39,14 @@ class BlokusGPU:
 
     @classmethod
     def shared(cls, device: int = 0) -> "BlokusGPU":
-        """One engine per device for batched callers (MCTSAgent.search_packed): the
-        agents of an arena share its handle and scratch instead of each allocating its
-        own.  Each native call takes the handle's lock."""
-        eng = cls._shared.get(device)
-        if eng is None:
-            eng = cls._shared.setdefault(device, cls(device))
-        return eng
+        """One engine per (thread, device) for batched callers (MCTSAgent.search_packed):
+        the agents of an arena share its handle and scratch instead of each allocating its
+        own.  Per thread, because a call binds the handle to the caller's current torch
+        stream (agents run in worker threads in the reference's web API)."""
+        engines = cls._shared.__dict__.setdefault("engines", {})
+        if device not in engines:
+            engines[device] = cls(device)
+        return engines[device]
 
     # ------------------------------------------------------------------ helpers
     def _stream_from_torch(self):
