@@ -388,7 +388,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     move order.  Per-move times are launch shares.  progress(round, games_left, profile),
     if given, is called at the start of every round."""
     from .. import _native as N
-    from ..engine.move_generator import order_moves, order_moves_many
+    from ..engine.move_generator import frontier_ranks, order_moves, order_moves_many
     from ..engine.pieces import ORIENT_CELLS, ORIENT_LIST
     from ..gpu import BlokusGPU, empty_state
     idx = list(game_indices)
@@ -478,7 +478,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
             cnt, rows = gpu.movegen(states[stopped], pl)
             chosen: Dict[int, Optional[int]] = {}
             by_kind: Dict[str, List[Tuple[int, Any, int, list]]] = {"mcts": [], "fast": []}
-            fast_k, fast_fr = [], []
+            fast_k = []
             for k, i in enumerate(stopped):
                 p = int(pl[k])
                 adapter = agents[i][seats[i][str(p + 1)]]
@@ -491,11 +491,11 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                         legal = [None] * int(cnt[k])
                 else:  # FastMCTS: the reference's list order (frontier sets), ordered below at once
                     fast_k.append(k)
-                    fast_fr.append([divmod(c, 20) for c in N.fset_list(sets[i:i + 1], p)])
                     legal = None
                 by_kind[kind].append((i, adapter, p, legal))
             if fast_k:
-                ordered = iter(order_moves_many(rows[np.array(fast_k)], fast_fr))
+                fk = np.array(fast_k)
+                ordered = iter(order_moves_many(rows[fk], ranks=frontier_ranks(sets[stopped[fk]], pl[fk])))
                 by_kind["fast"] = [(i, a, p, next(ordered)) for i, a, p, _ in by_kind["fast"]]
             if by_kind["mcts"]:
                 todo = [(i, a, p, lg) for i, a, p, lg in by_kind["mcts"] if len(lg) > 1]

@@ -107,12 +107,30 @@ def order_moves(rows: np.ndarray, frontier: Optional[Sequence] = None):
     return g[order], r[order], c[order]
 
 
-def order_moves_many(rows: np.ndarray, frontiers: Sequence[Sequence]):
+def frontier_ranks(sets: np.ndarray, players) -> np.ndarray:
+    """rank[i, cell]: the position of `cell` (r * 20 + c) in the iteration order of player
+    players[i]'s frontier set held in sets[i] (FSET_DTYPE, the CPython table: slot order
+    of the keys >= 0 in slots 0..mask), _BIG where absent.  The vectorised equivalent of
+    ranking fset_list(sets[i], players[i]) (engine/board.py:247-258 get_frontier)."""
+    m = len(sets)
+    pl = np.asarray(players, dtype=np.int64)
+    keys = sets["key"][np.arange(m), pl].astype(np.int64)  # [m, 256]
+    mask = sets["mask"][np.arange(m), pl].astype(np.int64)
+    valid = (keys >= 0) & (np.arange(keys.shape[1])[None, :] <= mask[:, None])
+    order = np.cumsum(valid, axis=1) - 1
+    rank = np.full((m, 400), _BIG, dtype=np.int64)
+    ii, ss = np.nonzero(valid)
+    rank[ii, keys[ii, ss]] = order[ii, ss]  # a set holds each key once
+    return rank
+
+
+def order_moves_many(rows: np.ndarray, frontiers: Optional[Sequence[Sequence]] = None, *,
+                     ranks: Optional[np.ndarray] = None):
     """order_moves for m board-players at once: rows uint32[m,91,20], frontiers[i] the
-    iteration-order (row, col) list of board-player i's frontier set.  Returns a list of
-    m (g, r, c) tuples, each in the reference's frontier list order (the key of
-    order_moves: piece asc, orientation asc, min over the move's cells on a frontier cell
-    of (rank, cell index))."""
+    iteration-order (row, col) list of board-player i's frontier set (or ranks, int64
+    [m, 400], from frontier_ranks).  Returns a list of m (g, r, c) tuples, each in the
+    reference's frontier list order (the key of order_moves: piece asc, orientation asc,
+    min over the move's cells on a frontier cell of (rank, cell index))."""
     rows = np.ascontiguousarray(rows, dtype="<u4")
     m = rows.shape[0]
     if m == 0:
@@ -123,11 +141,13 @@ def order_moves_many(rows: np.ndarray, frontiers: Sequence[Sequence]):
     bits = np.unpackbits(words.view(np.uint8).reshape(-1, 4), axis=1, bitorder="little")
     w, c = np.nonzero(bits)  # word-major (game, g, r ascending), columns ascending
     gi, g, r = gi[w], g[w], r[w]
-    rank = np.full((m, 400), _BIG, dtype=np.int64)
-    for i, fr in enumerate(frontiers):
-        for j, (a, b) in enumerate(fr):
-            if rank[i, a * 20 + b] == _BIG:
-                rank[i, a * 20 + b] = j
+    rank = ranks
+    if rank is None:
+        rank = np.full((m, 400), _BIG, dtype=np.int64)
+        for i, fr in enumerate(frontiers):
+            for j, (a, b) in enumerate(fr):
+                if rank[i, a * 20 + b] == _BIG:
+                    rank[i, a * 20 + b] = j
     cells = (r[:, None] + _DR[g]) * 20 + (c[:, None] + _DC[g])
     valid = np.arange(5)[None, :] < _NCELLS[g][:, None]
     cells = np.where(valid, np.clip(cells, 0, 399), 0)

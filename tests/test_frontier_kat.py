@@ -108,3 +108,30 @@ def test_bitboards_follow_grid_and_copy():
     c.place_piece([Position(19, 19)], Player.YELLOW, 1, validate=False)
     assert b.player_bits[Player.YELLOW] == 0 and c.player_bits[Player.YELLOW] == 1 << 399
     assert b.get_frontier(Player.RED) == c.get_frontier(Player.RED)
+
+
+def test_frontier_ranks_equal_fset_list_order():
+    """frontier_ranks (vectorised, from the tables) ranks every player's frontier cells
+    exactly as the iteration order fset_list gives (the batched arena's FastMCTS lists)."""
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.engine.move_generator import _BIG, frontier_ranks
+    from reinforcementlearning_blokus_amd.engine.pieces import ORIENT_CELLS, ORIENT_LIST
+    rng = np.random.RandomState(5)
+    boards = []
+    for t in range(24):
+        b = Board()
+        for _ in range(rng.randint(0, 30)):  # unvalidated placements: arbitrary table histories
+            g = rng.randint(len(ORIENT_CELLS))
+            ar, ac = rng.randint(0, 16), rng.randint(0, 16)
+            cells = [Position(ar + dr, ac + dc) for dr, dc in ORIENT_CELLS[g]]
+            if all(b.is_empty(p) for p in cells):
+                b.place_piece(cells, list(Player)[rng.randint(4)], ORIENT_LIST[g][0], validate=False)
+        boards.append(b)
+    sets = np.concatenate([b.frontier_tables for b in boards])
+    for p in range(4):
+        ranks = frontier_ranks(sets, [p] * len(boards))
+        for i in range(len(boards)):
+            want = np.full(400, _BIG, np.int64)
+            for j, cell in enumerate(N.fset_list(sets[i:i + 1], p)):
+                want[cell] = j
+            assert np.array_equal(ranks[i], want), (i, p)
