@@ -33,6 +33,7 @@ import numpy as np
 
 from ..engine.board import Board, Player
 from ..engine.move_generator import Move, get_shared_generator
+from ..gpu import BlokusGPU
 
 _MT_WORDS = 625
 _MAX_CHILDREN = 2048
@@ -253,8 +254,9 @@ class FastMCTSAgent:
         for c, ks in groups.items():
             mt = np.stack([agents[k]._rng_words() for k in ks])
             counts = [max(1, int(iterations[k])) for k in ks]
-            out = agents[ks[0]]._engine().fastmcts([len(legal_lists[k]) for k in ks], counts, [base_of[k] for k in ks],
-                                                   mt, _log_table(max(counts) + 1), c)
+            eng = BlokusGPU.shared(agents[ks[0]].device)  # one handle for all batched launches
+            out = eng.fastmcts([len(legal_lists[k]) for k in ks], counts, [base_of[k] for k in ks],
+                               mt, _log_table(max(counts) + 1), c)
             for j, k in enumerate(ks):
                 agents[k]._set_rng_words(mt[j])
                 res, legal = out[j], legal_lists[k]
@@ -298,8 +300,9 @@ class FastMCTSAgent:
         for ce, ks in groups.items():
             mt = np.stack([agents[k]._rng_words() for k in ks])
             counts = [max(1, int(iterations[k])) for k in ks]
-            res = agents[ks[0]]._engine().fastmcts([len(legal_arrays[k][0]) for k in ks], counts,
-                                                   [base_of[k] for k in ks], mt, _log_table(max(counts) + 1), ce)
+            eng = BlokusGPU.shared(agents[ks[0]].device)  # one handle for all batched launches
+            res = eng.fastmcts([len(legal_arrays[k][0]) for k in ks], counts, [base_of[k] for k in ks], mt,
+                               _log_table(max(counts) + 1), ce)
             for j, k in enumerate(ks):
                 agents[k]._set_rng_words(mt[j])
                 g, r, c = legal_arrays[k]
