@@ -4575,10 +4575,12 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     // persistent grid: every resident slot pulls whole searches from the counter
     const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;
     // one wave per search (k_mcts_coop) when the batch cannot fill the chip with one
-    // search per lane: a cooperative search runs ~6x faster than a lane's (config 4: MCTS
-    // phase 53 -> 8.6 s at ~500 searches per launch), so it wins while the searches take
-    // fewer than ~6 rounds of the resident waves (config 4's arena rounds, single calls)
-    bool coop = (int64_t)n_games <= 16 * (int64_t)h->num_cu;
+    // search per lane.  Measured crossovers (64 iterations, profiles/r03/coopsweep):
+    // random rollouts ~24 searches per CU (k_mcts_pair 229 ms flat vs k_mcts_coop 307 ms
+    // at 32 per CU); heuristic rollouts ~90 per CU (k_mcts_h 1.88 s flat vs k_mcts_coop_h
+    // 1.33 s at 64 per CU, 2.61 s at 128) -- config 4 with 8,192 games on one GPU
+    // searches 8,192 at once: 164 -> 242 games/s
+    bool coop = (int64_t)n_games <= (heur ? 80 : 24) * (int64_t)h->num_cu;
     if (const char* env = getenv("BK_MCTS_COOP")) coop = atoi(env) != 0;  // tuning / test override
     const int blk = coop ? COOP_WAVES * WAVE : heur ? HBLOCK : BLOCK;
     int blocks = h->num_cu * (coop ? 2 : heur ? 3 : h->mcts_blocks_per_cu);
