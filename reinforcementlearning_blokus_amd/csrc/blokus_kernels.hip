@@ -4575,15 +4575,20 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     // persistent grid: every resident slot pulls whole searches from the counter
     const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;
     // one wave per search (k_mcts_coop) when the batch cannot fill the chip with one
-    // search per lane.  Measured crossovers (64 iterations, profiles/r03/coopsweep):
-    // random rollouts ~24 searches per CU (k_mcts_pair 229 ms flat vs k_mcts_coop 307 ms
-    // at 32 per CU); heuristic rollouts ~90 per CU (k_mcts_h 1.88 s flat vs k_mcts_coop_h
-    // 1.33 s at 64 per CU, 2.61 s at 128) -- config 4 with 8,192 games on one GPU
-    // searches 8,192 at once: 164 -> 242 games/s
-    bool coop = (int64_t)n_games <= (heur ? 80 : 24) * (int64_t)h->num_cu;
+    // search per lane.  Measured crossovers (64 iterations, profiles/r03/coopsweep,
+    // coopblocks): random rollouts ~44 searches per CU (k_mcts_pair 229 ms flat vs
+    // k_mcts_coop 162 ms at 32 per CU with 4 blocks per CU); heuristic rollouts ~90 per CU
+    // (k_mcts_h 1.88 s flat vs k_mcts_coop_h 1.33 s at 64 per CU, 2.61 s at 128) --
+    // config 4 with 8,192 games on one GPU searches 8,192 at once: 164 -> 242 games/s
+    bool coop = (int64_t)n_games <= (heur ? 80 : 40) * (int64_t)h->num_cu;
     if (const char* env = getenv("BK_MCTS_COOP")) coop = atoi(env) != 0;  // tuning / test override
     const int blk = coop ? COOP_WAVES * WAVE : heur ? HBLOCK : BLOCK;
-    int blocks = h->num_cu * (coop ? 2 : heur ? 3 : h->mcts_blocks_per_cu);
+    // k_mcts_coop(_h) blocks (of COOP_WAVES searches) per CU: all the waves the registers
+    // allow (k_mcts_coop 225 VGPRs: 2 per SIMD, twice the throughput of 1 --
+    // profiles/r03/coopblocks; k_mcts_coop_h 404: 1)
+    int coop_bpc = heur ? 2 : 4;
+    if (const char* env = getenv("BK_COOP_BLOCKS_PER_CU")) coop_bpc = atoi(env) > 0 ? atoi(env) : coop_bpc;  // tuning
+    int blocks = h->num_cu * (coop ? coop_bpc : heur ? 3 : h->mcts_blocks_per_cu);
     // k_mcts is latency-bound at one wave per SIMD (config 5: 65,536 searches fill one
     // 256-lane block per CU): when the resident slots allow, every other lane takes a
     // search, so twice the waves hide each other's latency (11.14 vs 10.84 M sims/s,
