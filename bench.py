@@ -71,7 +71,9 @@ def parse(argv=None):
     ap.add_argument("--games", type=int, default=None, help="config3: 256; config5: 65536; config4: 8192 (whole job)")
     ap.add_argument("--rollouts", type=int, default=1024)
     ap.add_argument("--iterations", type=int, default=4096, help="config5 MCTS iterations per search")
-    ap.add_argument("--chunk", type=int, default=512, help="config5 iterations per launch")
+    ap.add_argument("--chunk", type=int, default=1024,
+                    help="config5 iterations per launch (1,024: 14.23 M sims/s vs 14.03 M at 512, "
+                         "profiles/r03/chunks)")
     ap.add_argument("--rollout-policy", choices=("random", "heuristic"), default="random",
                     help="config5: RandomAgent rollouts (the workload) or HeuristicAgent rollouts "
                          "(MCTSAgent's default rollout agent)")
