@@ -13,6 +13,7 @@ import random
 import time
 import warnings
 import traceback
+from concurrent.futures import ThreadPoolExecutor
 from datetime import datetime
 from pathlib import Path
 from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple
@@ -376,6 +377,24 @@ def _batchable(run_config: RunConfig, seats: Mapping[str, str]) -> bool:
 LAST_BATCH_PROFILE: Dict[str, float] = {}  # phase times of the last run_games_batched call
 
 
+_MCTS_WORKER: Optional[ThreadPoolExecutor] = None
+
+
+def _mcts_worker() -> ThreadPoolExecutor:
+    """The thread run_games_batched runs its MCTS launches on (one per process, idle
+    between runs; BlokusGPU.shared gives it its own engine and stream)."""
+    global _MCTS_WORKER
+    if _MCTS_WORKER is None:
+        _MCTS_WORKER = ThreadPoolExecutor(1, thread_name_prefix="bk-mcts")
+    return _MCTS_WORKER
+
+
+def _timed_search(agents, roots, sets, players):
+    t0 = time.perf_counter()
+    mv = MCTSAgent.search_packed(agents, roots, sets, players)
+    return mv, time.perf_counter() - t0
+
+
 def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
                       device: int = 0, progress=None) -> List[Dict[str, Any]]:
     """Mixed seatings (Random / Heuristic / MCTS / FastMCTS, config 4) in lockstep batches:
@@ -437,6 +456,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     # but a host's rounding could pick the neighbour (HeuristicAgent)
     prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0,
                 uncertified_heuristic=0)
+    worker = _mcts_worker()
     while len(active):
         prof["rounds"] += 1
         if progress is not None:
@@ -477,6 +497,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
             pl = (states["current_player"][stopped] & 3).astype(np.uint8)
             cnt, rows = gpu.movegen(states[stopped], pl)
             chosen: Dict[int, Optional[int]] = {}
+            mcts_job = None
             by_kind: Dict[str, List[Tuple[int, Any, int, list]]] = {"mcts": [], "fast": []}
             fast_k = []
             for k, i in enumerate(stopped):
@@ -509,17 +530,12 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                         e["total_simulations"] += a.agent.stats["iterations_run"]
                         e["moves_with_simulations"] += 1
                 if todo:
+                    # the MCTS searches run on a worker thread (its own engine and stream)
+                    # while this thread prepares and launches the FastMCTS seats; the two
+                    # sets of games are disjoint and nothing below reads them until joined
                     ti = np.array([t[0] for t in todo])
-                    tm = time.perf_counter()
-                    mv = MCTSAgent.search_packed([t[1].agent for t in todo], states[ti], sets[ti], [t[2] for t in todo])
-                    prof["mcts_s"] += time.perf_counter() - tm
-                    prof["uncertified_heuristic"] += sum(int(t[1].agent.stats.get("last_search_uncertified", False))
-                                                         for t in todo)
-                    for (i, a, p, lg), m in zip(todo, mv):
-                        chosen[i] = m
-                        e = per_agent[i][seats[i][str(p + 1)]]
-                        e["total_simulations"] += a.agent.stats["iterations_run"]
-                        e["moves_with_simulations"] += 1
+                    mcts_job = (todo, worker.submit(_timed_search, [t[1].agent for t in todo], states[ti], sets[ti],
+                                                    [t[2] for t in todo]))
             if by_kind["fast"]:
                 ags, lists, iters = [], [], []
                 for i, a, p, lg in by_kind["fast"]:
@@ -542,6 +558,17 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                     if len(g) > 1:
                         e["total_simulations"] += it
                         e["moves_with_simulations"] += 1
+            if mcts_job is not None:
+                todo, fut = mcts_job
+                mv, dt_m = fut.result()
+                prof["mcts_s"] += dt_m
+                prof["uncertified_heuristic"] += sum(int(t[1].agent.stats.get("last_search_uncertified", False))
+                                                     for t in todo)
+                for (i, a, p, lg), m in zip(todo, mv):
+                    chosen[i] = m
+                    e = per_agent[i][seats[i][str(p + 1)]]
+                    e["total_simulations"] += a.agent.stats["iterations_run"]
+                    e["moves_with_simulations"] += 1
             # place the search moves (Board.place_piece, engine/board.py:515-555), all games
             # of the round at once; the frontier tables per game (CPython set order)
             th = time.perf_counter()
@@ -566,6 +593,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
         active = np.array([i for i in active if results[i] is None], dtype=np.int64)
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
+    # (the MCTS launches overlap the FastMCTS phase: host_s is what neither covers)
     prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"]
     if prof["uncertified_heuristic"]:
         warnings.warn(f"run_games_batched: {prof['uncertified_heuristic']} HeuristicAgent draw(s) fell within 2^-40 "
