@@ -1443,12 +1443,14 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 // place_frontier on the DMA stage (stage_q = pair q's slot 0; mask / fill / used as
 // loaded): the ops in LDS, then the table (or, RECOPY, its copy) written to fl.  Falls
 // back to the global table when the ops outgrow the stage.
-template <bool RECOPY>
+// RUN_U4: uint4 distance between 16-slot runs (k_mcts_pair's pair stage: 64; the
+// cooperative kernels' one-per-wave stage, a plain array: 2)
+template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4>
 __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* stage_q, const uint64_t* htab,
                                                    const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
     uint16_t m = gfs->mask[p], f = gfs->fill[p], u = gfs->used[p];
-    FsetRef t{stage_q, DMA_RUN_I16, &m, &f, &u, 16u * DMA_RUNS, htab, 4};
+    FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4};
     if (fs_run_ops(t, fl->tmp, cells, real)) {
         bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
         const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(stage_q);
@@ -1457,8 +1459,8 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
 #pragma unroll
             for (int r = 0; r < DMA_RUNS; ++r) {
                 if ((uint32_t)(16 * r) <= m) {
-                    dst4[2 * r] = src4[r * (DMA_RUN_DWORDS / 4)];
-                    dst4[2 * r + 1] = src4[r * (DMA_RUN_DWORDS / 4) + 1];
+                    dst4[2 * r] = src4[r * RUN_U4];
+                    dst4[2 * r + 1] = src4[r * RUN_U4 + 1];
                 }
             }
             gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
@@ -1472,7 +1474,7 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
         int16_t* dk = gfs->key[p];
 #pragma unroll 1
         for (uint32_t i = 0; i <= m; i += 8) {
-            const uint4 v = src4[(i >> 4) * (DMA_RUN_DWORDS / 4) + ((i >> 3) & 1u)];
+            const uint4 v = src4[(i >> 4) * RUN_U4 + ((i >> 3) & 1u)];
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -2712,7 +2714,7 @@ __device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&p
 // RECOPY: the table then becomes its Board.copy() in place (expansion and replay edges:
 // node boards are copies).
 // stage_q (k_mcts_pair): the mover's table is already in the LDS-DMA stage at stage_q.
-template <bool RECOPY>
+template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4>
 __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
                                                 const uint64_t* htab, const uint32_t (&pm)[5],
                                                 const int32_t (&cells)[5], uint64_t real, int16_t* lk,
@@ -2726,7 +2728,7 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
             slab.at(4, ar + d) |= pm[d];
         }
     }
-    const bool ok = stage_q ? place_frontier_dma<RECOPY>(T, p, stage_q, htab, cells, real)
+    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real)
                             : place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
@@ -3539,6 +3541,9 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
     __shared__ __attribute__((aligned(16))) uint32_t lds[COOP_AREA * COOP_WAVES + 2 * BK_CELLS + HS_WORDS];
     __shared__ int16_t coop_rank[COOP_WAVES][448];  // coop_walk: slot of each frontier key
+    // the mover's table (<= 128 slots), one copy per wave, loaded by LDS-DMA while the
+    // orientations are evaluated: locate / walk read it and the set operations run on it
+    __shared__ __attribute__((aligned(16))) int16_t coop_stage[COOP_WAVES][16 * DMA_RUNS];
     const bool coop_walk_on = a.coop_walk != 0;
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint32_t* my = lds + wv * COOP_AREA;
@@ -3587,6 +3592,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         }
         // ---- one movegen, split over the lanes
         const int p = m.mode == MC_EXPAND ? ((m.root_player + m.depth) & 3) : m.cur;
+        const uint32_t tmask = L->A.s.mask[p];  // (loaded with the slab rows)
         Planes P;
         {
             uint32_t own[20], occ[20];
@@ -3599,6 +3605,12 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         }
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
+        const bool staged = tmask < 16u * DMA_RUNS;  // uniform: one search per wave
+        if (staged) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the table's last stores have landed
+            if (lane < 16)  // 16 lanes x 16 bytes = the 128-slot table
+                __builtin_amdgcn_global_load_lds((const void*)(L->A.s.key[p] + 8 * lane), (void*)coop_stage[wv], 16, 0, 0);
+        }
         const uint32_t avail = ~m.used.get(p) & 0x1FFFFFu;
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         // Board.move_count of the rollout board: placements on the way from the root
@@ -3658,6 +3670,8 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             gs = coop_find(sc, k, kk);
         }
         FsLane* T = &L->A;  // the node board at expansion, the rollout's sim board after it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
+        const int16_t* tkey = staged ? coop_stage[wv] : T->s.key[p];
         int ar, ac;
         SECT(3);
         int16_t* rank = coop_rank[wv];
@@ -3668,24 +3682,24 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             } else if (coop_walk_on) {
 #pragma unroll
                 for (int r = 0; r < 20; ++r) rows_lds[r * WAVE].y = h_ok[r];
-                if (!coop_walk<true>(gs, 0u, rows_lds, T->s.key[p], T->s.mask[p], rank, lane, hs, edge_w, h_target,
+                if (!coop_walk<true>(gs, 0u, rows_lds, tkey, (int)tmask, rank, lane, hs, edge_w, h_target,
                                      h_R, h_total, ar, ac, h_unc))
-                    heur_walk_frontier(gs, h_ok, rows_lds, T->s.key[p], T->s.mask[p], hs, edge_w, h_target, h_R,
+                    heur_walk_frontier(gs, h_ok, rows_lds, tkey, (int)tmask, hs, edge_w, h_target, h_R,
                                        h_total, ar, ac, h_unc);
             } else {
-                heur_walk_frontier(gs, h_ok, rows_lds, T->s.key[p], T->s.mask[p], hs, edge_w, h_target, h_R, h_total,
+                heur_walk_frontier(gs, h_ok, rows_lds, tkey, (int)tmask, hs, edge_w, h_target, h_R, h_total,
                                    ar, ac, h_unc);
             }
             if (h_unc) m.status |= BK_MCTS_EUNCERT;
         } else {
             bool walked = false;
-            if (coop_walk_on && T->s.mask[p] <= 2 * WAVE - 1) {
+            if (coop_walk_on && tmask <= 2 * WAVE - 1) {
                 bool unc_unused = false;
                 locate_pass1(gs, rows_lds);
-                walked = coop_walk<false>(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], rank, lane, hs, 0, 0.0, 0.0,
+                walked = coop_walk<false>(gs, kk, rows_lds, tkey, (int)tmask, rank, lane, hs, 0, 0.0, 0.0,
                                           0.0, ar, ac, unc_unused);
             }
-            if (!walked) locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
+            if (!walked) locate_move_frontier(gs, kk, rows_lds, tkey, (int)tmask, ar, ac);
         }
         if (ar < 0) {  // the table does not list the move: counts and tables disagree
             m.status |= BK_MCTS_EINTERNAL;
@@ -3713,8 +3727,9 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             pool[c] = ch;
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
         }
-        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
-        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk);
+        int16_t* sq = staged ? coop_stage[wv] : nullptr;
+        if (expand) ok &= mc_place_staged<true, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
+        else ok &= mc_place_staged<false, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
         if (expand) {
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
