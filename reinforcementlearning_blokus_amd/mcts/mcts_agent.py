@@ -97,6 +97,39 @@ def _search_on_device(gpu, ags, rts, sts, pl, rh, zob, zidx, mt, iters, max_roll
             "hit_flags": d_flags.cpu().numpy()}
 
 
+_MT_VIEWS_OK: Optional[bool] = None
+
+
+def _mt_view(rng) -> Optional[np.ndarray]:
+    """uint32[625] view of a numpy RandomState's MT19937 key[624] + pos (the bit
+    generator's C state), so search_packed moves 500 agents' rollout streams without 500
+    get_state / set_state round trips (~50 us each); the Gaussian cache stays untouched,
+    as set_state((.., key, pos, has_gauss, gauss)) with the old has_gauss leaves it.
+    None if this numpy's layout does not match get_state (checked once)."""
+    global _MT_VIEWS_OK
+    import ctypes
+
+    def view(r):
+        addr = r._bit_generator.ctypes.state_address
+        return np.ctypeslib.as_array(ctypes.cast(addr, ctypes.POINTER(ctypes.c_uint32)), shape=(625,))
+
+    if _MT_VIEWS_OK is None:
+        try:
+            probe = np.random.RandomState(20260301)
+            probe.random_sample(700)  # past a twist
+            v, st = view(probe), probe.get_state()
+            ok = np.array_equal(v[:624], st[1]) and int(v[624]) == st[2]
+            v[:624] = np.arange(624, dtype=np.uint32)
+            v[624] = 7
+            st = probe.get_state()
+            _MT_VIEWS_OK = bool(ok and np.array_equal(st[1], np.arange(624)) and st[2] == 7)
+        except Exception:  # noqa: BLE001 -- any other numpy: fall back to get_state
+            _MT_VIEWS_OK = False
+    if not _MT_VIEWS_OK or type(rng) is not np.random.RandomState:
+        return None
+    return view(rng)
+
+
 def _search_policy(agent) -> Optional[int]:
     """bk_mcts rollout policy replaying this rollout agent on the GPU, or None:
     RandomAgent, or HeuristicAgent with the reference's default weights (the kernel's
@@ -324,11 +357,16 @@ class MCTSAgent:
                 zidx.append(len(tabs) - 1)
             zob = np.stack(tabs)
             rh = hash_states(rts, zob)  # one table per search
-            mt = np.zeros((len(idx), 625), np.uint32)
-            rng_states = [a.rollout_agent.rng.get_state() for a in ags]
-            for j, st in enumerate(rng_states):
-                mt[j, :624] = st[1]
-                mt[j, 624] = st[2]
+            views = [_mt_view(a.rollout_agent.rng) for a in ags]
+            if all(v is not None for v in views):
+                mt = np.stack(views)  # a copy: the kernel advances it, written back below
+                rng_states = None
+            else:
+                mt = np.zeros((len(idx), 625), np.uint32)
+                rng_states = [a.rollout_agent.rng.get_state() for a in ags]
+                for j, st in enumerate(rng_states):
+                    mt[j, :624] = st[1]
+                    mt[j, 624] = st[2]
             t0 = time.time()
             r = _search_on_device(gpu, ags, rts, sts, pl, rh, zob, np.array(zidx, np.int32), mt, iters, max_roll, c,
                                   use_tt, tl_us, policy)
@@ -341,8 +379,11 @@ class MCTSAgent:
             f_it, f_hits, f_roll = ro["iterations_run"].tolist(), ro["tt_hits"].tolist(), ro["rollouts"].tolist()
             f_status, f_best = ro["status"].tolist(), ro["best_move"].tolist()
             for j, (i, a) in enumerate(zip(idx, ags)):
-                st = rng_states[j]
-                a.rollout_agent.rng.set_state((st[0], mt[j, :624].copy(), int(mt[j, 624]), st[3], st[4]))
+                if rng_states is None:
+                    views[j][:] = mt[j]
+                else:
+                    st = rng_states[j]
+                    a.rollout_agent.rng.set_state((st[0], mt[j, :624].copy(), int(mt[j, 624]), st[3], st[4]))
                 n_it = f_it[j]
                 hits = r["hit_flags"][j, :n_it]
                 rew = r["rewards"][j, :n_it]

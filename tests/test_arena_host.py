@@ -88,3 +88,29 @@ def test_wall_clock_fastmcts_seat_plays_in_host_loop(kind, tmp_path, monkeypatch
         {"name": "f", "type": kind, "thinking_time_ms": 20}]))
     seats2 = seat_assignment_for_game(cfg2.agent_names, 0, game_seed_from_run_seed(5, 0), "round_robin")
     assert runner._batchable(cfg2, seats2)
+
+
+def test_mt_state_views_match_get_state():
+    """search_packed moves rollout streams through direct views of numpy's MT19937 state
+    (mcts_agent._mt_view): a view reads what get_state returns and a write through it is
+    what set_state would leave, Gaussian cache included."""
+    import numpy as np
+
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import _mt_view
+    r = np.random.RandomState(99)
+    r.standard_normal()  # has_gauss set
+    r.random_sample(1000)
+    v = _mt_view(r)
+    assert v is not None
+    st = r.get_state()
+    assert np.array_equal(v[:624], st[1]) and int(v[624]) == st[2]
+    ref = np.random.RandomState(0)
+    ref.set_state(st)
+    nxt = np.random.RandomState(5).get_state()
+    v[:624] = nxt[1]
+    v[624] = nxt[2]
+    ref.set_state((st[0], nxt[1], nxt[2], st[3], st[4]))
+    assert r.get_state()[1].tolist() == ref.get_state()[1].tolist()
+    assert r.get_state()[2:] == ref.get_state()[2:]
+    assert r.randint(0, 1000, size=50).tolist() == ref.randint(0, 1000, size=50).tolist()
+    assert r.standard_normal() == ref.standard_normal()
