@@ -375,6 +375,11 @@ class MCTSAgent:
             SEARCH_TOTALS["kernel_ms"] += gpu.last_kernel_ms()
             SEARCH_TOTALS["sims"] += int(r["out"]["iterations_run"].sum())
             SEARCH_TOTALS["rollout_plies"] += int(r["out"]["rollout_plies"].astype(np.int64).sum())
+            # the non-hit rewards of every search as Python lists in one pass (NaN marks a
+            # TT hit or an iteration past the search's end: rewards are finite)
+            its = np.arange(r["rewards"].shape[1])[None, :]
+            live = (r["hit_flags"] == 0) & (its < r["out"]["iterations_run"][:, None])
+            rew_rows = np.where(live, r["rewards"], np.nan).tolist()
             ro = r["out"]  # per-search fields as Python ints (structured-scalar access is slow)
             f_it, f_hits, f_roll = ro["iterations_run"].tolist(), ro["tt_hits"].tolist(), ro["rollouts"].tolist()
             f_status, f_best = ro["status"].tolist(), ro["best_move"].tolist()
@@ -385,8 +390,6 @@ class MCTSAgent:
                     st = rng_states[j]
                     a.rollout_agent.rng.set_state((st[0], mt[j, :624].copy(), int(mt[j, 624]), st[3], st[4]))
                 n_it = f_it[j]
-                hits = r["hit_flags"][j, :n_it]
-                rew = r["rewards"][j, :n_it]
                 a.stats["iterations_run"] = n_it
                 # HeuristicAgent rollouts: a draw within 2^-40 of a probability boundary
                 # (BK_MCTS_EUNCERT; the kernel flags the search, it does not count draws)
@@ -401,7 +404,7 @@ class MCTSAgent:
                                       "bound before the time ran out", RuntimeWarning, stacklevel=2)
                 a.stats["time_elapsed"] = dt
                 a.stats["transposition_hits"] += f_hits[j]
-                a.stats["rollout_rewards"].extend(rew[hits == 0].tolist())
+                a.stats["rollout_rewards"].extend([x for x in rew_rows[j] if x == x])
                 if use_tt:
                     t = a.transposition_table
                     t.access_count += f_hits[j] + f_roll[j]
