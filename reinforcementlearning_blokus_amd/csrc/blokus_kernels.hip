@@ -3063,6 +3063,9 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         // replay and backpropagation of one lane cost the whole wave about one ply, so
         // batching them beats letting every finished rollout stall the other 63 lanes.
         // Lanes play independent searches: the order changes no result.
+        // PAIR: the tree phase stages tables in LDS over the DMA stage, so no DMA of the
+        // previous step may still be landing (a step that ended before locate never waited)
+        if constexpr (PAIR) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint64_t waiting = __ballot(!done && m.mode == MC_SELECT);
         const bool tree_now = __popcll(waiting) >= a.tree_batch || __ballot(!done && m.mode != MC_SELECT) == 0ull;
         while (tree_now && !done && m.mode == MC_SELECT) {
