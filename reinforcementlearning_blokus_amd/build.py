@@ -40,6 +40,44 @@ def built_hash():
         return None
 
 
+# translation units of csrc/blokus_kernels.hip (its BK_U_* numbers): the C-ABI host code,
+# then one unit per kernel family, compiled in parallel and linked into one .so
+UNITS = {"host": 1, "movegen": 2, "rollout": 3, "rollout_fr": 4, "rollout_frh": 5, "fastmcts": 6,
+         "mcts": 7, "mcts_pair": 8, "mcts_h": 9, "coop": 10, "coop_h": 11}
+
+
+def compile_library(out: str, defines=(), verbose: bool = True, jobs: int = 0) -> str:
+    """Compile every unit of csrc/blokus_kernels.hip with hipcc (gfx950) in parallel and
+    link them into `out` (one fat binary per kernel unit; kernels are launched from the
+    host unit through their host stubs)."""
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = out + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-pthread",
+            "-Wno-unused-command-line-argument"] + [f"-D{d}" for d in defines]
+
+    def unit(item):
+        name, u = item
+        obj = os.path.join(objdir, name + ".o")
+        cmd = base + [f"-DBK_TU={u}"]
+        cmd += ["-c", "-o", obj, SRC]
+        if verbose:
+            print("[build] " + " ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+        return obj
+
+    jobs = jobs or min(len(UNITS), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 4))
+    with ThreadPoolExecutor(max(1, jobs)) as ex:
+        objs = list(ex.map(unit, sorted(UNITS.items(), key=lambda kv: kv[1])))
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", out + ".tmp"] + objs
+    if verbose:
+        print("[build] " + " ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    shutil.rmtree(objdir, ignore_errors=True)
+    return out
+
+
 def build_native(force: bool = True, verbose: bool = True) -> str:
     """Compile libblokus_hip.so for gfx950 with hipcc.  Always compiles by default (the
     driver's build() check must exercise hipcc); force=False reuses an in-tree .so only
@@ -49,13 +87,8 @@ def build_native(force: bool = True, verbose: bool = True) -> str:
             print(f"[build] reusing {OUT} (built from sources {built_hash()[:12]})", flush=True)
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-pthread", "-Wno-unused-command-line-argument", "-o", OUT + ".tmp", SRC]
-    if verbose:
-        print("[build] " + " ".join(cmd), flush=True)
     digest = source_hash()
-    subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
+    compile_library(OUT, verbose=verbose)
     with open(HASH_FILE, "w") as f:
         f.write(digest + "\n")
     return OUT

@@ -47,12 +47,47 @@
 
 #define BK_TABLES_VERSION 1
 
+// Translation units.  build.py compiles this file once per unit, in parallel: -DBK_TU=u
+// defines unit u's kernels (the other kernels are only declared), BK_U_HOST the C-ABI
+// (host code only, --offload-host-only).  Without BK_TU (a one-shot build) the file
+// defines everything.  Device templates are instantiated only in the units that use them.
+#define BK_U_HOST 1
+#define BK_U_MOVEGEN 2
+#define BK_U_ROLLOUT 3
+#define BK_U_ROLLOUT_FR 4
+#define BK_U_ROLLOUT_FRH 5
+#define BK_U_FASTMCTS 6
+#define BK_U_MCTS 7
+#define BK_U_MCTS_PAIR 8
+#define BK_U_MCTS_H 9
+#define BK_U_COOP 10
+#define BK_U_COOP_H 11
+#ifndef BK_TU
+#define BK_TU 0
+#endif
+#define BK_DEF(u) (BK_TU == 0 || BK_TU == (u))
+
 // Section timers (diagnostic build only, -DBK_SECTION_PROF): per-wave shader-clock
 // cycles spent in each section of a kernel's loop, summed over waves into
-// g_sections[] (read with bk_debug_sections).  Compiled out of the product build.
+// g_sections[] (read with bk_debug_sections: every unit registers a reader of its own
+// copy, and the reads are summed).  Compiled out of the product build.
 #define BK_NSECT 16
 #ifdef BK_SECTION_PROF
-__device__ unsigned long long g_sections[BK_NSECT];
+static __device__ unsigned long long g_sections[BK_NSECT];
+void bk_register_sections(int (*rd)(unsigned long long*, int));
+#if BK_TU != BK_U_HOST
+static int bk_read_sections(unsigned long long* v, int reset) {
+    unsigned long long t[BK_NSECT];
+    if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_sections), sizeof t) != hipSuccess) return -1;
+    for (int i = 0; i < BK_NSECT; ++i) v[i] += t[i];
+    if (reset) {
+        memset(t, 0, sizeof t);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sections), t, sizeof t) != hipSuccess) return -1;
+    }
+    return 0;
+}
+static const int bk_sections_registered = (bk_register_sections(bk_read_sections), 0);
+#endif
 #define SECT_DECL uint64_t sect_acc[BK_NSECT] = {0}; uint64_t sect_t = clock64();
 #define SECT(i) do { const uint64_t now_ = clock64(); sect_acc[i] += now_ - sect_t; sect_t = now_; } while (0)
 #define SECT_FLUSH do { if ((threadIdx.x & (WAVE - 1)) == 0) for (int i_ = 0; i_ < BK_NSECT; ++i_) \
@@ -921,6 +956,7 @@ __device__ __forceinline__ void rows_class_group(int i0, int i1, int grp, int G,
 // atomicAdd per (board-player, group) into the zeroed out_count.
 #define MG_GROUPS_MAX 91
 #define MG_GROUPS_DEFAULT_MAX 32
+#if BK_DEF(BK_U_MOVEGEN)
 __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
     const int G = a.groups;
     const int grp = blockIdx.x % G;
@@ -966,6 +1002,9 @@ __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
 #undef BK_ROWS_GROUP
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
 }
+#else
+__global__ void k_movegen_g(MovegenArgs a);
+#endif
 
 // k_movegen_g with the SURVEY 8(b) output: each orientation's legal anchors as one
 // 400-bit mask (7 u64, bit 20 r + c, the reference's player_bits numbering), 5,096 B per
@@ -975,6 +1014,7 @@ __global__ __launch_bounds__(WAVE) void k_movegen_g(MovegenArgs a) {
 // XCD's L2 (not once per XCD) and the partial 128-B lines of one board's mask, written by
 // different group waves, merge in the same L2.
 #define MG_XCDS 8
+#if BK_DEF(BK_U_MOVEGEN)
 __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
     const int G = a.groups;
     const int xcd = blockIdx.x % MG_XCDS, j = blockIdx.x / MG_XCDS;
@@ -1025,7 +1065,11 @@ __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
     }
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
 }
+#else
+__global__ void k_movegen_m(MovegenArgs a);
+#endif
 
+#if BK_DEF(BK_U_MOVEGEN)
 __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
     const int lane = threadIdx.x & (WAVE - 1);
     const int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1054,6 +1098,9 @@ __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
     }
     if (live) a.out_mask4[i] = mask;
 }
+#else
+__global__ void k_has_moves(MovegenArgs a);
+#endif
 
 // ------------------------------------------------------------------------------------
 // Frontier sets: CPython 3.10 set of (row, col) tuples, restated for the reference's
@@ -2372,12 +2419,28 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
 
 // Two entry points over one body so profiles separate root generation (bk_advance)
 // from the measured playouts (bk_rollout).
+#if BK_DEF(BK_U_ROLLOUT)
 __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_rollout(RolloutArgs a) { rollout_body<false>(a); }
+#else
+__global__ void k_rollout(RolloutArgs a);
+#endif
+#if BK_DEF(BK_U_ROLLOUT)
 __global__ __launch_bounds__(BLOCK, ROLL_BLOCKS_PER_CU) void k_advance(RolloutArgs a) { rollout_body<false>(a); }
+#else
+__global__ void k_advance(RolloutArgs a);
+#endif
 // reference frontier order (compat parity mode)
+#if BK_DEF(BK_U_ROLLOUT_FR)
 __global__ __launch_bounds__(BLOCK, FR_BLOCKS_PER_CU) void k_rollout_fr(RolloutArgs a) { rollout_body<true>(a); }
+#else
+__global__ void k_rollout_fr(RolloutArgs a);
+#endif
 // reference frontier order with HeuristicAgent seats (cfg.heuristic_seats)
+#if BK_DEF(BK_U_ROLLOUT_FRH)
 __global__ __launch_bounds__(HBLOCK, 2) void k_rollout_fr_h(RolloutArgs a) { rollout_body<true, true>(a); }
+#else
+__global__ void k_rollout_fr_h(RolloutArgs a);
+#endif
 
 // ------------------------------------------------------------------------------------
 // FastMCTS simulate loop (agents/fast_mcts_agent.py:153-256): one wave per game
@@ -2489,6 +2552,7 @@ struct FastMctsArgs {
     uint32_t* err;
 };
 
+#if BK_DEF(BK_U_FASTMCTS)
 __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
     __shared__ uint32_t visits[BK_FASTMCTS_MAX_CHILDREN];
     __shared__ double total[BK_FASTMCTS_MAX_CHILDREN];
@@ -2567,13 +2631,21 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
     }
     if (lane == 0) o->n_top = ntop;
 }
+#else
+__global__ void k_fastmcts(FastMctsArgs a);
+#endif
 
 // bk_debug_fastmcts_select: one selection step of k_fastmcts on given child stats
+#if BK_DEF(BK_U_FASTMCTS)
 __global__ __launch_bounds__(WAVE) void k_fastmcts_select(const uint32_t* visits, const double* totals, int n,
                                                           uint32_t N, double L2, double c, PowFix fx, int32_t* out) {
     const int j = fm_select(visits, totals, n, threadIdx.x, L2, N, c, fx);
     if (threadIdx.x == 0) *out = j;
 }
+#else
+__global__ void k_fastmcts_select(const uint32_t* visits, const double* totals, int n, uint32_t N, double L2, double c,
+                                  PowFix fx, int32_t* out);
+#endif
 
 // ------------------------------------------------------------------------------------
 // MCTSAgent searches (mcts/mcts_agent.py:19-582) with RandomAgent rollouts: one lane =
@@ -3287,9 +3359,21 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
     SECT_FLUSH;
 }
 
+#if BK_DEF(BK_U_MCTS)
 __global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
+#else
+__global__ void k_mcts(MctsArgs a);
+#endif
+#if BK_DEF(BK_U_MCTS_PAIR)
 __global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts_pair(MctsArgs a) { mcts_body<false, true>(a); }
+#else
+__global__ void k_mcts_pair(MctsArgs a);
+#endif
+#if BK_DEF(BK_U_MCTS_H)
 __global__ __launch_bounds__(HBLOCK, 2) void k_mcts_h(MctsArgs a) { mcts_body<true>(a); }
+#else
+__global__ void k_mcts_h(MctsArgs a);
+#endif
 
 // ------------------------------------------------------------------------------------
 // Cooperative MCTSAgent searches: ONE 64-lane wave per search, for batches too small to
@@ -3760,10 +3844,19 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     SECT_FLUSH;
 }
 
+#if BK_DEF(BK_U_COOP)
 __global__ __launch_bounds__(COOP_WAVES * WAVE) void k_mcts_coop(MctsArgs a) { mcts_coop_body<false>(a); }
+#else
+__global__ void k_mcts_coop(MctsArgs a);
+#endif
+#if BK_DEF(BK_U_COOP_H)
 __global__ __launch_bounds__(COOP_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(COOP_H_WAVES_PER_SIMD)))
 void k_mcts_coop_h(MctsArgs a) { mcts_coop_body<true>(a); }
+#else
+__global__ void k_mcts_coop_h(MctsArgs a);
+#endif
 
+#if BK_DEF(BK_U_HOST)
 // ------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------
@@ -3791,6 +3884,14 @@ struct bk_handle_s {
     int mcts_blocks_per_cu = 0;  // k_mcts
     const char* last_kernel = "";  // name of the kernel the last timed call launched
 };
+
+#ifdef BK_SECTION_PROF
+static std::vector<int (*)(unsigned long long*, int)>& sect_readers() {
+    static std::vector<int (*)(unsigned long long*, int)> v;
+    return v;
+}
+void bk_register_sections(int (*rd)(unsigned long long*, int)) { sect_readers().push_back(rd); }
+#endif
 
 static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
     if (h) snprintf(h->err, sizeof h->err, fmt, detail ? detail : "");
@@ -3921,13 +4022,10 @@ int bk_debug_sections(bk_handle h, uint64_t* out, int32_t n, int32_t reset) {
 #ifdef BK_SECTION_PROF
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, hipStreamSynchronize(h->cur));
-    unsigned long long v[BK_NSECT];
-    HIPCHK(h, hipMemcpyFromSymbol(v, HIP_SYMBOL(g_sections), sizeof v));
+    unsigned long long v[BK_NSECT] = {0};
+    for (auto rd : sect_readers())  // every unit's own counters, summed
+        if (rd(v, reset) != 0) return set_err(h, BK_EHIP, "bk_debug_sections: counter copy failed%s", "");
     for (int i = 0; i < n; ++i) out[i] = i < BK_NSECT ? (uint64_t)v[i] : 0u;
-    if (reset) {
-        memset(v, 0, sizeof v);
-        HIPCHK(h, hipMemcpyToSymbol(HIP_SYMBOL(g_sections), v, sizeof v));
-    }
     return BK_OK;
 #else
     (void)reset;
@@ -4679,3 +4777,4 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
 }
 
 }  // extern "C"
+#endif  // BK_DEF(BK_U_HOST)

@@ -26,8 +26,7 @@ def build():
     sys.path.insert(0, ROOT)
     from reinforcementlearning_blokus_amd import build as B
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call([B.hipcc(), f"--offload-arch={B.ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread",
-                           "-DBK_SECTION_PROF", "-Wno-unused-command-line-argument", "-o", LIB, B.SRC])
+    B.compile_library(LIB, defines=("BK_SECTION_PROF",))
     print(LIB)
 
 
