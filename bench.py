@@ -280,35 +280,40 @@ def run_config3(args, world, rank, local, dist):
     from reinforcementlearning_blokus_amd import _native as N
     from reinforcementlearning_blokus_amd.gpu import BlokusGPU, empty_state
 
+    from reinforcementlearning_blokus_amd.workloads import Config3Plan
     games = args.games or 256
     gpu = BlokusGPU(local)
     dev = torch.device("cuda", local)
-    seed = args.seed + 1_000_003 * rank
+    # every stream is a function of the global game index: rank r plays global games
+    # r * games .. (r + 1) * games - 1 (workloads.Config3Plan), so the N-rank job's
+    # gathered records equal a 1-rank run of the same N * games games
+    plan = Config3Plan(args.seed, games, args.rollouts, rank)
     # synthetic mid-game roots, generated on the GPU (BK_SEM_ADVANCE from the empty board)
     if args.order == "frontier":
         roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), games,
-                                                 semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=seed,
+                                                 semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=plan.seed,
                                                  max_plies=args.root_plies,
-                                                 root_index=np.zeros(games, dtype=np.int32))
+                                                 root_index=np.zeros(games, dtype=np.int32),
+                                                 stream_base=plan.root_stream_base)
         sets = torch.from_numpy(sets_np.view(np.uint8).reshape(games, -1).copy()).to(dev)
     else:
-        roots_np = gpu.advance(empty_state(), games, args.root_plies, seed=seed,
-                               root_index=np.zeros(games, dtype=np.int32))
+        roots_np = gpu.advance(empty_state(), games, args.root_plies, seed=plan.seed,
+                               root_index=np.zeros(games, dtype=np.int32), stream_base=plan.root_stream_base)
     roots = torch.from_numpy(roots_np.view(np.uint8).reshape(games, 256)).to(dev)
-    n = games * args.rollouts
+    n = plan.n_playouts
     # game j's rollouts are contiguous (one wave plays 64 rollouts of the same game)
-    idx = torch.arange(n, dtype=torch.int32, device=dev) // args.rollouts
+    idx = torch.from_numpy(plan.root_index()).to(dev)
     out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     stream = torch.cuda.Stream(dev)  # our kernels and the timing events share this stream
     plies_acc = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def step(k):
         if args.order == "frontier":
-            gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k,
-                                 root_index=idx, out=out)
+            gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k),
+                                 root_index=idx, out=out, stream_base=plan.playout_stream_base)
         else:
-            gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=seed * 7919 + k, root_index=idx,
-                        out=out)
+            gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k), root_index=idx,
+                        out=out, stream_base=plan.playout_stream_base)
 
     def count_plies():
         plies_acc.add_(out[:, 10:12].contiguous().view(torch.int16).to(torch.int64).sum())
@@ -333,9 +338,9 @@ def run_config3(args, world, rank, local, dist):
     elapsed, (sims, all_plies) = reduce_max_sum(dist, dev, elapsed, [n * args.steps, int(plies_acc.item())])
     if dist:
         # RCCL gather of the last step's terminal results (32 B per playout) over xGMI,
-        # outside the timed region; rank r's playouts are global games r (mod W)
-        from reinforcementlearning_blokus_amd.shard import gather_results
-        gather_results(out, n * world, rank, world, dist)
+        # outside the timed region; rank r's playouts are the global block r
+        from reinforcementlearning_blokus_amd.shard import gather_blocks
+        gather_blocks(out, rank, world, dist)
     value = sims / elapsed
     if rank != 0:
         return None
@@ -360,7 +365,7 @@ def run_config3(args, world, rank, local, dist):
     }
     if not args.no_cpu_baseline and world == 1:
         cb = cpu_baseline_playouts(roots_np, args.cpu_seconds, args.order, args.rollouts,
-                                   seed=seed * 7919 + 1000 + args.steps - 1, gpu_out=out)
+                                   seed=plan.step_seed(1000 + args.steps - 1), gpu_out=out)
         cb["gpu_over_cpu"] = value / cb["value"]
         cb["reference_python"] = ref_python(value, REF_PY_ARENA_SIMS_PER_CORE, cb["cores"],
                                             "terminal random playout from ply 20, telemetry off")
@@ -728,18 +733,23 @@ def cpu_baseline_movegen(st, pl, seconds, value):
 
 
 def run_selftest(args, world, rank, local, dist):
-    """CPU check of the N-rank path with gloo (no GPU, no kernels): every rank takes its
-    shard of a config-3-sized job's game indices (shard.shard_indices), makes each
-    game's 32-byte record from the same per-game quantities the GPU path derives from
-    the global index (root seed, arena agent seeds, MctsBatch zobrist table / rollout
-    stream seed / MT state), all-gathers them with shard.gather_results, and rank 0
-    checks the result equals one process making every record."""
+    """CPU check of the N-rank path with gloo (no GPU, no kernels), on the same shard /
+    seed / gather code the GPU workloads run:
+    * config 3 (weak scaling): every rank takes its Config3Plan (the global games, root
+      streams and playout streams run_config3 launches with), makes each local playout's
+      32-byte record from them, and all-gathers the blocks with shard.gather_blocks;
+    * configs 4/5 (a fixed job split r mod W): every rank takes its shard of the game
+      indices (shard.shard_indices), makes each game's record from the per-game inputs the
+      GPU path derives from the global index (MctsBatch zobrist table, rollout MT state),
+      and all-gathers them with shard.gather_results.
+    Rank 0 checks both against one process making every record of the whole job."""
     import numpy as np
     import torch
 
-    from reinforcementlearning_blokus_amd.shard import gather_results, shard_indices
-    from reinforcementlearning_blokus_amd.workloads import mcts_game_inputs
+    from reinforcementlearning_blokus_amd.shard import gather_blocks, gather_results, shard_indices
+    from reinforcementlearning_blokus_amd.workloads import Config3Plan, mcts_game_inputs
     total = args.games or 1001  # odd: shards of unequal size
+    c3_games, c3_rollouts = 5, 7
 
     def records(idx):
         idx = np.asarray(idx, dtype=np.int64)
@@ -753,18 +763,36 @@ def run_selftest(args, world, rank, local, dist):
         w[:, 7] = np.bitwise_xor.reduce(mt[:, :624], axis=1)
         return rec
 
+    def c3_records(plan, step):
+        """What bk_rollout keys each local playout by: its Philox stream id and key, and
+        the stream of its root (bk_advance) -- all as run_config3 passes them."""
+        rec = np.zeros((plan.n_playouts, 32), np.uint8)
+        w = rec.view(np.uint32)
+        w[:, 0] = plan.global_playouts()
+        w[:, 1] = plan.root_index() + plan.root_stream_base  # the root's Philox stream = global game
+        key = plan.step_seed(step)
+        w[:, 2], w[:, 3] = key & 0xFFFFFFFF, key >> 32
+        w[:, 4] = plan.seed
+        return rec
+
     if os.environ.get("BENCH_SELFTEST_FAIL_RANK") == str(rank):  # failure injection (tests)
         raise SystemExit(3)
     mine = shard_indices(total, rank, world)
     got = gather_results(torch.from_numpy(records(mine)), total, rank, world, dist) if dist else \
         torch.from_numpy(records(mine))
+    plan = Config3Plan(args.seed, c3_games, c3_rollouts, rank)
+    c3 = torch.from_numpy(c3_records(plan, 1000))
+    c3_got = gather_blocks(c3, rank, world, dist) if dist else c3
     if rank != 0:
         return None
-    ok = bool(np.array_equal(got.numpy(), records(range(total))))
-    if not ok:
+    if not np.array_equal(got.numpy(), records(range(total))):
         raise SystemExit("bench.py --selftest: gathered records differ from the one-process records")
+    whole = Config3Plan(args.seed, c3_games * world, c3_rollouts, 0)
+    if not np.array_equal(c3_got.numpy(), c3_records(whole, 1000)):
+        raise SystemExit("bench.py --selftest: gathered config-3 records differ from a one-rank run of the job")
     return {"selftest": "ok", "n_ranks": world, "backend": "gloo" if dist else "none", "games": total,
-            "shard_sizes": [len(shard_indices(total, r, world)) for r in range(world)]}
+            "shard_sizes": [len(shard_indices(total, r, world)) for r in range(world)],
+            "config3": {"games_per_rank": c3_games, "rollouts": c3_rollouts, "job_playouts": whole.n_playouts}}
 
 
 def main():

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 3
+#define BK_ABI_VERSION 4
 #define BK_BOARD 20
 #define BK_CELLS 400
 #define BK_PLAYERS 4
@@ -95,6 +95,10 @@ typedef struct bk_rollout_cfg {
                                    :39-244) instead of RandomAgent; BK_ORDER_FRONTIER only.
                                    Its choice is certified exact (result status bit 4 set
                                    otherwise)                               */
+    uint32_t stream_base;       /* BK_RNG_PHILOX: playout i of this call draws from stream
+                                   (seed, stream_base + i), so a job sharded over ranks plays
+                                   the games of its global playout ids (ABI 4)             */
+    int32_t reserved;
 } bk_rollout_cfg;
 
 /* One playout result: 32 bytes */

@@ -748,15 +748,17 @@ static int quick_eval(const int32_t* legal, int n) { /* _quick_move_evaluation :
     return best;
 }
 
-int or_fastmcts(const or_board* b, int player, int64_t seed, int iterations, int order,
-                int32_t* move, int32_t* nodes, int32_t* top_moves, int32_t* top_visits,
-                double* top_q, int top_cap) {
+/* FastMCTSAgent.think with the agent's random.Random stream m (advanced in place: the
+   agent keeps one stream across its calls, fast_mcts_agent.py:99) */
+int or_fastmcts_mt(const or_board* b, int player, or_mt* mp, int iterations, int order,
+                   int32_t* move, int32_t* nodes, int32_t* top_moves, int32_t* top_visits,
+                   double* top_q, int top_cap) {
     static __thread int32_t legal[BK_ORIENTS * 400];
     int n = or_legal_moves(b, player, order, legal, BK_ORIENTS * 400);
     *nodes = 0;
     if (n == 0) { *move = -1; return 0; }
     if (n == 1) { *move = legal[0]; *nodes = 1; return 0; }
-    or_mt m; py_seed_int(&m, seed);
+#define m (*mp)
     fm_child* ch = (fm_child*)calloc((size_t)n, sizeof(fm_child));
     int nch = 0, untried = n, root_visits = 0;
     const int qm = quick_eval(legal, n);
@@ -801,6 +803,14 @@ int or_fastmcts(const or_board* b, int player, int64_t seed, int iterations, int
     }
     free(idx); free(ch);
     return nch < top_cap ? nch : top_cap;
+#undef m
+}
+
+int or_fastmcts(const or_board* b, int player, int64_t seed, int iterations, int order,
+                int32_t* move, int32_t* nodes, int32_t* top_moves, int32_t* top_visits,
+                double* top_q, int top_cap) {
+    or_mt m; py_seed_int(&m, seed);
+    return or_fastmcts_mt(b, player, &m, iterations, order, move, nodes, top_moves, top_visits, top_q, top_cap);
 }
 
 /* mcts/zobrist.py:41-68 table; :70-99 hash_board */
@@ -965,6 +975,7 @@ static int heur_choice_c(const or_board* b, int p, or_mt* rng, int32_t* scratch,
 
 /* 0: RandomAgent rollouts; 1: HeuristicAgent rollouts (MCTSAgent's default) */
 static __thread int g_rollout_policy = 0;
+void or_set_rollout_policy(int policy) { g_rollout_policy = policy ? 1 : 0; }
 
 static double or_rollout_mt(const or_board* b, int player, or_mt* rng, int max_moves, int32_t* scratch) {
     or_board* sim = (or_board*)malloc(sizeof(or_board));

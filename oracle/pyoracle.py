@@ -93,6 +93,9 @@ def lib():
                                        P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
             "or_fastmcts": (C.c_int, [P(Board), C.c_int, C.c_int64, C.c_int, C.c_int, P(C.c_int32),
                                       P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_double), C.c_int]),
+            "or_fastmcts_mt": (C.c_int, [P(Board), C.c_int, P(MT), C.c_int, C.c_int, P(C.c_int32),
+                                         P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_double), C.c_int]),
+            "or_set_rollout_policy": (None, [C.c_int]),
             "or_zobrist_table": (None, [C.c_int64, P(C.c_uint64)]),
             "or_zobrist_hash": (C.c_uint64, [P(Board), P(C.c_uint64)]),
             "or_batch_playouts": (C.c_int, [P(State), C.c_int, C.c_int, C.c_uint64, C.c_int, C.c_int,
@@ -262,6 +265,32 @@ def fastmcts(b, player, seed, iterations, order=ORDER_FRONTIER, top=10):
     return mv.value, nodes.value, [(tm[i], tv[i], tq[i]) for i in range(k)]
 
 
+def python_mt(seed):
+    """random.Random(seed) (CPython int seeding: init_by_array over the 32-bit words)."""
+    seed = int(seed)
+    words = []
+    x = abs(seed)
+    while True:
+        words.append(x & 0xFFFFFFFF)
+        x >>= 32
+        if not x:
+            break
+    m = MT()
+    key = (C.c_uint32 * len(words))(*words)
+    lib().or_mt_seed_python(C.byref(m), key, len(words))
+    return m
+
+
+def fastmcts_mt(b, player, m, iterations, order=ORDER_FRONTIER):
+    """FastMCTSAgent.think drawing from the agent's persistent random.Random stream m
+    (an MT, advanced in place): the chosen move int (-1: none)."""
+    mv, nodes = C.c_int32(), C.c_int32()
+    tm, tv, tq = _i32(1), _i32(1), (C.c_double * 1)()
+    lib().or_fastmcts_mt(C.byref(b), player, C.byref(m), iterations, order, C.byref(mv), C.byref(nodes),
+                         tm, tv, tq, 1)
+    return mv.value
+
+
 def orient_table():
     out = []
     for g in range(lib().or_num_orients()):
@@ -311,9 +340,10 @@ class TT:
         self.count = 0
 
 
-def mcts(b, player, iterations, exploration, max_rollout, ztab, rng, tt=None, child_cap=4096):
+def mcts(b, player, iterations, exploration, max_rollout, ztab, rng, tt=None, child_cap=4096, heuristic=False):
     """or_mcts: one MCTSAgent search (mcts/mcts_agent.py:304-582) with RandomAgent
-    rollouts drawing from `rng` (an MT, advanced in place).  tt: a TT or None."""
+    rollouts (heuristic=True: HeuristicAgent rollouts, the reference's default) drawing
+    from `rng` (an MT, advanced in place).  tt: a TT or None."""
     log_table = np.zeros(iterations + 2)
     log_table[1:] = np.log(np.arange(1, iterations + 2))
     use_tt = tt is not None
@@ -339,11 +369,13 @@ def mcts(b, player, iterations, exploration, max_rollout, ztab, rng, tt=None, ch
     cm = np.zeros(child_cap, np.int32)
     cv = np.zeros(child_cap, np.int32)
     ct = np.zeros(child_cap)
+    lib().or_set_rollout_policy(1 if heuristic else 0)
     rc = lib().or_mcts(C.byref(b), player, iterations, exploration, max_rollout, log_table.ctypes.data,
                        len(log_table), ztab.ctypes.data, C.byref(rng), int(use_tt), keys.ctypes.data,
                        vals.ctypes.data, cap, C.byref(cnt), C.byref(best), C.byref(hits),
                        rewards.ctypes.data, flags.ctypes.data, cm.ctypes.data, cv.ctypes.data,
                        ct.ctypes.data, child_cap, C.byref(nch))
+    lib().or_set_rollout_policy(0)
     if rc != 0:
         raise RuntimeError(f"or_mcts failed: {rc}")
     if use_tt:

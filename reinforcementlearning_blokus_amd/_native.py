@@ -61,7 +61,8 @@ class BkResult(C.Structure):
 
 class BkRolloutCfg(C.Structure):
     _fields_ = [("semantics", C.c_int32), ("order", C.c_int32), ("rng", C.c_int32), ("max_plies", C.c_int32),
-                ("seed", C.c_uint64), ("seats_share_stream", C.c_int32), ("heuristic_seats", C.c_int32)]
+                ("seed", C.c_uint64), ("seats_share_stream", C.c_int32), ("heuristic_seats", C.c_int32),
+                ("stream_base", C.c_uint32), ("reserved", C.c_int32)]
 
 
 class BkFastMctsOut(C.Structure):
@@ -75,7 +76,7 @@ FASTMCTS_OUT_DTYPE = np.dtype([("best_index", "<i4"), ("iterations", "<i4"), ("n
                                ("n_top", "<i4"), ("top_index", "<i4", (10,)), ("top_visits", "<i4", (10,)),
                                ("top_q", "<f8", (10,))])
 assert FASTMCTS_OUT_DTYPE.itemsize == 176
-assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRolloutCfg) == 32
+assert C.sizeof(BkState) == 256 and C.sizeof(BkResult) == 32 and C.sizeof(BkRolloutCfg) == 40
 
 
 class BkMctsCfg(C.Structure):
@@ -108,7 +109,7 @@ RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("statu
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
 assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
 
-ABI_VERSION = 3  # include/blokus_hip.h BK_ABI_VERSION
+ABI_VERSION = 4  # include/blokus_hip.h BK_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 

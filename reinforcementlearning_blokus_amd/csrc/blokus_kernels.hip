@@ -2156,7 +2156,7 @@ __device__ __forceinline__ uint32_t draw_index(const RolloutArgs& a, Game& g, co
         if (v > rng) v = 0;
     } else {
         do {
-            v = philox_u32(g.pcount++, (uint32_t)g.pid, a.cfg.seed) & mask;
+            v = philox_u32(g.pcount++, (uint32_t)g.pid + a.cfg.stream_base, a.cfg.seed) & mask;
             g.draws++;
         } while (v > rng);
     }
@@ -2178,8 +2178,8 @@ __device__ __forceinline__ double draw_double(const RolloutArgs& a, Game& g, con
         if (ov) g.status |= 1u;
         base[0] = m.i; base[1] = m.a; base[2] = m.b; base[3] = m.c;
     } else {
-        x0 = philox_u32(g.pcount++, (uint32_t)g.pid, a.cfg.seed);
-        x1 = philox_u32(g.pcount++, (uint32_t)g.pid, a.cfg.seed);
+        x0 = philox_u32(g.pcount++, (uint32_t)g.pid + a.cfg.stream_base, a.cfg.seed);
+        x1 = philox_u32(g.pcount++, (uint32_t)g.pid + a.cfg.stream_base, a.cfg.seed);
     }
     g.draws += 2;
     return ((double)(x0 >> 5) * 67108864.0 + (double)(x1 >> 6)) * (1.0 / 9007199254740992.0);

@@ -162,14 +162,16 @@ class BlokusGPU:
     # ------------------------------------------------------------------ rollouts
     def rollout(self, roots, n_playouts: int, *, semantics: int = N.SEM_ARENA, rng: int = N.RNG_PHILOX,
                 seed: int = 0, max_plies: int | None = None, compat_seeds=None, root_index=None,
-                order: int = N.ORDER_NAIVE, seats_share_stream: bool = False, out=None):
+                order: int = N.ORDER_NAIVE, seats_share_stream: bool = False, out=None, stream_base: int = 0):
         """Random playouts from roots (see bk_rollout in include/blokus_hip.h).
 
         Host numpy in -> numpy RESULT_DTYPE out; torch cuda in -> torch uint8 [n,32] out.
+        stream_base: playout i draws from Philox stream (seed, stream_base + i).
         """
         if max_plies is None:
             max_plies = 2500 if semantics == N.SEM_ARENA else 50
-        cfg = N.BkRolloutCfg(semantics, order, rng, max_plies, seed & (2**64 - 1), int(seats_share_stream), 0)
+        cfg = N.BkRolloutCfg(semantics, order, rng, max_plies, seed & (2**64 - 1), int(seats_share_stream), 0,
+                             _stream_base(stream_base, n_playouts))
         if _is_torch(roots):
             import torch
             dev = roots.device
@@ -197,7 +199,8 @@ class BlokusGPU:
     def rollout_frontier(self, roots, root_sets, n_playouts: int, *, semantics: int = N.SEM_ARENA,
                          rng: int = N.RNG_NUMPY_MT, seed: int = 0, max_plies: int | None = None,
                          compat_seeds=None, root_index=None, seats_share_stream: bool = False, out=None,
-                         with_results: bool = False, with_states: bool = False, heuristic_seats: int = 0):
+                         with_results: bool = False, with_states: bool = False, heuristic_seats: int = 0,
+                         stream_base: int = 0):
         """Playouts in the reference's FRONTIER list order (bk_rollout_frontier): with the
         numpy-MT compat stream these are the reference's default-config games.
         root_sets: FSET_DTYPE records (one per root).  Host numpy in/out.  SEM_ADVANCE
@@ -207,7 +210,7 @@ class BlokusGPU:
         if max_plies is None:
             max_plies = 2500 if semantics == N.SEM_ARENA else 50
         cfg = N.BkRolloutCfg(semantics, N.ORDER_FRONTIER, rng, max_plies, seed & (2**64 - 1),
-                             int(seats_share_stream), int(heuristic_seats))
+                             int(seats_share_stream), int(heuristic_seats), _stream_base(stream_base, n_playouts))
         if _is_torch(roots):  # device tensors: roots uint8 [n,256], root_sets uint8 [n,2080]
             import torch
             assert semantics != N.SEM_ADVANCE, "device path: playout results only"
@@ -269,11 +272,12 @@ class BlokusGPU:
         return out
 
     # ------------------------------------------------------------------ positions
-    def advance(self, roots, n: int, plies: int, *, seed: int = 0, root_index=None):
+    def advance(self, roots, n: int, plies: int, *, seed: int = 0, root_index=None, stream_base: int = 0):
         """Play `plies` uniformly random moves (naive order, Philox stream) from each root
         and return the reached states (BK_SEM_ADVANCE).  Batched analogue of
         tests/utils_game_states.py:12 generate_random_valid_state (different RNG)."""
-        cfg = N.BkRolloutCfg(N.SEM_ADVANCE, N.ORDER_NAIVE, N.RNG_PHILOX, plies, seed & (2**64 - 1), 0, 0)
+        cfg = N.BkRolloutCfg(N.SEM_ADVANCE, N.ORDER_NAIVE, N.RNG_PHILOX, plies, seed & (2**64 - 1), 0, 0,
+                             _stream_base(stream_base, n))
         if _is_torch(roots):
             import torch
             out = torch.empty((n, 256), dtype=torch.uint8, device=roots.device)
@@ -468,6 +472,13 @@ class BlokusGPU:
         if bad:
             raise RuntimeError(f"bk_mcts: {bad} searches stopped early, status bits "
                                f"{sorted(set(st[st != 0].tolist()))[:8]}")
+
+
+def _stream_base(base: int, n: int) -> int:
+    """Philox stream id of a launch's playout 0 (stream ids are uint32 in the kernel)."""
+    if base < 0 or base + max(n, 0) > 2**32:
+        raise ValueError(f"stream_base {base} + {n} playouts exceeds the uint32 stream ids")
+    return int(base)
 
 
 def _host_root_index(root_index, n_playouts):

@@ -2,8 +2,10 @@
 
 Games are independent and every per-game seed is a pure function of (run seed, game
 index) (analytics/tournament/arena_runner.py:241-254), so rank r of W plays the games
-with index == r (mod W) and the only collective is one gather of fixed-size 32-byte
-bk_result records at the end.  On GPUs the process group is RCCL
+with index == r (mod W) (configs 4 and 5: a fixed job split over the ranks) or the
+contiguous block r (config 3: each rank adds its own block of games, weak scaling), and
+the only collective is one gather of fixed-size 32-byte bk_result records at the end
+(SURVEY 8e).  On GPUs the process group is RCCL
 (backend "nccl"); the same code runs on gloo over CPU tensors in the tests.
 """
 from __future__ import annotations
@@ -36,3 +38,13 @@ def gather_results(local, n_total: int, rank: int, world: int, dist, device=None
         idx = shard_indices(n_total, r, world)
         out[torch.from_numpy(idx).to(out.device)] = parts[r][: len(idx)].to(out.device)
     return out
+
+
+def gather_blocks(local, rank: int, world: int, dist, device=None):
+    """All-gather equal-sized contiguous blocks (rank r holds global records r * n ..
+    (r + 1) * n - 1, uint8 [n, 32] torch tensor) and return them in global order,
+    uint8 [world * n, 32] on `device`."""
+    import torch
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local.contiguous())
+    return torch.cat([p.to(device or local.device) for p in parts], dim=0)

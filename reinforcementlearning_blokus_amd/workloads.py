@@ -13,18 +13,55 @@ from . import _native as N
 from .gpu import BlokusGPU, empty_state, mcts_log_table, mcts_node_cap
 
 
-def frontier_roots(gpu: BlokusGPU, n: int, plies: int, seed: int, *, distinct: int | None = None):
+def frontier_roots(gpu: BlokusGPU, n: int, plies: int, seed: int, *, distinct: int | None = None,
+                   stream_base: int = 0):
     """n synthetic mid-game positions with their frontier-set tables: `plies` uniform
     random moves from the empty board in the reference's frontier list order (Philox
-    stream), i.e. positions a reference Board reaches by place_piece.  distinct: make
-    only that many positions and repeat them (position i % distinct)."""
+    stream (seed, stream_base + i) for position i), i.e. positions a reference Board
+    reaches by place_piece.  distinct: make only that many positions and repeat them
+    (position i % distinct)."""
     k = n if distinct is None else min(n, distinct)
     st, fs = gpu.rollout_frontier(empty_state(), N.fset_new(1), k, semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX,
-                                  seed=seed, max_plies=plies, root_index=np.zeros(k, dtype=np.int32))
+                                  seed=seed, max_plies=plies, root_index=np.zeros(k, dtype=np.int32),
+                                  stream_base=stream_base)
     if k < n:
         idx = np.arange(n) % k
         st, fs = st[idx], fs[idx]
     return st, fs
+
+
+class Config3Plan:
+    """Config 3's random streams as functions of the GLOBAL game index (BASELINE.json
+    configs[2], weak scaling): rank r of a job plays global games r * games .. (r + 1) *
+    games - 1, so the records an N-rank job gathers equal a 1-rank run of the same N *
+    games games (per-game seeds are a pure function of (run seed, game
+    index), analytics/tournament/arena_runner.py:248-254).
+
+    * Root of global game G: `root_plies` uniform random moves from the empty board on
+      Philox stream (seed, G) (bk_advance, or bk_rollout_frontier SEM_ADVANCE in frontier
+      order).
+    * Playout i of global game G (i < rollouts): global playout id P = G * rollouts + i,
+      Philox stream (step_seed(k), P) in step k.
+    A rank's launch uses its local ids with stream_base = the global id of its first."""
+
+    def __init__(self, seed: int, games: int, rollouts: int, rank: int = 0):
+        self.seed, self.games, self.rollouts, self.rank = int(seed), int(games), int(rollouts), int(rank)
+        self.first_game = self.rank * self.games
+        self.n_playouts = self.games * self.rollouts
+        self.root_stream_base = self.first_game
+        self.playout_stream_base = self.first_game * self.rollouts
+
+    def step_seed(self, k: int) -> int:
+        """Philox key of step k (warmup steps k = 0.., timed steps 1000 + k)."""
+        return self.seed * 7919 + k
+
+    def root_index(self) -> np.ndarray:
+        """Local root of each local playout (a game's rollouts are contiguous: one wave
+        plays 64 rollouts of the same game)."""
+        return (np.arange(self.n_playouts, dtype=np.int64) // self.rollouts).astype(np.int32)
+
+    def global_playouts(self) -> np.ndarray:
+        return np.arange(self.n_playouts, dtype=np.int64) + self.playout_stream_base
 
 
 def numpy_mt_states(seeds) -> np.ndarray:

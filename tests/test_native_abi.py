@@ -23,14 +23,14 @@ def test_library_exports_every_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bk_abi_version() == N.ABI_VERSION == 3
+    assert lib.bk_abi_version() == N.ABI_VERSION == 4
     assert lib.bk_tables_version() >= 1
 
 
 def test_struct_sizes():
     assert ctypes.sizeof(N.BkState) == 256
     assert ctypes.sizeof(N.BkResult) == 32
-    assert ctypes.sizeof(N.BkRolloutCfg) == 32
+    assert ctypes.sizeof(N.BkRolloutCfg) == 40
 
 
 def test_orientation_table_matches_reference():

@@ -1,0 +1,24 @@
+"""The config-4 oracle checker (tests/oracle_arena.py) against the reference: it replays
+the run_single_game records of bench.py's config-4 seats at full strength
+(tests/golden/arena_bench.json: MCTS 64 iterations with HeuristicAgent rollouts,
+FastMCTS 1,000 iterations, run seed 20260301, games 0..3), field for field.  CPU only.
+Reference: analytics/tournament/arena_runner.py:578-777.  Tolerance: exact."""
+import json
+
+import pytest
+
+from reinforcementlearning_blokus_amd.arena import RunConfig
+from tests.conftest import load_golden
+from tests.oracle_arena import oracle_arena_game
+
+FX = load_golden("arena_bench.json")
+
+
+@pytest.mark.parametrize("k", range(len(FX["games"])))
+def test_oracle_arena_game_replays_reference_record(k):
+    cfg = RunConfig.from_dict(FX["config"])
+    ref = FX["games"][k]
+    got = oracle_arena_game(cfg, ref["game_index"])
+    for f in ("seat_assignment", "winner_ids", "final_scores", "moves_made", "turn_count", "passes"):
+        assert got[f] == json.loads(json.dumps(ref[f])), (ref["game_index"], f)
+    assert got["simulations"].get("mcts", 0) == ref["mcts_total_simulations"]
