@@ -248,20 +248,24 @@ def reduce_max_sum(dist, dev, tmax, sums):
     return float(t.item()), [float(x) for x in s.tolist()]
 
 
-def traffic_for(kernel):
-    """PMC bytes / VALU instructions per launch of `kernel` from the committed profile
-    summary (tools/summarize_prof.py), if it covers that kernel."""
+def traffic_for(kernel, units_per_launch):
+    """PMC HBM bytes and VALU instructions of ONE launch of `kernel` holding
+    `units_per_launch` units of work (playouts, board-players or simulations), from the
+    committed per-unit profile summary (profiles/traffic_latest.json, written by
+    tools/summarize_prof.py), with the profile it came from; (None, None, None) if no
+    profile covers the kernel."""
     tpath = os.path.join(ROOT, "profiles", "traffic_latest.json")
     try:
-        tj = json.load(open(tpath))
+        per = json.load(open(tpath)).get("kernels", {}).get(kernel)
     except (OSError, ValueError):
-        return None, None
-    per = tj.get("kernels", {}).get(kernel)
-    if per:
-        return per.get("bytes_per_launch"), per.get("valu_insts_per_launch")
-    if tj.get("kernel", "k_rollout") == kernel:
-        return tj.get("bytes_per_launch"), tj.get("valu_insts_per_launch")
-    return None, None
+        per = None
+    if not per or per.get("bytes_per_unit") is None:
+        return None, None, None
+    valu = per.get("valu_insts_per_unit")
+    src = {"pmc": per.get("source"), "stats": per.get("stats"), "unit": per.get("unit"),
+           "profiled_units_per_launch": per.get("units_per_launch"), "units_per_launch": units_per_launch,
+           "bytes_per_unit": per["bytes_per_unit"], "valu_insts_per_unit": valu}
+    return per["bytes_per_unit"] * units_per_launch, (valu * units_per_launch if valu is not None else None), src
 
 
 def compute_roofline(valu_insts, avg_ms):
@@ -349,7 +353,7 @@ def run_config3(args, world, rank, local, dist):
     bytes_per_sim = 2.0 * STATE_B * plies_per_sim + RESULT_B  # 256 B read + write per ply
     achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
     kname = "k_rollout_fr" if args.order == "frontier" else "k_rollout"
-    traffic, valu_insts = traffic_for(kname)
+    traffic, valu_insts, tsrc = traffic_for(kname, n)
     line = {
         "metric": METRIC, "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -360,7 +364,7 @@ def run_config3(args, world, rank, local, dist):
                    "playouts_per_step": n, "parallelism": f"dp{world} (independent games per rank)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "kernel_ms": avg_ms,
-                     "plies_per_sim": plies_per_sim, "bytes_per_sim": bytes_per_sim},
+                     "plies_per_sim": plies_per_sim, "bytes_per_sim": bytes_per_sim, "traffic_profile": tsrc},
         "compute_roofline": compute_roofline(valu_insts, avg_ms),
     }
     if not args.no_cpu_baseline and world == 1:
@@ -430,7 +434,8 @@ def run_config5(args, world, rank, local, dist):
     bytes_rank0 = 2.0 * STATE_B * plies_local + (RESULT_B + 16 + 24 + 48) * sims_rank0
     achieved = bytes_rank0 / (kernel_ms * 1e-3) / 1e9
     kname = gpu.last_kernel() or ("k_mcts_h" if heur else "k_mcts")  # bk_mcts picks it by batch size
-    traffic, valu_insts = traffic_for(kname)
+    # counters per simulation x this line's simulations per launch (its --chunk)
+    traffic, valu_insts, tsrc = traffic_for(kname, sims_rank0 / max(1, len(kms)))
     line = {
         "metric": METRIC if not heur else "MCTSAgent (default HeuristicAgent rollouts) simulations/sec",
         "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
@@ -449,8 +454,8 @@ def run_config5(args, world, rank, local, dist):
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
-                     "kernel_ms": kernel_ms, "launches": len(kms)},
-        # traffic_for gives VALU instructions per launch: pair them with the average launch time
+                     "kernel_ms": kernel_ms, "launches": len(kms), "traffic_profile": tsrc},
+        # VALU instructions of one launch of this line's size over the average launch time
         "compute_roofline": compute_roofline(valu_insts, kernel_ms / max(1, len(kms))),
     }
     if heur:  # no C restatement of the heuristic search to time: the reference's own numbers
@@ -536,12 +541,11 @@ def run_config4(args, world, rank, local, dist):
             print(f"config4 rank {rank}: round {rnd}, {left} games in play, mcts {prof['mcts_s']:.1f} s",
                   file=sys.stderr, flush=True)
 
-    from reinforcementlearning_blokus_amd.mcts.mcts_agent import SEARCH_TOTALS
+    from reinforcementlearning_blokus_amd.mcts.mcts_agent import SEARCH_TOTALS, reset_search_totals
     for _ in range(args.warmup):
         run_games_batched(cfg, mine[:64], device=local)
     barrier_sync(dist)
-    for k in SEARCH_TOTALS:
-        SEARCH_TOTALS[k] = 0
+    reset_search_totals()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         recs = run_games_batched(cfg, mine, device=local, progress=progress)
@@ -560,12 +564,16 @@ def run_config4(args, world, rank, local, dist):
         dist.all_gather_object(gathered, [(r["game_index"], r["final_scores"]) for r in recs])
     if rank != 0:
         return None
-    # roofline of the dominant kernel, bk_mcts (k_mcts_coop_h for these batch sizes): SURVEY
-    # 8(d) bytes, 256 B state read + write per rollout ply, plus 120 B per simulation (result,
-    # TT probe, node write, path update), over the launches' HIP-event time
-    kms = st["kernel_ms"] or float("nan")
-    mcts_bytes = 2.0 * STATE_B * st["rollout_plies"] + (RESULT_B + 16 + 24 + 48) * st["sims"]
+    # roofline of the dominant kernel, the bk_mcts kernel with the most launch time
+    # (k_mcts_coop_h at these batch sizes; bk_mcts picks it by searches per CU): SURVEY
+    # 8(d) bytes, 256 B state read + write per rollout ply, plus 120 B per simulation
+    # (result, TT probe, node write, path update), over its launches' HIP-event time
+    kname, kst = max(st["by_kernel"].items(), key=lambda kv: kv[1]["kernel_ms"]) if st["by_kernel"] else \
+        ("k_mcts_coop_h", {"launches": 0, "kernel_ms": float("nan"), "sims": 0, "rollout_plies": 0})
+    kms = kst["kernel_ms"] or float("nan")
+    mcts_bytes = 2.0 * STATE_B * kst["rollout_plies"] + (RESULT_B + 16 + 24 + 48) * kst["sims"]
     achieved = mcts_bytes / (kms * 1e-3) / 1e9
+    traffic, valu_insts, tsrc = traffic_for(kname, kst["sims"] / max(1, kst["launches"]))
     line = {
         "metric": "arena games/sec (Random/Heuristic/MCTS/FastMCTS round-robin, reference-exact records)",
         "value": games / elapsed, "unit": "games/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -579,9 +587,11 @@ def run_config4(args, world, rank, local, dist):
                    "rank0_phase_seconds": phases,
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_for("k_mcts_coop_h")[0],
-                     "kernel": "k_mcts_coop_h", "kernel_ms": kms, "launches": st["launches"],
-                     "mcts_sims": st["sims"], "rollout_plies_per_sim": st["rollout_plies"] / max(st["sims"], 1)},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "kernel_ms": kms,
+                     "launches": kst["launches"], "mcts_sims": kst["sims"],
+                     "rollout_plies_per_sim": kst["rollout_plies"] / max(kst["sims"], 1), "traffic_profile": tsrc,
+                     "all_search_kernels": st["by_kernel"]},
+        "compute_roofline": compute_roofline(valu_insts, kms / max(1, kst["launches"])),
         "reference_python": {"value": 1.0 / 20.3, "unit": "games/s/core",
                              "what": "a 4-random-agent game with the reference's default telemetry (20.3 s), "
                                      "measured in the build container (SURVEY.md 6); MCTS seats are slower"},
@@ -675,7 +685,7 @@ def run_config2(args, world, rank, local, dist):
         return None
     value = pairs / elapsed
     achieved = n * MOVEGEN_B / (kernel_ms * 1e-3) / 1e9
-    traffic, valu_insts = traffic_for("k_movegen_m")
+    traffic, valu_insts, tsrc = traffic_for("k_movegen_m", n)
     line = {
         "metric": "batched legal-move generation (board-players/s, 20x20, 4p)", "value": value,
         "unit": "board-players/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -690,7 +700,7 @@ def run_config2(args, world, rank, local, dist):
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen_m",
                      "kernel_ms": kernel_ms, "bytes_per_board_player": MOVEGEN_B,
-                     "bytes_written_per_board_player": 91 * 7 * 8 + 4},
+                     "bytes_written_per_board_player": 91 * 7 * 8 + 4, "traffic_profile": tsrc},
         "compute_roofline": compute_roofline(valu_insts, kernel_ms),
     }
     if not args.no_cpu_baseline and world == 1:

@@ -560,8 +560,10 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                         e["moves_with_simulations"] += 1
             if mcts_job is not None:
                 todo, fut = mcts_job
+                tw = time.perf_counter()
                 mv, dt_m = fut.result()
-                prof["mcts_s"] += dt_m
+                prof["mcts_s"] += dt_m  # the searches' own time (overlaps the FastMCTS phase)
+                prof["mcts_wait_s"] = prof.get("mcts_wait_s", 0.0) + time.perf_counter() - tw
                 prof["uncertified_heuristic"] += sum(int(t[1].agent.stats.get("last_search_uncertified", False))
                                                      for t in todo)
                 for (i, a, p, lg), m in zip(todo, mv):
@@ -593,8 +595,11 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
         active = np.array([i for i in active if results[i] is None], dtype=np.int64)
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
-    # (the MCTS launches overlap the FastMCTS phase: host_s is what neither covers)
-    prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"]
+    # the MCTS searches run on the worker thread while this thread runs the FastMCTS phase:
+    # this thread's timeline is setup, advance, FastMCTS, the wait for the searches
+    # (mcts_wait_s) and host work (host_s, everything else); mcts_s is the searches' own
+    # time, overlapping the FastMCTS phase, and is not subtracted
+    prof["host_s"] = (dt - prof["setup_s"] - prof["advance_s"] - prof["fast_s"] - prof.get("mcts_wait_s", 0.0))
     if prof["uncertified_heuristic"]:
         warnings.warn(f"run_games_batched: {prof['uncertified_heuristic']} HeuristicAgent draw(s) fell within 2^-40 "
                       "of a probability boundary (choice not certified equal to the reference's on every host)",

@@ -576,12 +576,21 @@ class MctsTT:
         self.keys, self.vals = keys, vals
 
 
+# One lock for every TTPool: agents search from several threads (web-API executor,
+# the arena's MCTS worker), and a pool's lease / growth / release and a search's
+# gather -> launch -> scatter of its rows must not interleave with another thread's
+# (a growth reassigns the pool's tensors).  mcts_agent._search_on_device holds it from
+# the row gather until the scattered rows are synchronized.
+TT_LOCK = threading.RLock()
+
+
 class TTPool:
     """Device-resident transposition tables of one capacity (the MctsTT layout in HBM:
     keys int64 / vals float64 [rows, cap], NaN = empty, count int32 [rows]).  An agent
     leases one row (TTRow) and keeps it across select_action calls, so a search never
     moves its table between host and device (mcts/mcts_agent.py:304-341 keeps the TT
-    across moves; mcts/zobrist.py:155-220).  One pool per (device, cap): pools()."""
+    across moves; mcts/zobrist.py:155-220).  One pool per (device, cap): get(); a pool
+    whose rows are all released is dropped (its HBM freed).  Thread safety: TT_LOCK."""
 
     _pools: dict = {}
 
@@ -597,26 +606,36 @@ class TTPool:
 
     @classmethod
     def get(cls, device: int, cap: int) -> "TTPool":
-        key = (device, cap)
-        if key not in cls._pools:
-            cls._pools[key] = TTPool(device, cap)
-        return cls._pools[key]
+        with TT_LOCK:
+            key = (device, cap)
+            if key not in cls._pools:
+                cls._pools[key] = TTPool(device, cap)
+            return cls._pools[key]
 
     def lease(self) -> "TTRow":
         import torch
-        if not self.free:  # double the rows (new rows empty)
-            n = self.keys.shape[0]
-            self.keys = torch.cat([self.keys, torch.zeros_like(self.keys)])
-            self.vals = torch.cat([self.vals, torch.full_like(self.vals, float("nan"))])
-            self.count = torch.cat([self.count, torch.zeros_like(self.count)])
-            self.free = list(range(2 * n - 1, n - 1, -1))
-        return TTRow(self, self.free.pop())
+        with TT_LOCK:
+            if not self.free:  # double the rows (new rows empty)
+                n = self.keys.shape[0]
+                # the old tensors may still be read by this thread's queued work: the
+                # copies are ordered after it on this stream, and the old storage is
+                # freed by the caching allocator only after that stream's use
+                self.keys = torch.cat([self.keys, torch.zeros_like(self.keys)])
+                self.vals = torch.cat([self.vals, torch.full_like(self.vals, float("nan"))])
+                self.count = torch.cat([self.count, torch.zeros_like(self.count)])
+                self.free = list(range(2 * n - 1, n - 1, -1))
+            return TTRow(self, self.free.pop())
 
     def release(self, row: int):
-        self.keys[row] = 0
-        self.vals[row] = float("nan")
-        self.count[row] = 0
-        self.free.append(row)
+        import torch
+        with TT_LOCK:
+            self.keys[row] = 0
+            self.vals[row] = float("nan")
+            self.count[row] = 0
+            self.free.append(row)
+            torch.cuda.current_stream(self.keys.device).synchronize()  # visible to every thread's stream
+            if len(self.free) == self.keys.shape[0] and TTPool._pools.get((self.device, self.cap)) is self:
+                del TTPool._pools[(self.device, self.cap)]  # no row leased: free the pool's HBM
 
 
 class TTRow:

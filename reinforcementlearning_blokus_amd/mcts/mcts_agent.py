@@ -28,6 +28,7 @@ The learned-evaluator options of the reference are out of scope and rejected.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import time
 import warnings
@@ -50,7 +51,7 @@ def _search_on_device(gpu, ags, rts, sts, pl, rh, zob, zidx, mt, iters, max_roll
     import torch
 
     from .. import _native as N
-    from ..gpu import TTPool, mcts_log_table, mcts_node_cap
+    from ..gpu import TT_LOCK, TTPool, mcts_log_table, mcts_node_cap
     n = len(ags)
     dev = f"cuda:{gpu.device}"
     up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
@@ -63,39 +64,44 @@ def _search_on_device(gpu, ags, rts, sts, pl, rh, zob, zidx, mt, iters, max_roll
     d_rew = torch.empty((n, iters), dtype=torch.float64, device=dev)
     d_flags = torch.empty((n, iters), dtype=torch.uint8, device=dev)
     tk = tv = tc = rows = pool = None
-    if use_tt:
-        cap = max([a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12])
-        need = max([int(a._gpu_tt.count[0]) for a in ags if a._gpu_tt is not None] or [0]) + iters + 2
-        while 2 * need > cap:
-            cap *= 2
-        pool = TTPool.get(gpu.device, cap)
-        for a in ags:
-            row = a._gpu_tt
-            if row is None:
-                a._gpu_tt = pool.lease()
-            elif row.pool is not pool:  # grown: re-insert into a row of the larger pool
-                nr = pool.lease()
-                nr.load(*row.items(0))
-                row.release()
-                a._gpu_tt = nr
-        rows = torch.tensor([a._gpu_tt.row for a in ags], dtype=torch.int64, device=dev)
-        tk, tv, tc = (pool.keys.index_select(0, rows), pool.vals.index_select(0, rows),
-                      pool.count.index_select(0, rows))
-    gpu.mcts_device(up(rts.view(np.uint8).reshape(n, 256)), up(sts.view(np.uint8).reshape(n, -1)), up(pl),
-                    up(rh.view(np.int64)), up(zob.view(np.int64)), up(zidx), d_mt, lts[iters],
-                    torch.empty((n, cap_nodes * N.MCTS_NODE_DTYPE.itemsize), dtype=torch.uint8, device=dev), d_out,
-                    iterations=iters, tt_keys=tk, tt_vals=tv, tt_count=tc, rewards=d_rew, hit_flags=d_flags,
-                    max_rollout_moves=max_roll, exploration=c, rollout_policy=policy, time_limit_us=tl_us)
-    if use_tt:
-        pool.keys.index_copy_(0, rows, tk)
-        pool.vals.index_copy_(0, rows, tv)
-        pool.count.index_copy_(0, rows, tc)
-        for a, cnt in zip(ags, tc.cpu().numpy()):
-            a._gpu_tt.count[0] = cnt
+    # TT_LOCK from the rows' lease / gather to their scatter (synchronized by the count
+    # copy): another thread's search or pool growth cannot interleave (gpu.TT_LOCK)
+    with (TT_LOCK if use_tt else contextlib.nullcontext()):
+        if use_tt:
+            cap = max([a._gpu_tt.cap for a in ags if a._gpu_tt is not None] or [1 << 12])
+            need = max([int(a._gpu_tt.count[0]) for a in ags if a._gpu_tt is not None] or [0]) + iters + 2
+            while 2 * need > cap:
+                cap *= 2
+            pool = TTPool.get(gpu.device, cap)
+            for a in ags:
+                row = a._gpu_tt
+                if row is None:
+                    a._gpu_tt = pool.lease()
+                elif row.pool is not pool:  # grown: re-insert into a row of the larger pool
+                    nr = pool.lease()
+                    nr.load(*row.items(0))
+                    row.release()
+                    a._gpu_tt = nr
+            rows = torch.tensor([a._gpu_tt.row for a in ags], dtype=torch.int64, device=dev)
+            tk, tv, tc = (pool.keys.index_select(0, rows), pool.vals.index_select(0, rows),
+                          pool.count.index_select(0, rows))
+        gpu.mcts_device(up(rts.view(np.uint8).reshape(n, 256)), up(sts.view(np.uint8).reshape(n, -1)), up(pl),
+                        up(rh.view(np.int64)), up(zob.view(np.int64)), up(zidx), d_mt, lts[iters],
+                        torch.empty((n, cap_nodes * N.MCTS_NODE_DTYPE.itemsize), dtype=torch.uint8, device=dev),
+                        d_out, iterations=iters, tt_keys=tk, tt_vals=tv, tt_count=tc, rewards=d_rew,
+                        hit_flags=d_flags, max_rollout_moves=max_roll, exploration=c, rollout_policy=policy,
+                        time_limit_us=tl_us)
+        if use_tt:
+            pool.keys.index_copy_(0, rows, tk)
+            pool.vals.index_copy_(0, rows, tv)
+            pool.count.index_copy_(0, rows, tc)
+            for a, cnt in zip(ags, tc.cpu().numpy()):  # synchronizes this stream
+                a._gpu_tt.count[0] = cnt
     mt[:] = d_mt.cpu().numpy().view(np.uint32)
-    return {"out": d_out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(n), "rewards": d_rew.cpu().numpy(),
-            "hit_flags": d_flags.cpu().numpy()}
-
+    out = d_out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(n)
+    # only the iterations some search ran cross PCIe (a timed search's bound is far above)
+    live = max(1, int(out["iterations_run"].max())) if n else 1
+    return {"out": out, "rewards": d_rew[:, :live].cpu().numpy(), "hit_flags": d_flags[:, :live].cpu().numpy()}
 
 _MT_VIEWS_OK: Optional[bool] = None
 
@@ -150,8 +156,13 @@ def _positions(move: Move) -> List[Position]:
 
 
 # search_packed's running totals (bench / arena profiling): launches, their kernel time
-# (HIP events around bk_mcts), simulations and rollout plies
-SEARCH_TOTALS: Dict[str, float] = {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0}
+# (HIP events around bk_mcts), simulations and rollout plies, overall and per kernel
+# (bk_mcts picks the kernel by batch size; "by_kernel": {name: the same four totals})
+SEARCH_TOTALS: Dict[str, Any] = {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0, "by_kernel": {}}
+
+
+def reset_search_totals() -> None:
+    SEARCH_TOTALS.update(launches=0, kernel_ms=0.0, sims=0, rollout_plies=0, by_kernel={})
 
 # Timed searches (time_limit): iteration bound per second of limit, and overall.  One
 # search runs ~100-1,000 iterations/s on the GPU (a lane of a persistent wave), so the
@@ -371,10 +382,14 @@ class MCTSAgent:
             r = _search_on_device(gpu, ags, rts, sts, pl, rh, zob, np.array(zidx, np.int32), mt, iters, max_roll, c,
                                   use_tt, tl_us, policy)
             dt = time.time() - t0
-            SEARCH_TOTALS["launches"] += 1
-            SEARCH_TOTALS["kernel_ms"] += gpu.last_kernel_ms()
-            SEARCH_TOTALS["sims"] += int(r["out"]["iterations_run"].sum())
-            SEARCH_TOTALS["rollout_plies"] += int(r["out"]["rollout_plies"].astype(np.int64).sum())
+            kms, ksims = gpu.last_kernel_ms(), int(r["out"]["iterations_run"].sum())
+            kplies = int(r["out"]["rollout_plies"].astype(np.int64).sum())
+            for tot in (SEARCH_TOTALS, SEARCH_TOTALS["by_kernel"].setdefault(
+                    gpu.last_kernel(), {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0})):
+                tot["launches"] += 1
+                tot["kernel_ms"] += kms
+                tot["sims"] += ksims
+                tot["rollout_plies"] += kplies
             # the non-hit rewards of every search as Python lists in one pass (NaN marks a
             # TT hit or an iteration past the search's end: rewards are finite)
             its = np.arange(r["rewards"].shape[1])[None, :]
