@@ -276,9 +276,12 @@ struct StencilClass {
             return BITOP3(c, b, b, LUT_ANDN);
         }
     }
-    // LANE_W1: w1 differs per lane (the lane-pair split of count_class_pair)
+    // LANE_W1: w1 differs per lane (the lane-pair split of count_class_pair).  live: bit r
+    // set iff anchor row r can hold a legal placement in some lane of the wave (a C row
+    // in r .. r + H - 1, wave-uniform, see live_anchor_rows); the other rows are skipped
+    // with a uniform branch (their ok is 0 in every lane, f is not called)
     template <bool LANE_W1 = false, typename F>
-    __device__ __forceinline__ static void scan(const Planes& P, uint32_t w1, F&& f) {
+    __device__ __forceinline__ static void scan(const Planes& P, uint32_t w1, F&& f, uint32_t live = ~0u) {
         // Shift amounts go to VGPRs: a VALU op reading an SGPR is never dual-issued on
         // gfx950 (tools/valu_probe2.hip).  NOTE: the v_bcnt below keeps
         // the whole stream at the single-issue rate anyway, so today this is neutral.
@@ -294,12 +297,41 @@ struct StencilClass {
         // and the live set no longer fits 3 waves per SIMD (other waves hide latency)
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
+            // test the row's bit here (an opaque copy per row: hoisted out of the entry
+            // loop, the 20 row conditions would take 40 SGPRs and spill)
+            uint32_t lv = live;
+            asm volatile("" : "+s"(lv));
+            if (!((lv >> r) & 1u)) continue;
             const uint64_t t0 = tv<0>(P, r, sh);
             f(r, fold<1>(P, r, sh, lo(t0), hi(t0)));
             __builtin_amdgcn_sched_barrier(0);
         }
     }
 };
+
+// Anchor rows that can hold a legal placement of a piece of height H in some lane of the
+// wave: a legal placement covers a C (corner) cell, so rows r whose span r .. r + H - 1
+// holds no C row in ANY lane count 0 everywhere.  Bit r of lh[H - 1]; wave-uniform (one
+// ballot per board row).  The lanes of a rollout wave play the same root, so their
+// movers' corners lie in the same bands of rows (~10 % of the stencil's anchor rows
+// are skipped over random playouts from 20-ply roots).
+struct LiveRows {
+    uint32_t lh[5];
+};
+__device__ __forceinline__ LiveRows live_anchor_rows(const Planes& P) {
+    uint32_t live = 0;
+#pragma unroll
+    for (int R = 0; R < 20; ++R) live |= (__builtin_amdgcn_ballot_w64(P.c(R) != 0u) != 0ull) ? (1u << R) : 0u;
+    live = __builtin_amdgcn_readfirstlane(live);
+    LiveRows L;
+    uint32_t acc = live;
+#pragma unroll
+    for (int h = 0; h < 5; ++h) {
+        L.lh[h] = acc;  // rows r with a C row in r .. r + h
+        acc |= live >> (h + 1);
+    }
+    return L;
+}
 
 // Per-orientation counts in LDS, 10 bits each, three per dword: orientation g lives in
 // dword g / 3 at bit 10 * (g % 3), laid out [dword][lane] (31 dwords per lane).  The
@@ -345,7 +377,8 @@ struct StencilClass {
 // Orientations whose piece no lane of the wave may still play are skipped with a
 // uniform branch.
 template <bool STORE, int H, int... T>
-__device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl) {
+__device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl,
+                                                const LiveRows& L) {
     uint32_t total = 0;
     uint32_t w0 = kClass[i0][0], w1 = kClass[i0][1];
 #pragma unroll 1
@@ -357,7 +390,7 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
         const bool av = (avail >> (piece - 1u)) & 1u;
         if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
             uint32_t c = 0;
-            StencilClass<H, T...>::scan(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); });
+            StencilClass<H, T...>::scan(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); }, L.lh[H - 1]);
             c = av ? c : 0u;
             if constexpr (STORE) atomicAdd(cl + (g / 3) * WAVE, c << (10 * (g % 3)));
             total += c;
@@ -375,7 +408,7 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
 // field stays 0, so the two columns add up to the full count vector (pick_orient<true>).
 template <bool STORE, int H, int... T>
 __device__ __forceinline__ uint32_t count_class_pair(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl,
-                                                     bool odd) {
+                                                     bool odd, const LiveRows& L) {
     uint32_t total = 0;
 #pragma unroll 1
     for (int ia = i0; ia < i1; ia += 2) {
@@ -388,7 +421,8 @@ __device__ __forceinline__ uint32_t count_class_pair(int i0, int i1, const Plane
         const bool av = ((avail >> (piece - 1u)) & 1u) && (has_b || !odd);
         if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
             uint32_t c = 0;
-            StencilClass<H, T...>::template scan<true>(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); });
+            StencilClass<H, T...>::template scan<true>(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); },
+                                                       L.lh[H - 1]);
             c = av ? c : 0u;
             if constexpr (STORE) atomicAdd(cl + (g / 3) * WAVE, c << (10 * (g % 3)));
             total += c;
@@ -456,7 +490,8 @@ __device__ __forceinline__ uint32_t count_entry(const Planes& P, uint32_t avail,
 // PAIR: lanes 2j and 2j + 1 hold the same board-player and split the entries
 // (count_class_pair); each returns its share of the total.
 template <bool STORE, bool PAIR = false>
-__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane) {
+__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane,
+                                                   bool rowskip = true) {
     uint32_t t = 0;
     uint32_t* cl = cnt + lane;  // this lane's dwords; the orientation part is uniform
     if constexpr (STORE) {
@@ -470,6 +505,9 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     int tb0 = 0;
     asm volatile("" : "+s"(tb0));
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
+    LiveRows L = live_anchor_rows(P);
+    if (!rowskip)  // uniform (tuning A/B: BK_ROWSKIP=0)
+        for (int h = 0; h < 5; ++h) L.lh[h] = ~0u;
 #ifdef BK_STENCIL_LITERAL
     (void)tb0;
 #define BK_COUNT_ENTRY(PIECE, G, H, ...) t += count_entry<STORE, PIECE, G, H, __VA_ARGS__>(P, avail, cl);
@@ -478,11 +516,11 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
 #else
     if constexpr (PAIR) {
         const bool odd = (lane & 1) != 0;
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd);
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd, L);
         BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     } else {
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl);
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, L);
         BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     }
@@ -1858,6 +1896,7 @@ struct RolloutArgs {
                                // s, s + nslots, ...; 2: slot s plays s, then only slots
                                // < long_slots pull the rest from the counter (whole waves)
     uint32_t long_slots;
+    int32_t rowskip;           // 1: skip anchor rows no lane of the wave can use (live_anchor_rows)
 };
 
 // four per-player scalars (kept as separate SSA values: an array indexed by a
@@ -2288,7 +2327,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             total = 0;
             // uniform-random movers: counts, draw, orientation (before the area is reused)
             if (__builtin_amdgcn_ballot_w64(!idle && !heur)) {
-                const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane);
+                const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane, a.rowskip != 0);
                 if (!idle && !heur) {
                     total = t;
                     // (a stop seat draws nothing: bk_arena_advance hands its turn back)
@@ -2313,7 +2352,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 }
             }
         } else {
-            total = movegen_counts<true>(P, avail, my, lane);
+            total = movegen_counts<true>(P, avail, my, lane, a.rowskip != 0);
         }
         SECT(2);
         if (idle) continue;
@@ -4276,7 +4315,8 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
                   (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr,
-                  (const uint8_t*)d_masks, (uint32_t*)d_rng, fr ? 0 : 2, 0u};
+                  (const uint8_t*)d_masks, (uint32_t*)d_rng, fr ? 0 : 2, 0u, 1};
+    if (const char* env = getenv("BK_ROWSKIP")) a.rowskip = atoi(env);  // tuning A/B
     // Playout hand-out.  Config 3 has 1.33 playouts per resident slot: pulled per lane
     // from one counter (handout 0), the extra third lands on lanes of EVERY wave, and each
     // wave then runs a second playout length with a third of its lanes; given to whole
