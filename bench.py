@@ -83,6 +83,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=20260301)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-cores", type=int, default=None,
+                    help="config4: host cores this rank may use (default: the usable cores / local ranks; "
+                         "each rank's host phases and worker threads are pinned to its own cores)")
     ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
                     help="config3 in-kernel move order: naive (default) or the reference's frontier order "
                          "(CPython set tables carried per game)")
@@ -161,6 +164,25 @@ def cpu_baseline_playouts(roots_np, seconds, order, rollouts, seed=None, gpu_out
         out["sample"] += "; the GPU's own games (same roots and Philox streams as the last timed step)"
         out["same_games_bit_identical"] = g == bytes(res)
     return out
+
+
+def pin_host_cores(k=None):
+    """Pin this rank (its current thread, and so every thread it starts later: the arena's
+    search worker, the library's host threads) to its own share of the host's cores: k
+    cores, default the usable cores / LOCAL_WORLD_SIZE (an 8-rank node leaves each rank
+    1/8 of the host).  Returns {"cores": k, "cpus": [...]}."""
+    import torch
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    nloc = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    if k is None:
+        k = max(1, host_cpu()["cores"] // max(1, nloc))
+    k = max(1, int(k))
+    mine = cpus[local * k:(local + 1) * k] or cpus[:k]
+    if mine and hasattr(os, "sched_setaffinity"):
+        os.sched_setaffinity(0, mine)
+    torch.set_num_threads(k)
+    return {"cores": k, "cpus": mine}
 
 
 # ------------------------------------------------------------------ N-rank launch
@@ -532,6 +554,7 @@ def run_config4(args, world, rank, local, dist):
     from reinforcementlearning_blokus_amd.shard import shard_indices
 
     total = args.games or 8192
+    host = pin_host_cores(args.host_cores)
     cfg = RunConfig.from_dict({"agents": CONFIG4_AGENTS, "num_games": total, "seed": args.seed,
                                "seat_policy": "round_robin"})
     mine = shard_indices(total, rank, world).tolist()
@@ -584,7 +607,7 @@ def run_config4(args, world, rank, local, dist):
                                "iterations/move, lockstep batches (bk_arena_advance + bk_mcts + bk_fastmcts)",
                    "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
                    "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
-                   "rank0_phase_seconds": phases,
+                   "rank0_phase_seconds": phases, "host_cores_per_rank": host,
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "kernel_ms": kms,

@@ -37,6 +37,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <sched.h>
+
 #include <mutex>
 #include <thread>
 #include <new>
@@ -4514,6 +4516,8 @@ int bk_pow_half_fix(const double* log_table, int32_t log_len, int32_t* offsets, 
     double (*const pw)(double, double) = powp;
     std::vector<std::vector<int32_t>> rows((size_t)log_len);
     unsigned nt = std::thread::hardware_concurrency();
+    cpu_set_t aff;  // the CPUs this process may run on (a bench rank's share of the host)
+    if (sched_getaffinity(0, sizeof aff, &aff) == 0 && CPU_COUNT(&aff) > 0) nt = (unsigned)CPU_COUNT(&aff);
     nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;  // the GPU box's CPU share is 16
     if ((int64_t)log_len * log_len < 4000000) nt = 1;
     std::vector<char> ok(nt, 1);
