@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import json
 import random
+import os
 import time
 import warnings
 import traceback
@@ -389,6 +390,18 @@ def _mcts_worker() -> ThreadPoolExecutor:
     return _MCTS_WORKER
 
 
+class _InlineWorker:
+    """BK_ARENA_SERIAL=1: the MCTS searches run on the calling thread (profiling: cProfile
+    sees one thread), the same work in the same order."""
+
+    @staticmethod
+    def submit(fn, *args):
+        from concurrent.futures import Future
+        f: Future = Future()
+        f.set_result(fn(*args))
+        return f
+
+
 def _timed_search(agents, roots, sets, players):
     t0 = time.perf_counter()
     mv = MCTSAgent.search_packed(agents, roots, sets, players)
@@ -456,7 +469,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     # but a host's rounding could pick the neighbour (HeuristicAgent)
     prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0,
                 uncertified_heuristic=0)
-    worker = _mcts_worker()
+    worker = _InlineWorker() if os.environ.get("BK_ARENA_SERIAL") == "1" else _mcts_worker()
     while len(active):
         prof["rounds"] += 1
         if progress is not None:
