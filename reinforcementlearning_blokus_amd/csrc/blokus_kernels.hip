@@ -3552,6 +3552,136 @@ __device__ __forceinline__ int coop_heur_pick(const double (&es)[2], int lane, c
     return L + WAVE * h;
 }
 
+// legal anchor rows and counts of this lane's orientations g = lane + 64 h (rows = {B, C}
+// in the lane's column); 0 rows for g >= 91 or a used piece.  The rows stay in registers
+// for the balanced heuristic pass.
+__device__ __forceinline__ uint32_t coop_ok_count1(const uint2* rows, uint32_t avail, int g, uint32_t (&ok)[20]) {
+    const bool live = g < BK_NUM_ORIENTS && ((avail >> ((kInfo[g < BK_NUM_ORIENTS ? g : 0] & 0xFFu) - 1u)) & 1u);
+    if (live) {
+        lane_ok_rows(g, rows, ok);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 20; ++r) ok[r] = 0u;
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < 20; ++r) c += __builtin_popcount(ok[r]);
+    return c;
+}
+
+__device__ __forceinline__ void coop_ok_counts(const uint2* rows, uint32_t avail, int lane, uint32_t (&ok0)[20],
+                                               uint32_t (&ok1)[20], uint32_t (&cnt)[2]) {
+    cnt[0] = coop_ok_count1(rows, avail, lane, ok0);
+    cnt[1] = coop_ok_count1(rows, avail, lane + WAVE, ok1);
+}
+
+// orientation g's legal moves (rows ok) into the move list from index idx: naive order
+__device__ __forceinline__ void coop_list_moves(uint16_t* ml, uint32_t idx, uint32_t g, const uint32_t (&ok)[20]) {
+#pragma unroll
+    for (int r = 0; r < 20; ++r) {
+        uint32_t w = ok[r];
+        while (w) {
+            const uint32_t x = (uint32_t)__builtin_ctz(w);
+            w &= w - 1u;
+            ml[idx++] = (uint16_t)(g * 400u + (uint32_t)r * 20u + x);
+        }
+    }
+}
+
+// Balanced HeuristicAgent pass A for the wave's search (k_mcts_coop_h): instead of each
+// lane summing e over its own two orientations' moves (the wave then iterates the
+// largest orientation's move count, ~1 legal move per lane-iteration), the ply's legal
+// moves go to a list in LDS in naive order (orientation ascending, anchors row-major:
+// orientation g at [s_g, s_g + c_g) from the count scan), and the wave evaluates
+// e = exp(score) 64 moves at a time, with a running prefix sum.  The lane holding the
+// first / last move of an orientation records the cumulative e before / after it; the
+// crossing of target = u * total is then found at orientation level by a ballot, exactly
+// what coop_heur_pick decides from per-orientation sums (the sums differ by rounding only;
+// the walk certifies the draw against HEUR_MARGIN).  area = the wave's LDS area (the move
+// list and the cumulative sums after the {B, C} rows).  false: more than COOP_MOVE_CAP
+// legal moves (nothing done; the caller runs coop_orients<true> + coop_heur_pick).
+#define COOP_MOVE_CAP 2048
+#define COOP_ML_DWORD (40 * WAVE)                        // after the rows' 40 dwords per lane
+#define COOP_CUM_DWORD (COOP_ML_DWORD + COOP_MOVE_CAP / 2)  // cumE[91], cumS[91] (doubles)
+__device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* area, int lane, const HeurShared* hs,
+                                                   int edge_w, const uint32_t (&ok0)[20], const uint32_t (&ok1)[20],
+                                                   const uint32_t (&cnt)[2], const CoopScan& sc, const uint32_t* st,
+                                                   uint32_t& pos, uint32_t pre0, uint32_t pre1, double& target,
+                                                   double& R, double& total, bool& uncertain, int& gs,
+                                                   uint32_t (&gok)[20]) {
+    const uint32_t n_moves = sc.total;
+    if (n_moves > COOP_MOVE_CAP) return false;
+    uint16_t* ml = reinterpret_cast<uint16_t*>(area + COOP_ML_DWORD);
+    double* cumE = reinterpret_cast<double*>(area + COOP_CUM_DWORD);
+    double* cumS = cumE + BK_NUM_ORIENTS;
+    coop_list_moves(ml, sc.i0 - sc.c0, (uint32_t)lane, ok0);
+    coop_list_moves(ml, sc.i1 - sc.c1, (uint32_t)(lane + WAVE), ok1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double carry = 0.0;
+#pragma unroll 1
+    for (uint32_t k0 = 0; k0 < n_moves; k0 += WAVE) {
+        const uint32_t k = k0 + (uint32_t)lane;
+        const bool in = k < n_moves;
+        const uint32_t mv = in ? ml[k] : 0u;
+        const int g = (int)(mv / 400u), cell = (int)(mv % 400u);
+        const int gn = k + 1u < n_moves ? (int)(ml[k + 1u] / 400u) : -1;
+        const int gp = in && k > 0u ? (int)(ml[k - 1u] / 400u) : -1;
+        double e = 0.0;
+        if (in) {
+            int n;
+            uint32_t cd[5], cc[5];
+            orient_cells(g, n, cd, cc);
+            e = heur_e(n, cd, cc, cell / 20, cell % 20, rows, hs, edge_w);
+        }
+        const double incl = wave_incl_scan_f64(e, lane) + carry;
+        const double up = __shfl_up(incl, 1);
+        const double excl = lane ? up : carry;
+        if (in && gn != g) cumE[g] = incl;
+        if (in && gp != g) cumS[g] = excl;
+        carry = __shfl(incl, WAVE - 1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    total = carry;
+    // the HeuristicAgent's draw (random_sample), as coop_heur_pick
+    double u;
+    if (pos + 2u <= (uint32_t)FM_N) {
+        u = ((double)(mc_temper(pre0) >> 5) * 67108864.0 + (double)(mc_temper(pre1) >> 6)) *
+            (1.0 / 9007199254740992.0);
+        pos += 2u;
+    } else {
+        u = mc_random_sample(const_cast<uint32_t*>(st), pos);
+    }
+    target = u * total;
+    const double e0 = cnt[0] ? cumE[lane] : 0.0;
+    const double e1 = cnt[1] ? cumE[lane + WAVE] : 0.0;
+    const uint64_t b0 = __ballot(cnt[0] != 0u && e0 > target);
+    const uint64_t b1 = __ballot(cnt[1] != 0u && e1 > target);
+    int L = -1, h = 0;
+    if (b0) { L = __ffsll((unsigned long long)b0) - 1; }
+    else if (b1) { L = __ffsll((unsigned long long)b1) - 1; h = 1; }
+    else {
+        uncertain = true;
+        const uint64_t l1 = __ballot(cnt[1] != 0u), l0 = __ballot(cnt[0] != 0u);
+        if (l1) { L = 63 - __clzll((unsigned long long)l1); h = 1; }
+        else if (l0) { L = 63 - __clzll((unsigned long long)l0); }
+    }
+    if (L < 0) { R = 0.0; gs = -1; return true; }
+    gs = L + WAVE * h;
+    R = cumS[gs];
+    if (h) {  // the chosen orientation's rows, from the lane that listed them
+#pragma unroll
+        for (int r = 0; r < 20; ++r) gok[r] = __shfl(ok1[r], L);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 20; ++r) gok[r] = __shfl(ok0[r], L);
+    }
+    return true;
+}
+
 // Cooperative pass 2 of locate_move_frontier / heur_walk_frontier (one wave = one search;
 // the legal anchors of gs in rows[r * WAVE].y, identical in every lane's column).  Lane j
 // takes the table's slots j and j + 64.  The anchor a = f - cell_k of the key f at slot s
@@ -3663,6 +3793,8 @@ __device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows
     return true;
 }
 
+static_assert(COOP_CUM_DWORD + 4 * BK_NUM_ORIENTS <= COOP_AREA, "the move list and sums fit a wave's area");
+
 template <bool HEUR>
 __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     constexpr int BLK = COOP_WAVES * WAVE;
@@ -3752,7 +3884,8 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         SECT(1);
         uint32_t cnt[2];
         double es[2];
-        if (hroll) coop_orients<true>(rows_lds, avail, lane, hs, edge_w, cnt, es);
+        uint32_t okA[20], okB[20];  // hroll: this lane's orientations' legal rows (balanced pass)
+        if (hroll) coop_ok_counts(rows_lds, avail, lane, okA, okB, cnt);
         else coop_orients<false>(rows_lds, avail, lane, hs, edge_w, cnt, es);
         const CoopScan sc = coop_scan(cnt, lane);
         const uint32_t total = sc.total;
@@ -3791,9 +3924,15 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         uint32_t h_ok[20];
         bool h_unc = false;
         if (hroll) {
-            gs = coop_heur_pick(es, lane, a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, h_pre0, h_pre1, h_target,
-                                h_R, h_total, h_unc);
-            if (gs >= 0) lane_ok_rows(gs, rows_lds, h_ok);
+            uint32_t* st = a.mt + (size_t)m.game * (FM_N + 1);
+            if (!coop_heur_balanced(rows_lds - lane, my, lane, hs, edge_w, okA, okB, cnt, sc, st, m.mt_pos, h_pre0,
+                                    h_pre1, h_target, h_R, h_total, h_unc, gs, h_ok)) {
+                // more legal moves than the list holds: per-lane orientation sums
+                es[0] = cnt[0] ? lane_orient_sum(lane, okA, rows_lds, hs, edge_w) : 0.0;
+                es[1] = cnt[1] ? lane_orient_sum(lane + WAVE, okB, rows_lds, hs, edge_w) : 0.0;
+                gs = coop_heur_pick(es, lane, st, m.mt_pos, h_pre0, h_pre1, h_target, h_R, h_total, h_unc);
+                if (gs >= 0) lane_ok_rows(gs, rows_lds, h_ok);
+            }
         } else {
             gs = coop_find(sc, k, kk);
         }
