@@ -1166,8 +1166,12 @@ struct FsetRef {  // one player's table: runs of 2^sh slots, run j at key[j * st
     uint32_t cap;     // largest table this storage holds (power of 2)
     const uint64_t* hash;  // hash((r, c)) by cell
     int sh = 1;       // log2 of the run length
+    uint32_t* dirty = nullptr;  // if set: bit j marks 8-slot chunk j written (all: a resize)
     __host__ __device__ __forceinline__ int16_t& at(uint64_t i) const {
         return key[(i >> sh) * (uint64_t)stride + (i & ((1u << sh) - 1u))];
+    }
+    __host__ __device__ __forceinline__ void mark(uint64_t i) const {
+        if (dirty) *dirty |= 1u << ((i >> 3) & 31u);
     }
 };
 
@@ -1234,6 +1238,7 @@ __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool a
             if (kk == k) {
                 if (!add) {
                     t.at(e) = FS_DUMMY;
+                    t.mark(e);
                     *t.used -= 1;
                 }
                 return true;
@@ -1250,12 +1255,15 @@ __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool a
     if (freeslot >= 0) {
         *t.used += 1;
         t.at(freeslot) = k;
+        t.mark((uint64_t)freeslot);
         return true;
     }
     *t.fill += 1;
     *t.used += 1;
     t.at(e) = k;
+    t.mark(e);
     if ((uint64_t)*t.fill * 5 < (uint64_t)mask * 3) return true;
+    if (t.dirty) *t.dirty = ~0u;  // every slot is rewritten
     return fs_resize(t, tmp, *t.used > 50000 ? *t.used * 2u : *t.used * 4u);
 }
 
@@ -1484,19 +1492,23 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
                 lw[(4 * i + 3) * WAVE] = v.w;
             }
         }
-        uint16_t m = (uint16_t)gmask, f = gfs->fill[p], u = gfs->used[p];
-        FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab};
+        const uint16_t m0 = (uint16_t)gmask, f0 = gfs->fill[p], u0 = gfs->used[p];
+        uint16_t m = m0, f = f0, u = u0;
+        uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
+        FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab, 1, &dirty};
         if (fs_run_ops(t, fl->tmp, cells, real)) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
             const uint32_t newsize = fs_copy_size(u);
             if (!RECOPY || (newsize - 1 == m && f == u)) {  // (a copy of a clean table is the table)
 #pragma unroll
                 for (int i = 0; i < STAGE / 8; ++i) {
-                    if ((uint32_t)(8 * i) <= m)
+                    if ((uint32_t)(8 * i) <= m && ((dirty >> i) & 1u))
                         dst4[i] = make_uint4(lw[(4 * i + 0) * WAVE], lw[(4 * i + 1) * WAVE],
                                              lw[(4 * i + 2) * WAVE], lw[(4 * i + 3) * WAVE]);
                 }
-                gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+                if (m != m0) gfs->mask[p] = m;
+                if (f != f0) gfs->fill[p] = f;
+                if (u != u0) gfs->used[p] = u;
                 return true;
             }
             // the copy: newsize <= 2 * STAGE <= BK_FSET_SLOTS (u < STAGE * 3 / 5)
@@ -1536,8 +1548,10 @@ template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4>
 __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* stage_q, const uint64_t* htab,
                                                    const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
-    uint16_t m = gfs->mask[p], f = gfs->fill[p], u = gfs->used[p];
-    FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4};
+    const uint16_t m0 = gfs->mask[p], f0 = gfs->fill[p], u0 = gfs->used[p];
+    uint16_t m = m0, f = f0, u = u0;
+    uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
+    FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4, &dirty};
     if (fs_run_ops(t, fl->tmp, cells, real)) {
         bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
         const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(stage_q);
@@ -1546,11 +1560,13 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
 #pragma unroll
             for (int r = 0; r < DMA_RUNS; ++r) {
                 if ((uint32_t)(16 * r) <= m) {
-                    dst4[2 * r] = src4[r * RUN_U4];
-                    dst4[2 * r + 1] = src4[r * RUN_U4 + 1];
+                    if ((dirty >> (2 * r)) & 1u) dst4[2 * r] = src4[r * RUN_U4];
+                    if ((dirty >> (2 * r + 1)) & 1u) dst4[2 * r + 1] = src4[r * RUN_U4 + 1];
                 }
             }
-            gfs->mask[p] = m; gfs->fill[p] = f; gfs->used[p] = u;
+            if (m != m0) gfs->mask[p] = m;
+            if (f != f0) gfs->fill[p] = f;
+            if (u != u0) gfs->used[p] = u;
             return true;
         }
         const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
