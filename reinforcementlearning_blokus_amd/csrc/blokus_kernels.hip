@@ -2756,6 +2756,7 @@ struct MctsArgs {
     int32_t tree_batch;    // tree phase once this many lanes of a wave wait for it (or no lane is busy)
     int32_t spread;        // only lanes with lane % spread == 0 take searches (more waves, fewer lanes each)
     int32_t coop_walk;     // k_mcts_coop(_h): frontier walk split over the wave (coop_walk), else serial
+    int32_t coop_balanced; // k_mcts_coop_h: balanced HeuristicAgent pass (coop_heur_balanced), else per lane
 };
 
 struct Mc {
@@ -3941,7 +3942,8 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         bool h_unc = false;
         if (hroll) {
             uint32_t* st = a.mt + (size_t)m.game * (FM_N + 1);
-            if (!coop_heur_balanced(rows_lds - lane, my, lane, hs, edge_w, okA, okB, cnt, sc, st, m.mt_pos, h_pre0,
+            if (!a.coop_balanced ||
+                !coop_heur_balanced(rows_lds - lane, my, lane, hs, edge_w, okA, okB, cnt, sc, st, m.mt_pos, h_pre0,
                                     h_pre1, h_target, h_R, h_total, h_unc, gs, h_ok)) {
                 // more legal moves than the list holds: per-lane orientation sums
                 es[0] = cnt[0] ? lane_orient_sum(lane, okA, rows_lds, hs, edge_w) : 0.0;
@@ -4936,8 +4938,9 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (int32_t*)sec[9].dev, (const double*)sec[10].dev, log_len, (bk_mcts_node*)sec[11].dev,
                (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
-               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1};
+               (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1, 1};
     if (const char* env = getenv("BK_COOP_WALK")) a.coop_walk = atoi(env);  // tuning / test override
+    if (const char* env = getenv("BK_COOP_BAL")) a.coop_balanced = atoi(env);  // tuning / test override
     // spread 2: the idle odd lane of each pair splits the even lane's stencil (k_mcts_pair)
     bool pair = true;
     if (const char* env = getenv("BK_MCTS_PAIR")) pair = atoi(env) != 0;  // tuning / test override
