@@ -89,3 +89,23 @@ def test_coop_time_limit_stops(gpu, monkeypatch):
     r, _, _ = _run(gpu, roots, sets, 200000, N.MCTS_ROLLOUT_RANDOM, 50, True, monkeypatch, time_limit_us=30000)
     it = r["out"]["iterations_run"]
     assert (it >= 1).all() and (it < 200000).all()
+
+
+@pytest.mark.parametrize("n,iters,root_plies", [(40, 48, 6), (24, 64, 30)])
+def test_coop_balanced_heuristic_pass_equals_per_lane_sums(gpu, monkeypatch, n, iters, root_plies):
+    """k_mcts_coop_h's balanced HeuristicAgent pass (the ply's legal moves listed in LDS,
+    e evaluated 64 moves at a time, coop_heur_balanced) against the per-lane orientation
+    sums it replaces (BK_COOP_BAL=0, also its fallback above 2,048 legal moves), early
+    (6-ply roots: many legal moves) and late (30-ply roots): every output bit-identical."""
+    from reinforcementlearning_blokus_amd.workloads import frontier_roots
+    roots, sets = frontier_roots(gpu, n, root_plies, seed=31337 + n)
+    pol = N.MCTS_ROLLOUT_HEURISTIC
+    a, mta, tta = _run(gpu, roots, sets, iters, pol, 50, True, monkeypatch, env={"BK_COOP_BAL": "1"})
+    b, mtb, ttb = _run(gpu, roots, sets, iters, pol, 50, True, monkeypatch, env={"BK_COOP_BAL": "0"})
+    assert (a["out"]["status"] & ~np.uint32(N.MCTS_EUNCERT) == 0).all()
+    assert (a["out"]["iterations_run"] == iters).all()
+    assert a["out"].tobytes() == b["out"].tobytes()
+    assert np.array_equal(a["rewards"], b["rewards"]) and np.array_equal(a["hit_flags"], b["hit_flags"])
+    assert np.array_equal(mta, mtb)
+    assert np.array_equal(tta.keys, ttb.keys) and np.array_equal(tta.count, ttb.count)
+    assert a["nodes"].tobytes() == b["nodes"].tobytes()
