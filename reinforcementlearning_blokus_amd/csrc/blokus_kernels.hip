@@ -68,6 +68,12 @@
 #define BK_TU 0
 #endif
 #define BK_DEF(u) (BK_TU == 0 || BK_TU == (u))
+// 1: the stencil skips anchor rows no lane of the wave can use (live_anchor_rows) --
+// measured no faster: the per-row branches cost the kernel spills;
+// 0: the round-3 stencil (every anchor row), a build for the A/B measurement
+#ifndef BK_ROWSKIP_BUILD
+#define BK_ROWSKIP_BUILD 0
+#endif
 
 // Section timers (diagnostic build only, -DBK_SECTION_PROF): per-wave shader-clock
 // cycles spent in each section of a kernel's loop, summed over waves into
@@ -301,9 +307,11 @@ struct StencilClass {
         for (int r = 0; r < NR; ++r) {
             // test the row's bit here (an opaque copy per row: hoisted out of the entry
             // loop, the 20 row conditions would take 40 SGPRs and spill)
+#if BK_ROWSKIP_BUILD
             uint32_t lv = live;
             asm volatile("" : "+s"(lv));
             if (!((lv >> r) & 1u)) continue;
+#endif
             const uint64_t t0 = tv<0>(P, r, sh);
             f(r, fold<1>(P, r, sh, lo(t0), hi(t0)));
             __builtin_amdgcn_sched_barrier(0);
@@ -507,9 +515,14 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     int tb0 = 0;
     asm volatile("" : "+s"(tb0));
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
+#if BK_ROWSKIP_BUILD
     LiveRows L = live_anchor_rows(P);
     if (!rowskip)  // uniform (tuning A/B: BK_ROWSKIP=0)
         for (int h = 0; h < 5; ++h) L.lh[h] = ~0u;
+#else
+    (void)rowskip;
+    const LiveRows L{{~0u, ~0u, ~0u, ~0u, ~0u}};
+#endif
 #ifdef BK_STENCIL_LITERAL
     (void)tb0;
 #define BK_COUNT_ENTRY(PIECE, G, H, ...) t += count_entry<STORE, PIECE, G, H, __VA_ARGS__>(P, avail, cl);
