@@ -262,6 +262,31 @@ int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_
 #define BK_STATUS_STOP 32
 int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const bk_rollout_cfg* cfg,
                      const uint8_t* seat_masks, uint32_t* rng_state, bk_result* out, int mem);
+/*
+ * bk_arena_advance with the search seats' moves and their inputs kept on the device, so an
+ * arena round is bk_arena_step -> bk_mcts / bk_fastmcts -> bk_arena_step with no
+ * position or table crossing PCIe (config 4).  Extra arguments (each may be NULL):
+ * forced[i]: the move the agent at game i's stop seat chose in the previous round, placed
+ *   first: -1 none (a stopped game stays stopped); g * 400 + 20 r + c a move
+ *   (bk_mcts best_move); BK_FORCE_INDEX | k the k-th entry of the mover's legal list in
+ *   the reference's order (FastMCTSAgent's child index into get_legal_moves).
+ * quick_masks[i] bit p: stop seat p is a FastMCTSAgent; when game i stops there,
+ *   stop_out[i] receives its root's FastMCTS inputs: the legal-move count, and
+ *   _quick_move_evaluation (agents/fast_mcts_agent.py:285-298: of the first 3 moves by
+ *   piece id descending, stable, the one nearest the centre by |r - 9.5| + |c - 9.5|,
+ *   stable) as its list index and its reward pid * 0.1 + (20 - dist) * 0.05 (:260-283).
+ */
+#define BK_FORCE_INDEX 0x40000000
+typedef struct bk_stop_info {
+    int32_t n_legal;      /* legal moves of the player to move                        */
+    int32_t quick_index;  /* list index of _quick_move_evaluation's move              */
+    double quick_reward;  /* _fast_rollout's reward before the noise term             */
+} bk_stop_info;
+
+int bk_arena_step(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const bk_rollout_cfg* cfg,
+                  const uint8_t* seat_masks, const uint8_t* quick_masks, const int32_t* forced,
+                  uint32_t* rng_state, bk_result* out, bk_stop_info* stop_out, int mem);
+
 /* numpy RandomState(seed) cursor for rng_state (host, no GPU) */
 int bk_mt_cursor_init(uint32_t seed, uint32_t* out4);
 

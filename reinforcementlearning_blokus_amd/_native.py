@@ -17,7 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BK_LIB_PATH") or os.path.join(_HERE, "_lib", "libblokus_hip.so")
 
 OK, EINVAL, EHIP, ENOMEM, EOVERFLOW = 0, -1, -2, -3, -4
-STATUS_CAP, STATUS_UNCERT, STATUS_STOP = 8, 16, 32  # bk_result.status bits
+STATUS_CAP, STATUS_UNCERT, STATUS_STOP, STATUS_BADFORCE = 8, 16, 32, 64  # bk_result.status bits
+FORCE_INDEX = 0x40000000  # bk_arena_step forced[i]: the k-th entry of the legal list (BK_FORCE_INDEX | k)
 MEM_HOST, MEM_DEVICE = 0, 1
 SEM_ARENA, SEM_ROLLOUT, SEM_ADVANCE = 0, 1, 2
 ORDER_NAIVE, ORDER_FRONTIER = 0, 1
@@ -32,7 +33,7 @@ EXPORTS = (
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms", "bk_last_kernel",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
-    "bk_mt_cursor_init",
+    "bk_arena_step", "bk_mt_cursor_init",
 )
 FSET_SLOTS = 256
 # bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
@@ -104,6 +105,7 @@ MCTS_ROLLOUT_RANDOM, MCTS_ROLLOUT_HEURISTIC = 0, 1
 STATE_DTYPE = np.dtype([("planes", "<u8", (4, 7)), ("used", "<u4", (4,)), ("first_move", "u1"),
                         ("current_player", "u1"), ("out_mask", "u1"), ("flags", "u1"),
                         ("move_count", "<u2"), ("reserved16", "<u2"), ("reserved", "<u4", (2,))])
+STOP_DTYPE = np.dtype([("n_legal", "<i4"), ("quick_index", "<i4"), ("quick_reward", "<f8")])  # bk_stop_info
 RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("status", "u1"),
                          ("plies", "<u2"), ("passes", "<u2"), ("turns", "<u2"), ("reward", "<i4"),
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
@@ -159,6 +161,7 @@ def load():
                                       vp, vp, C.c_int]),
             "bk_pow_half_fix": (C.c_int, [vp, C.c_int32, vp, vp, C.c_int32, P(C.c_int32)]),
             "bk_arena_advance": (C.c_int, [vp, vp, vp, C.c_int32, P(BkRolloutCfg), vp, vp, vp, C.c_int]),
+            "bk_arena_step": (C.c_int, [vp, vp, vp, C.c_int32, P(BkRolloutCfg), vp, vp, vp, vp, vp, vp, C.c_int]),
             "bk_mt_cursor_init": (C.c_int, [C.c_uint32, vp]),
             "bk_debug_fastmcts_select": (C.c_int, [vp, C.c_int32, vp, vp, C.c_uint32, vp, C.c_int32, vp, vp,
                                                    C.c_int32, C.c_double, P(C.c_int32)]),
@@ -400,6 +403,14 @@ class Handle:
             rc = self._L.bk_arena_advance(self._h, C.c_void_p(states_ptr), C.c_void_p(sets_ptr), n, C.byref(cfg),
                                           C.c_void_p(masks_ptr), C.c_void_p(rng_ptr), C.c_void_p(out_ptr), mem)
         self.check(rc, "bk_arena_advance")
+
+    def arena_step(self, states_ptr, sets_ptr, n, cfg: BkRolloutCfg, masks_ptr, quick_ptr, forced_ptr, rng_ptr,
+                   out_ptr, stop_ptr, mem):
+        with self._lock:
+            rc = self._L.bk_arena_step(self._h, C.c_void_p(states_ptr), C.c_void_p(sets_ptr), n, C.byref(cfg),
+                                       C.c_void_p(masks_ptr), C.c_void_p(quick_ptr), C.c_void_p(forced_ptr),
+                                       C.c_void_p(rng_ptr), C.c_void_p(out_ptr), C.c_void_p(stop_ptr), mem)
+        self.check(rc, "bk_arena_step")
 
     def advance(self, roots_ptr, n_roots, index_ptr, n, cfg: BkRolloutCfg, seeds_ptr, out_ptr, mem):
         with self._lock:

@@ -408,6 +408,290 @@ def _timed_search(agents, roots, sets, players):
     return mv, time.perf_counter() - t0
 
 
+def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]], idx: Sequence[int]):
+    """The search-seat agents of every game as run_single_game builds them (build_agent,
+    agent_seed), reduced to what the device driver carries: per MCTSAgent its search
+    parameters, Zobrist table and rollout agent's numpy MT19937 state; per FastMCTSAgent
+    its iteration count, exploration constant and random.Random state.  None if some agent
+    cannot be replayed on the device (wall-clock budgets, rollout agents the kernels do not
+    implement): run_games_batched then plays the host-staged loop."""
+    from ..mcts.mcts_agent import _search_policy
+    from ..mcts.zobrist import flat_keys
+    cfgs = {a.name: a for a in run_config.agents}
+    mcts, fast = [], []  # (game i, name, ...)
+    seat_agent = np.full((len(idx), 4), -1, np.int64)  # index into mcts / fast
+    seat_kind = np.zeros((len(idx), 4), np.int8)  # 0 random/heuristic, 1 mcts, 2 fast
+    for i, gi in enumerate(idx):
+        st = seats_of[i]
+        done: Dict[str, Tuple[int, int]] = {}
+        for p in range(4):
+            name = st[str(p + 1)]
+            c = cfgs[name]
+            kind = c.type.lower()
+            if kind not in _SEARCH_KINDS:
+                continue
+            if name not in done:
+                ad = build_agent(c, agent_seed(run_config.seed, gi, name))
+                if isinstance(ad, _SelectActionAdapter) and isinstance(ad.agent, MCTSAgent):
+                    a = ad.agent
+                    pol = _search_policy(a.rollout_agent) if a.rollout_backend == "search" else None
+                    if a.time_limit or pol is None:
+                        return None
+                    rs = a.rollout_agent.rng.get_state()
+                    mt = np.zeros(625, np.uint32)
+                    mt[:624], mt[624] = rs[1], rs[2]
+                    mcts.append({"i": i, "name": name, "iters": int(a.iterations), "roll": int(a.max_rollout_moves),
+                                 "c": float(a.exploration_constant), "tt": bool(a.use_transposition_table),
+                                 "policy": int(pol), "zob": flat_keys(a.zobrist_hash), "mt": mt})
+                    done[name] = (1, len(mcts) - 1)
+                elif isinstance(ad, (_FastMCTSAdapter, _GameplayFastMCTSAdapter)):
+                    if not ad.deterministic_time_budget:
+                        return None
+                    if isinstance(ad, _FastMCTSAdapter):
+                        fa = ad.agent
+                        budget = int(c.thinking_time_ms or max(int(fa.time_limit * 1000), 1))
+                    else:
+                        fa = ad.agent._agent
+                        budget = int(c.thinking_time_ms or 1)
+                    fast.append({"i": i, "name": name, "iters": max(1, int(round(ad.iterations_per_ms * budget))),
+                                 "c": float(fa.exploration_constant), "mt": fa._rng_words()})
+                    done[name] = (2, len(fast) - 1)
+                else:
+                    return None
+            seat_kind[i, p], seat_agent[i, p] = done[name]
+    return mcts, fast, seat_kind, seat_agent
+
+
+def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping[str, str]], gseeds: List[int],
+                      agents_dev, *, run_id: str, device: int, progress=None) -> List[Dict[str, Any]]:
+    """run_games_batched with every position, frontier table and agent stream resident in
+    HBM for the whole run.  A round is: bk_arena_step over all games (each first places
+    the move its stop seat chose last round, then plays random / heuristic seats to the
+    next search seat or the end; at a FastMCTS seat it also returns the root's legal count
+    and _quick_move_evaluation), one bk_mcts launch per MCTS parameter group on the
+    stopped positions (gathered on the device), one bk_fastmcts launch for the FastMCTS
+    seats; the chosen moves go back as forced moves (a move int, or a list index for
+    FastMCTS).  Only results, stop infos and forced moves cross PCIe each round, plus the
+    searched positions' 256 bytes for their root Zobrist hash.  Same agents, seeds, streams
+    and move order as run_single_game (arena_runner.py:578-777)."""
+    import torch
+
+    from .. import _native as N
+    from ..agents.fast_mcts_agent import _log_table
+    from ..gpu import BlokusGPU, empty_state, mcts_log_table, mcts_node_cap
+    from ..mcts.zobrist import hash_states
+    mcts, fast, seat_kind, seat_agent = agents_dev
+    n = len(idx)
+    cfgs = {a.name: a for a in run_config.agents}
+    gpu = BlokusGPU(device)
+    dev = torch.device("cuda", device)
+    prof = LAST_BATCH_PROFILE
+    prof.clear()
+    t0 = time.perf_counter()
+    masks = np.zeros(n, np.uint8)
+    quick = np.zeros(n, np.uint8)
+    rng = np.zeros((n, 16), np.uint32)
+    for i, gi in enumerate(idx):
+        for p in range(4):
+            name = seats[i][str(p + 1)]
+            kind = cfgs[name].type.lower()
+            if kind in ("random", "heuristic"):
+                rng[i, 4 * p:4 * p + 4] = N.mt_cursors([agent_seed(run_config.seed, gi, name)])[0]
+                if kind == "heuristic":
+                    masks[i] |= 1 << p
+            else:
+                masks[i] |= 16 << p
+                if seat_kind[i, p] == 2:
+                    quick[i] |= 1 << p
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    states_d = up(np.repeat(empty_state(), n).view(np.uint8).reshape(n, 256))
+    sets_d = up(N.fset_new(n).view(np.uint8).reshape(n, -1))
+    masks_d, quick_d, rng_d = up(masks), up(quick), up(rng.view(np.int32))
+    forced_d = torch.full((n,), -1, dtype=torch.int32, device=dev)
+    out_d = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    stop_d = torch.zeros((n, N.STOP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    # MCTS agents: Zobrist tables, rollout streams and TTs (one row each) on the device
+    am = len(mcts)
+    if am:
+        zob_h = np.stack([a["zob"] for a in mcts])
+        zob_d = up(zob_h.view(np.int64))
+        mtm_d = up(np.stack([a["mt"] for a in mcts]).view(np.int32))
+        it_max = max(a["iters"] for a in mcts)
+        cap = 1 << 12
+        while cap < 2 * (22 * it_max + 2):  # an agent searches at most once per piece
+            cap *= 2
+        ttk_d = torch.zeros((am, cap), dtype=torch.int64, device=dev)
+        ttv_d = torch.full((am, cap), float("nan"), dtype=torch.float64, device=dev)
+        ttc_d = torch.zeros(am, dtype=torch.int32, device=dev)
+        last_iters = np.zeros(am, np.int64)
+        log_tables = {}
+    mtf = np.stack([a["mt"] for a in fast]) if fast else np.zeros((0, 625), np.uint32)
+    per_agent = [{nm: {"moves": 0.0, "total_time_ms": 0.0, "total_simulations": 0.0, "moves_with_simulations": 0.0,
+                       "move_times_ms": []} for nm in set(seats[i].values())} for i in range(n)]
+    tot = np.zeros((n, 2), np.int64)  # turn_count, passes so far
+    results: List[Optional[Tuple[Any, int, int, bool]]] = [None] * n
+    active = np.ones(n, bool)
+    prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0,
+                uncertified_heuristic=0, device_driver=1)
+    forced = np.full(n, -1, np.int32)
+    stream = torch.cuda.current_stream(dev)
+    while active.any():
+        prof["rounds"] += 1
+        if progress is not None:
+            progress(prof["rounds"], int(active.sum()), prof)
+        ta = time.perf_counter()
+        gpu.arena_step(states_d, sets_d, masks_d, rng_d, quick_d, forced_d, out_d, stop_d,
+                       max_turns=run_config.max_turns)
+        res = out_d.cpu().numpy().view(N.RESULT_DTYPE).reshape(n)
+        stops = stop_d.cpu().numpy().view(N.STOP_DTYPE).reshape(n)
+        prof["advance_s"] += time.perf_counter() - ta
+        status = res["status"].astype(np.int64)
+        act = np.flatnonzero(active)
+        tot[act, 0] += res["turns"][act]
+        tot[act, 1] += res["passes"][act]
+        prof["uncertified_heuristic"] += int(np.count_nonzero(status[act] & N.STATUS_UNCERT))
+        bad = status[act] & ~(N.STATUS_CAP | N.STATUS_STOP | N.STATUS_UNCERT)
+        if bad.any():
+            j = int(act[np.flatnonzero(bad)[0]])
+            raise RuntimeError(f"game {idx[j]}: kernel status {int(status[j])}")
+        stop = act[(status[act] & N.STATUS_STOP) != 0]
+        fin = act[(status[act] & N.STATUS_STOP) == 0]
+        for i in fin.tolist():
+            r = res[i].copy()
+            turns, passes, truncated = int(tot[i, 0]), int(tot[i, 1]), False
+            if status[i] & N.STATUS_CAP:  # cut by max_turns: over or not (arena_runner.py:702)
+                st_i = states_d[i:i + 1].cpu().numpy().view(N.STATE_DTYPE)
+                if int(gpu.has_moves(st_i)[0]) != 0:
+                    truncated = True
+                else:
+                    turns -= int(r["reserved"][0])
+                    passes -= int(r["reserved"][0])
+            results[i] = (r, turns, passes, truncated)
+            active[i] = False
+        forced[:] = -1
+        if len(stop):
+            pl = (np.zeros(len(stop), np.int64))
+            cur = states_d.index_select(0, up(stop))[:, 241].cpu().numpy().astype(np.int64) & 3
+            pl[:] = cur
+            kind = seat_kind[stop, pl]
+            ag = seat_agent[stop, pl]
+            nleg = stops["n_legal"][stop].astype(np.int64)
+            # ---- MCTS seats (select_action answers a single legal move without a search)
+            sel = np.flatnonzero(kind == 1)
+            if len(sel):
+                tm = time.perf_counter()
+                one = sel[nleg[sel] == 1]
+                for k in one.tolist():
+                    i, a = int(stop[k]), int(ag[k])
+                    forced[i] = N.FORCE_INDEX
+                    e = per_agent[i][mcts[a]["name"]]
+                    e["total_simulations"] += float(last_iters[a])  # the agent's stale iterations_run
+                    e["moves_with_simulations"] += 1
+                multi = sel[nleg[sel] > 1]
+                groups: Dict[Tuple, List[int]] = {}
+                for k in multi.tolist():
+                    a = mcts[int(ag[k])]
+                    groups.setdefault((a["iters"], a["roll"], a["c"], a["tt"], a["policy"]), []).append(k)
+                for (iters, roll, c, use_tt, policy), ks in groups.items():
+                    ks = np.array(ks)
+                    gi_d = up(stop[ks])
+                    aid = ag[ks]
+                    aid_d = up(aid)
+                    roots_d = states_d.index_select(0, gi_d).contiguous()
+                    sets_g = sets_d.index_select(0, gi_d).contiguous()
+                    roots_h = roots_d.cpu().numpy().view(N.STATE_DTYPE).reshape(len(ks))
+                    rh = hash_states(roots_h, zob_h[aid])
+                    players = up(pl[ks].astype(np.uint8))
+                    mt_g = mtm_d.index_select(0, aid_d).contiguous()
+                    if iters not in log_tables:
+                        log_tables[iters] = up(mcts_log_table(iters))
+                    nodes = torch.empty((len(ks), mcts_node_cap(iters) * N.MCTS_NODE_DTYPE.itemsize),
+                                        dtype=torch.uint8, device=dev)
+                    o_d = torch.zeros((len(ks), N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+                    tk = tv = tc = None
+                    if use_tt:
+                        tk, tv, tc = (ttk_d.index_select(0, aid_d), ttv_d.index_select(0, aid_d),
+                                      ttc_d.index_select(0, aid_d))
+                    gpu.mcts_device(roots_d, sets_g, players, up(rh.view(np.int64)), zob_d, aid_d.to(torch.int32),
+                                    mt_g, log_tables[iters], nodes, o_d, iterations=iters, tt_keys=tk, tt_vals=tv,
+                                    tt_count=tc, max_rollout_moves=roll, exploration=c, rollout_policy=policy)
+                    mtm_d.index_copy_(0, aid_d, mt_g)
+                    if use_tt:
+                        ttk_d.index_copy_(0, aid_d, tk)
+                        ttv_d.index_copy_(0, aid_d, tv)
+                        ttc_d.index_copy_(0, aid_d, tc)
+                    o = o_d.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(len(ks))
+                    prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
+                    its = o["iterations_run"].astype(np.int64)
+                    last_iters[aid] = its
+                    for k, a, mv, it in zip(ks.tolist(), aid.tolist(), o["best_move"].tolist(), its.tolist()):
+                        i = int(stop[k])
+                        forced[i] = int(mv)
+                        e = per_agent[i][mcts[a]["name"]]
+                        e["total_simulations"] += float(it)
+                        e["moves_with_simulations"] += 1
+                    if use_tt and int(tc.max().item()) > 500000:  # mcts_agent.py:338-339
+                        full = aid[(tc.cpu().numpy() > 500000)]
+                        ttk_d[up(full)] = 0
+                        ttv_d[up(full)] = float("nan")
+                        ttc_d[up(full)] = 0
+                prof["mcts_s"] += time.perf_counter() - tm
+            # ---- FastMCTS seats (think: a single legal move draws nothing)
+            sel = np.flatnonzero(kind == 2)
+            if len(sel):
+                tf = time.perf_counter()
+                for k in sel[nleg[sel] == 1].tolist():
+                    forced[int(stop[k])] = N.FORCE_INDEX
+                multi = sel[nleg[sel] > 1]
+                groups = {}
+                for k in multi.tolist():
+                    groups.setdefault(fast[int(ag[k])]["c"], []).append(k)
+                for ce, ks in groups.items():
+                    ks = np.array(ks)
+                    aid = ag[ks]
+                    counts = [fast[int(a)]["iters"] for a in aid]
+                    mt = np.ascontiguousarray(mtf[aid])
+                    r = gpu.fastmcts(nleg[ks].tolist(), counts, stops["quick_reward"][stop[ks]].tolist(), mt,
+                                     _log_table(max(counts) + 1), ce)
+                    mtf[aid] = mt
+                    for k, a, it_run, bi, nch, it in zip(ks.tolist(), aid.tolist(), r["iterations"].tolist(),
+                                                          r["best_index"].tolist(), r["n_children"].tolist(), counts):
+                        i = int(stop[k])
+                        j = int(stops["quick_index"][i]) if it_run < 5 else (int(bi) if nch > 0 else 0)
+                        forced[i] = N.FORCE_INDEX | j
+                        e = per_agent[i][fast[a]["name"]]
+                        e["total_simulations"] += it
+                        e["moves_with_simulations"] += 1
+                prof["fast_s"] += time.perf_counter() - tf
+        forced_d.copy_(torch.from_numpy(forced))
+    stream.synchronize()
+    dt = time.perf_counter() - t0
+    prof["total_s"] = dt
+    prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"]
+    if prof["uncertified_heuristic"]:
+        warnings.warn(f"run_games_batched: {prof['uncertified_heuristic']} HeuristicAgent draw(s) fell within 2^-40 "
+                      "of a probability boundary (choice not certified equal to the reference's on every host)",
+                      RuntimeWarning, stacklevel=2)
+    final = states_d.cpu().numpy().view(N.STATE_DTYPE).reshape(n)
+    out = []
+    for i, gi in enumerate(idx):
+        r, turns, passes, truncated = results[i]
+        scores = {p + 1: int(r["scores"][p]) for p in range(4)}
+        winners = [p for p, sc in scores.items() if sc == max(scores.values())]
+        pa = per_agent[i]
+        for p in range(4):
+            pa[seats[i][str(p + 1)]]["moves"] += float(bin(int(final["used"][i, p])).count("1"))
+        total_moves = max(sum(e["moves"] for e in pa.values()), 1.0)
+        for e in pa.values():
+            e["total_time_ms"] = dt / n * (e["moves"] / total_moves) * 1000.0
+        _finish_stats(pa)
+        out.append(_record(run_id=run_id, game_index=gi, game_seed=gseeds[i], run_config=run_config, seats=seats[i],
+                           scores=scores, winner_ids=winners, is_tie=len(winners) > 1,
+                           moves_made=int(final["move_count"][i]), turn_count=turns, passes=passes, invalid=0,
+                           duration=dt / n, truncated=truncated, per_agent=pa, error=None))
+    return out
+
+
 def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
                       device: int = 0, progress=None) -> List[Dict[str, Any]]:
     """Mixed seatings (Random / Heuristic / MCTS / FastMCTS, config 4) in lockstep batches:
@@ -428,6 +712,19 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     if n == 0:
         return []
     cfgs = {a.name: a for a in run_config.agents}
+    if os.environ.get("BK_ARENA_DEVICE", "1") != "0":
+        seats_d, gseeds_d = [], []
+        for gi in idx:
+            gs = game_seed_from_run_seed(run_config.seed, gi)
+            st = seat_assignment_for_game(run_config.agent_names, gi, gs, run_config.seat_policy)
+            if not _batchable(run_config, st):
+                raise ValueError(f"game {gi}: seating {st} cannot be batched; use run_single_game")
+            seats_d.append(st)
+            gseeds_d.append(gs)
+        ag = _device_agents(run_config, seats_d, idx)
+        if ag is not None:
+            return _run_games_device(run_config, idx, seats_d, gseeds_d, ag, run_id=run_id, device=device,
+                                     progress=progress)
     gpu = BlokusGPU(device)
     t0 = time.perf_counter()
     states = np.repeat(empty_state(), n)

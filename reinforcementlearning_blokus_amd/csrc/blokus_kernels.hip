@@ -68,6 +68,12 @@
 #define BK_TU 0
 #endif
 #define BK_DEF(u) (BK_TU == 0 || BK_TU == (u))
+// 1: the stencil skips anchor rows no lane of the wave can use (live_anchor_rows) --
+// measured no faster: the per-row branches cost the kernel spills;
+// 0: the round-3 stencil (every anchor row), a build for the A/B measurement
+#ifndef BK_ROWSKIP_BUILD
+#define BK_ROWSKIP_BUILD 0
+#endif
 
 // Section timers (diagnostic build only, -DBK_SECTION_PROF): per-wave shader-clock
 // cycles spent in each section of a kernel's loop, summed over waves into
@@ -301,9 +307,11 @@ struct StencilClass {
         for (int r = 0; r < NR; ++r) {
             // test the row's bit here (an opaque copy per row: hoisted out of the entry
             // loop, the 20 row conditions would take 40 SGPRs and spill)
+#if BK_ROWSKIP_BUILD
             uint32_t lv = live;
             asm volatile("" : "+s"(lv));
             if (!((lv >> r) & 1u)) continue;
+#endif
             const uint64_t t0 = tv<0>(P, r, sh);
             f(r, fold<1>(P, r, sh, lo(t0), hi(t0)));
             __builtin_amdgcn_sched_barrier(0);
@@ -507,9 +515,14 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     int tb0 = 0;
     asm volatile("" : "+s"(tb0));
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
+#if BK_ROWSKIP_BUILD
     LiveRows L = live_anchor_rows(P);
     if (!rowskip)  // uniform (tuning A/B: BK_ROWSKIP=0)
         for (int h = 0; h < 5; ++h) L.lh[h] = ~0u;
+#else
+    (void)rowskip;
+    const LiveRows L{{~0u, ~0u, ~0u, ~0u, ~0u}};
+#endif
 #ifdef BK_STENCIL_LITERAL
     (void)tb0;
 #define BK_COUNT_ENTRY(PIECE, G, H, ...) t += count_entry<STORE, PIECE, G, H, __VA_ARGS__>(P, avail, cl);
@@ -1888,6 +1901,7 @@ __device__ __forceinline__ void heur_walk_frontier(int gs, const uint32_t (&ok)[
 // counter[2] of a handle: sticky error bits of device-path launches, reported (and
 // cleared) by bk_synchronize
 #define BK_STATUS_CAP 8u     // bk_result.status: arena run stopped by the turn cap
+#define BK_STATUS_BADFORCE 64u  // bk_arena_step: the forced move is not legal here (game stopped)
 // BK_STATUS_STOP (32, include/blokus_hip.h): bk_arena_advance stopped at a stop seat
 #define BK_STICKY_GUARD 1u  // a persistent kernel's iteration guard tripped: results incomplete
 #define BK_STICKY_ROOT 2u   // a root_index entry outside [0, n_roots)
@@ -1915,6 +1929,9 @@ struct RolloutArgs {
                                // < long_slots pull the rest from the counter (whole waves)
     uint32_t long_slots;
     int32_t rowskip;           // 1: skip anchor rows no lane of the wave can use (live_anchor_rows)
+    const uint8_t* quick_masks;  // bk_arena_step: per game, bits 0-3 FastMCTS stop seats (stop_out)
+    const int32_t* forced;       // bk_arena_step: per game, the stop seat's chosen move (or -1)
+    bk_stop_info* stop_out;      // bk_arena_step: per game, the FastMCTS root inputs at a stop
 };
 
 // four per-player scalars (kept as separate SSA values: an array indexed by a
@@ -1946,6 +1963,7 @@ struct Game {
     uint32_t smask;     // stop seats (bk_arena_advance)
     int32_t cap;        // turn / ply budget of this game in this launch
     uint32_t turns0, passes0;  // bk_arena_advance: the game's counts before this launch
+    int32_t forced;     // bk_arena_step: the stop seat's move to place first (-1: none)
 };
 
 __device__ __forceinline__ int board_score_q(const Game& g, int q) {  // q static
@@ -2176,6 +2194,7 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
     g.turns0 = a.seat_masks ? s->reserved[0] : 0u;
     g.passes0 = a.seat_masks ? s->reserved[1] : 0u;
     g.cap = a.cfg.max_plies - (int32_t)g.turns0;  // arena_runner max_turns over the whole game
+    g.forced = a.forced ? a.forced[pid] : -1;
     if (a.rng_io) {  // seats' streams carried over from the previous call
 #pragma unroll
         for (int w = 0; w < 16; ++w) slab.word(SLAB_RNG_BASE + w) = a.rng_io[(size_t)pid * 16 + w];
@@ -2240,6 +2259,63 @@ __device__ __forceinline__ double draw_double(const RolloutArgs& a, Game& g, con
     }
     g.draws += 2;
     return ((double)(x0 >> 5) * 67108864.0 + (double)(x1 >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// bk_arena_step: the FastMCTSAgent root inputs of game g stopped at FastMCTS seat p
+// (agents/fast_mcts_agent.py:260-298): the legal-move count, and _quick_move_evaluation --
+// of the first 3 moves by piece id descending (a stable sort of the list: the first moves,
+// in list order, of the largest pieces with moves), the first nearest the centre by
+// |anchor_row - 9.5| + |anchor_col - 9.5| -- as its list index and its reward
+// pid * 0.1 + (20 - dist) * 0.05 (CPython float ops, no fused multiply-add).  The counts
+// are recomputed (the LDS area held other data since); locate overwrites the rows' C
+// half, so the rows are rewritten before each of the (at most 3) locates.
+__device__ __forceinline__ void stop_info(const RolloutArgs& a, const Game& g, const Planes& P, uint32_t* my, int lane,
+                                       uint2* rows_lds, const bk_fset* fs, int p, uint32_t avail, uint32_t total) {
+    bk_stop_info si;
+    si.n_legal = (int32_t)total;
+    si.quick_index = 0;
+    si.quick_reward = 0.0;
+    if (a.quick_masks && ((a.quick_masks[g.pid] >> p) & 1u)) {
+        (void)movegen_counts<true>(P, avail, my, lane, a.rowskip != 0);
+        // list positions of the first 3 moves by piece descending: orientations are
+        // piece-major, so piece P's moves are one run [s, s + c) of the list
+        uint32_t k3[3] = {0u, 0u, 0u}, suf = 0u, cp = 0u;
+        int n3 = 0;
+#pragma unroll 1
+        for (int gg = BK_NUM_ORIENTS - 1; gg >= 0 && n3 < 3; --gg) {
+            cp += (my[(gg / 3) * WAVE + lane] >> (10 * (gg % 3))) & 0x3FFu;
+            const uint32_t piece = kInfo[gg] & 0xFFu;
+            if (gg == 0 || (kInfo[gg - 1] & 0xFFu) != piece) {  // first orientation of the piece
+                const uint32_t s0 = total - suf - cp;
+                for (uint32_t j = 0; j < cp && n3 < 3; ++j) k3[n3++] = s0 + j;
+                suf += cp;
+                cp = 0u;
+            }
+        }
+        uint32_t kk3[3] = {0u, 0u, 0u};
+        int g3[3] = {0, 0, 0};
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (i < n3) g3[i] = pick_orient(my, lane, k3[i], kk3[i]);  // before the rows overwrite the counts
+        double best = 0.0;
+        int q = -1;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (i >= n3) continue;
+#pragma unroll
+            for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
+            int ar, ac;
+            locate_move_frontier(g3[i], kk3[i], rows_lds, fs->key[p], fs->mask[p], ar, ac);
+            const double d = __dadd_rn(fabs((double)ar - 9.5), fabs((double)ac - 9.5));
+            if (q < 0 || d < best) { best = d; q = i; }  // min(): the first nearest
+        }
+        if (q >= 0) {
+            si.quick_index = (int32_t)k3[q];
+            si.quick_reward = __dadd_rn(__dmul_rn((double)(kInfo[g3[q]] & 0xFFu), 0.1),
+                                        __dmul_rn(__dadd_rn(20.0, -best), 0.05));
+        }
+    }
+    a.stop_out[g.pid] = si;
 }
 
 // heuristic-policy kernels: 128-lane blocks, per lane 84 LDS dwords ({B, C} rows, then
@@ -2337,7 +2413,9 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         int gs = 0;
         uint32_t kk = 0;
         // heuristic policy (HEUR kernels): this lane's mover plays HeuristicAgent
-        const bool heur = HEUR && !idle && ((g.hmask >> p) & 1u);
+        // bk_arena_step: this ply places the stop seat's chosen move (HEUR kernels only)
+        const bool forced = HEUR && !idle && g.forced >= 0;
+        const bool heur = HEUR && !idle && !forced && ((g.hmask >> p) & 1u);
         double h_target = 0.0, h_R = 0.0, h_total = 0.0;
         uint32_t h_ok[20];
         bool h_unc = false;
@@ -2348,8 +2426,15 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane, a.rowskip != 0);
                 if (!idle && !heur) {
                     total = t;
-                    // (a stop seat draws nothing: bk_arena_advance hands its turn back)
-                    if (t > 0u && !((g.smask >> p) & 1u)) gs = pick_orient(my, lane, draw_index(a, g, slab, slot, t), kk);
+                    // (a stop seat draws nothing: bk_arena_advance hands its turn back; a
+                    // forced list index k picks its move as a draw of k would)
+                    if (forced) {
+                        gs = -1;
+                        if ((g.forced & BK_FORCE_INDEX) && (uint32_t)(g.forced & ~BK_FORCE_INDEX) < t)
+                            gs = pick_orient(my, lane, (uint32_t)(g.forced & ~BK_FORCE_INDEX), kk);
+                    } else if (t > 0u && !((g.smask >> p) & 1u)) {
+                        gs = pick_orient(my, lane, draw_index(a, g, slab, slot, t), kk);
+                    }
                 }
             }
             if (__builtin_amdgcn_ballot_w64(heur)) {
@@ -2374,10 +2459,25 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         }
         SECT(2);
         if (idle) continue;
-        if (FR && total > 0u && ((g.smask >> p) & 1u)) {  // a search seat is to move: hand the game back
+        if (FR && total > 0u && ((g.smask >> p) & 1u) && !forced) {  // a search seat is to move: hand the game back
+            if constexpr (HEUR) {
+                if (a.stop_out) stop_info(a, g, P, my, lane, rows_lds, &a.fslab[slot].s, p, avail, total);
+            }
             g.status |= BK_STATUS_STOP;
             finish_game<FR>(a, g, slab, slot);
             continue;
+        }
+        bool fmove = false;  // forced as a move int (bk_mcts best_move): no pick, no locate
+        if constexpr (HEUR) {
+            if (forced) {
+                fmove = !(g.forced & BK_FORCE_INDEX);
+                const bool bad = total == 0u || (fmove ? (g.forced / 400 >= BK_NUM_ORIENTS) : gs < 0);
+                if (bad) {
+                    g.status |= BK_STATUS_BADFORCE;
+                    finish_game<FR>(a, g, slab, slot);
+                    continue;
+                }
+            }
         }
         if (total == 0u) {
             if (arena) {
@@ -2400,7 +2500,13 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         int ar, ac;
         if constexpr (FR) {
             const bk_fset* fs = &a.fslab[slot].s;
-            if (heur && gs < 0) {
+            if (fmove) {  // the search's move: legal iff its anchor is in the orientation's legal set
+                gs = g.forced / 400;
+                ar = (g.forced % 400) / 20;
+                ac = g.forced % 20;
+                locate_pass1(gs, rows_lds);
+                if (!((rows_lds[ar * WAVE].y >> ac) & 1u)) ar = -1;
+            } else if (heur && gs < 0) {
                 ar = -1;
                 ac = 0;
             } else if (heur) {
@@ -2415,10 +2521,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             locate_move_lds(gs, kk, rows_lds, ar, ac);
         }
         if (HEUR && ar < 0) {  // cannot happen (counts > 0 means e sums > 0); never write off the board
-            g.status |= BK_STATUS_UNCERT;
+            g.status |= forced ? BK_STATUS_BADFORCE : BK_STATUS_UNCERT;
             finish_game<FR>(a, g, slab, slot);
             continue;
         }
+        if constexpr (HEUR) g.forced = -1;  // consumed
         SECT(4);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
         const uint32_t info = kInfo[gs];
@@ -4075,6 +4182,7 @@ struct bk_handle_s {
     void* d_fslab = nullptr; size_t d_fslab_cap = 0; // frontier: per-slot records
     void* d_mc = nullptr; size_t d_mc_cap = 0;       // bk_mcts: staged inputs/outputs
     void* d_mclane = nullptr; size_t d_mclane_cap = 0; // bk_mcts: per-slot records
+    void* d_step = nullptr; size_t d_step_cap = 0;   // bk_arena_step: staged extras
     uint32_t* d_counter = nullptr;
     int num_cu = 0;
     int rollout_blocks_per_cu = 0;
@@ -4179,7 +4287,7 @@ int bk_destroy(bk_handle h) {
     (void)hipSetDevice(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_mc, h->d_mclane, h->d_counter};
+                    h->d_mc, h->d_mclane, h->d_step, h->d_counter};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -4383,7 +4491,8 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                            int32_t n_playouts, const bk_rollout_cfg* cfg, const uint32_t* compat_seeds,
                            bk_result* out, bk_state* out_states, int mem, const bk_fset* root_sets = nullptr,
                            bk_fset* out_sets = nullptr, const uint8_t* seat_masks = nullptr,
-                           uint32_t* rng_io = nullptr) {
+                           uint32_t* rng_io = nullptr, const uint8_t* quick_masks = nullptr,
+                           const int32_t* forced = nullptr, bk_stop_info* stop_out = nullptr) {
     if (!h || !roots || !cfg || n_roots <= 0 || n_playouts < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
         return set_err(h, BK_EINVAL, "bk_rollout: invalid arguments%s", "");
     if (cfg->semantics != BK_SEM_ARENA && cfg->semantics != BK_SEM_ROLLOUT && cfg->semantics != BK_SEM_ADVANCE)
@@ -4428,12 +4537,36 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         rc = stage_in(h, root_sets, sizeof(bk_fset) * (size_t)n_roots, mem, &d_rsets, &h->d_fin, &h->d_fin_cap);
         if (rc) return rc;
     }
-    void *d_masks = nullptr, *d_rng = nullptr;
-    if (seat_masks) {  // bk_arena_advance
+    void *d_masks = nullptr, *d_rng = nullptr, *d_quick = nullptr, *d_forced = nullptr;
+    bk_stop_info* d_stop = stop_out;
+    if (seat_masks) {  // bk_arena_advance / bk_arena_step
         rc = stage_in(h, seat_masks, (size_t)n_playouts, mem, &d_masks, &h->d_aux, &h->d_aux_cap);
         if (rc) return rc;
         rc = stage_in(h, rng_io, sizeof(uint32_t) * 16 * (size_t)n_playouts, mem, &d_rng, &h->d_aux2, &h->d_aux2_cap);
         if (rc) return rc;
+        // bk_arena_step's extras share one staging buffer (host mode): quick masks,
+        // forced moves, stop infos at 16-byte aligned offsets
+        const size_t qb = quick_masks ? ((size_t)n_playouts + 15) & ~(size_t)15 : 0;
+        const size_t fb = forced ? (sizeof(int32_t) * (size_t)n_playouts + 15) & ~(size_t)15 : 0;
+        const size_t sb = stop_out ? sizeof(bk_stop_info) * (size_t)n_playouts : 0;
+        if (mem == BK_MEM_HOST && (qb + fb + sb)) {
+            rc = grow(h, &h->d_step, &h->d_step_cap, qb + fb + sb);
+            if (rc) return rc;
+            char* base = (char*)h->d_step;
+            if (quick_masks) {
+                d_quick = base;
+                HIPCHK(h, hipMemcpyAsync(d_quick, quick_masks, (size_t)n_playouts, hipMemcpyHostToDevice, h->cur));
+            }
+            if (forced) {
+                d_forced = base + qb;
+                HIPCHK(h, hipMemcpyAsync(d_forced, forced, sizeof(int32_t) * (size_t)n_playouts,
+                                         hipMemcpyHostToDevice, h->cur));
+            }
+            if (stop_out) d_stop = (bk_stop_info*)(base + qb + fb);
+        } else {
+            d_quick = const_cast<uint8_t*>(quick_masks);
+            d_forced = const_cast<int32_t*>(forced);
+        }
     }
     bk_result* d_out = out;
     bk_state* d_states = out_states;
@@ -4476,6 +4609,9 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                   (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr,
                   (const uint8_t*)d_masks, (uint32_t*)d_rng, fr ? 0 : 2, 0u, 1};
     if (const char* env = getenv("BK_ROWSKIP")) a.rowskip = atoi(env);  // tuning A/B
+    a.quick_masks = (const uint8_t*)d_quick;
+    a.forced = (const int32_t*)d_forced;
+    a.stop_out = d_stop;
     // Playout hand-out.  Config 3 has 1.33 playouts per resident slot: pulled per lane
     // from one counter (handout 0), the extra third lands on lanes of EVERY wave, and each
     // wave then runs a second playout length with a third of its lanes; given to whole
@@ -4519,6 +4655,9 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
                                      hipMemcpyDeviceToHost, h->cur));
         if (rng_io)
             HIPCHK(h, hipMemcpyAsync(rng_io, d_rng, sizeof(uint32_t) * 16 * (size_t)n_playouts,
+                                     hipMemcpyDeviceToHost, h->cur));
+        if (stop_out)
+            HIPCHK(h, hipMemcpyAsync(stop_out, d_stop, sizeof(bk_stop_info) * (size_t)n_playouts,
                                      hipMemcpyDeviceToHost, h->cur));
         uint32_t ctr[4];
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
@@ -4564,6 +4703,25 @@ int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, co
     if (n == 0) return BK_OK;
     return launch_playouts(h, states, n, nullptr, n, cfg, nullptr, out, states, mem, sets, sets, seat_masks,
                            rng_state);
+}
+
+int bk_arena_step(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const bk_rollout_cfg* cfg,
+                  const uint8_t* seat_masks, const uint8_t* quick_masks, const int32_t* forced, uint32_t* rng_state,
+                  bk_result* out, bk_stop_info* stop_out, int mem) {
+    if (!h || !states || !sets || !cfg || !seat_masks || !rng_state || !out || n < 0)
+        return set_err(h, BK_EINVAL, "bk_arena_step: invalid arguments%s", "");
+    if (cfg->semantics != BK_SEM_ARENA || cfg->order != BK_ORDER_FRONTIER || cfg->rng != BK_RNG_NUMPY_MT ||
+        cfg->seats_share_stream)
+        return set_err(h, BK_EINVAL, "bk_arena_step: needs ARENA, FRONTIER order, NUMPY_MT per-seat streams%s", "");
+    if (quick_masks && !stop_out)
+        return set_err(h, BK_EINVAL, "bk_arena_step: quick_masks goes with stop_out%s", "");
+    if (mem == BK_MEM_HOST && forced)
+        for (int32_t i = 0; i < n; ++i)
+            if (forced[i] < -1 || (forced[i] >= 0 && !(forced[i] & BK_FORCE_INDEX) && forced[i] >= BK_NUM_ORIENTS * 400))
+                return set_err(h, BK_EINVAL, "bk_arena_step: forced move out of range%s", "");
+    if (n == 0) return BK_OK;
+    return launch_playouts(h, states, n, nullptr, n, cfg, nullptr, out, states, mem, sets, sets, seat_masks,
+                           rng_state, quick_masks, forced, stop_out);
 }
 
 int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_sets, int32_t n_roots,

@@ -271,6 +271,30 @@ class BlokusGPU:
                                   rng_state.ctypes.data, out.ctypes.data, N.MEM_HOST)
         return out
 
+    def arena_step(self, states, sets, seat_masks, rng_state, quick_masks, forced, out, stop_out, *,
+                   max_turns: int = 2500):
+        """bk_arena_step on device tensors, in place (BK_MEM_DEVICE, torch's current
+        stream): states uint8[n,256], sets uint8[n,2080], seat_masks / quick_masks uint8[n],
+        forced int32[n], rng_state int32[n,16], out uint8[n,32], stop_out uint8[n,16]
+        (STOP_DTYPE).  No position or table crosses PCIe (config 4's device driver)."""
+        import torch
+        n = states.shape[0]
+        for t, name, dt, shape in ((states, "states", torch.uint8, (n, 256)),
+                                   (sets, "sets", torch.uint8, (n, N.FSET_DTYPE.itemsize)),
+                                   (seat_masks, "seat_masks", torch.uint8, (n,)),
+                                   (quick_masks, "quick_masks", torch.uint8, (n,)),
+                                   (forced, "forced", torch.int32, (n,)), (rng_state, "rng_state", torch.int32, (n, 16)),
+                                   (out, "out", torch.uint8, (n, 32)),
+                                   (stop_out, "stop_out", torch.uint8, (n, N.STOP_DTYPE.itemsize))):
+            _check_device_tensor(t, name, dt, shape, self.device)
+        cfg = N.BkRolloutCfg(N.SEM_ARENA, N.ORDER_FRONTIER, N.RNG_NUMPY_MT, int(max_turns), 0, 0, 0)
+        if n == 0:
+            return
+        self._stream_from_torch()
+        self.handle.arena_step(states.data_ptr(), sets.data_ptr(), n, cfg, seat_masks.data_ptr(),
+                               quick_masks.data_ptr(), forced.data_ptr(), rng_state.data_ptr(), out.data_ptr(),
+                               stop_out.data_ptr(), N.MEM_DEVICE)
+
     # ------------------------------------------------------------------ positions
     def advance(self, roots, n: int, plies: int, *, seed: int = 0, root_index=None, stream_base: int = 0):
         """Play `plies` uniformly random moves (naive order, Philox stream) from each root
