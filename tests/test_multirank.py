@@ -220,3 +220,24 @@ def test_gloo_two_ranks_config5_searches():
     ref = _search_records(range(n_total))
     assert np.array_equal(got, ref)
     assert len(set(ref.view(np.int32)[:, 1].tolist())) > 1  # real, differing searches
+
+
+def test_bench_roofline_counters_scale_with_launch_size():
+    """bench.py rooflines come from per-unit PMC counters (profiles/traffic_latest.json,
+    tools/summarize_prof.py) scaled by the line's own units per launch: a launch with
+    twice the work is charged twice the bytes and VALU instructions, whatever launch size
+    the profile was taken at (config 5's --chunk, config 4's per-round searches)."""
+    import json
+
+    import bench
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for kernel, entry in json.load(open(os.path.join(ROOT, "profiles", "traffic_latest.json")))["kernels"].items():
+        u = entry["units_per_launch"]
+        b1, v1, src = bench.traffic_for(kernel, u)
+        b2, v2, _ = bench.traffic_for(kernel, 2 * u)
+        assert abs(b1 - entry["bytes_per_launch"]) <= 1e-6 * entry["bytes_per_launch"]
+        assert abs(b2 - 2 * b1) <= 1e-6 * b1
+        if v1 is not None:
+            assert abs(v2 - 2 * v1) <= 1e-6 * v1
+        assert src["pmc"] == entry["source"] and os.path.exists(os.path.join(ROOT, entry["source"]))
+    assert bench.traffic_for("no_such_kernel", 1) == (None, None, None)
