@@ -620,16 +620,18 @@ def run_config4(args, world, rank, local, dist):
                                      "measured in the build container (SURVEY.md 6); MCTS seats are slower"},
     }
     if not args.no_cpu_baseline and world == 1:
-        cb = cpu_baseline_config4(cfg, args.cpu_seconds)
+        cb = cpu_baseline_config4(cfg, args.cpu_seconds, recs)
         cb["gpu_over_cpu"] = line["value"] / cb["value"]
         line["cpu_baseline"] = cb
     return line
 
 
-def cpu_baseline_config4(cfg, seconds):
+def cpu_baseline_config4(cfg, seconds, gpu_recs=None):
     """oracle/blokus_oracle.c or_arena4_game on this host's cores: the first games of the
     same run (seat assignment and agent seeds of game i from the run config, as the GPU
-    run derives them), one game per thread at a time, as many as fit in about `seconds`."""
+    run derives them), one game per thread at a time, as many as fit in about `seconds`.
+    or_arena4_game replays the reference's records (tests/test_oracle_arena.py), so its
+    final scores are compared with the GPU run's records of the same games."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import pyoracle as O
@@ -643,7 +645,7 @@ def cpu_baseline_config4(cfg, seconds):
         seats = seat_assignment_for_game(cfg.agent_names, gi, game_seed_from_run_seed(cfg.seed, gi), cfg.seat_policy)
         names = [seats[str(p + 1)] for p in range(4)]
         return O.arena4_game([kinds[n] for n in names], [agent_seed(cfg.seed, gi, n) for n in names],
-                             CONFIG4_AGENTS[2]["params"]["iterations"], 1000)[0]
+                             CONFIG4_AGENTS[2]["params"]["iterations"], 1000)
 
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL inside or_arena4_game
@@ -652,12 +654,20 @@ def cpu_baseline_config4(cfg, seconds):
     n = max(threads, int(threads * seconds / max(dt1, 1e-3)) // threads * threads)
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
-        plies = sum(ex.map(game, range(n)))
+        games = list(ex.map(game, range(n)))
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "games/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
-            "host": cpu, "sample": f"the run's first {n} games ({plies} plies), oracle/blokus_oracle.c "
-                                   f"or_arena4_game (MCTS 64 iterations with HeuristicAgent rollouts, FastMCTS 1,000 "
-                                   f"iterations), {threads} threads, {dt:.1f} s"}
+    plies = sum(g[0] for g in games)
+    out = {"value": n / dt, "unit": "games/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+           "host": cpu, "sample": f"the run's first {n} games ({plies} plies), oracle/blokus_oracle.c "
+                                  f"or_arena4_game (MCTS 64 iterations with HeuristicAgent rollouts, FastMCTS 1,000 "
+                                  f"iterations), {threads} threads, {dt:.1f} s"}
+    if gpu_recs is not None:
+        by = {r["game_index"]: r for r in gpu_recs}
+        cmp = [gi for gi in range(n) if gi in by]
+        out["same_games_compared"] = len(cmp)
+        out["same_games_bit_identical"] = all(
+            [by[gi]["final_scores"][str(p + 1)] for p in range(4)] == list(games[gi][1]) for gi in cmp)
+    return out
 
 
 # ------------------------------------------------------------------ config 2

@@ -1125,7 +1125,7 @@ int or_arena4_game(const int32_t* kinds4, const uint32_t* seeds4, int mcts_iters
     or_init();
     or_board* b = (or_board*)malloc(sizeof(or_board));
     or_board_init(b);
-    or_mt rng[4];
+    or_mt rng[4], fast_rng[4];
     uint64_t* ztab[4] = {0, 0, 0, 0};
     uint64_t* tkeys[4] = {0, 0, 0, 0};
     double* tvals[4] = {0, 0, 0, 0};
@@ -1133,6 +1133,7 @@ int or_arena4_game(const int32_t* kinds4, const uint32_t* seeds4, int mcts_iters
     const int tcap = 1 << 16;
     for (int p = 0; p < 4; ++p) {
         or_mt_seed_numpy(&rng[p], seeds4[p]);
+        py_seed_int(&fast_rng[p], (int64_t)seeds4[p]);
         if (kinds4[p] == 2) {
             ztab[p] = (uint64_t*)malloc(sizeof(uint64_t) * 2088);
             or_zobrist_table(seeds4[p], ztab[p]);
@@ -1178,7 +1179,8 @@ int or_arena4_game(const int32_t* kinds4, const uint32_t* seeds4, int mcts_iters
             } else {
                 int32_t nodes, tm[1], tv[1];
                 double tq[1];
-                or_fastmcts(b, p, (int64_t)seeds4[p] + turns, fast_iters, BK_ORDER_FRONTIER, &mv, &nodes, tm, tv, tq, 1);
+                /* the agent's one random.Random(seed) stream across its moves (fast_mcts_agent.py:99) */
+                or_fastmcts_mt(b, p, &fast_rng[p], fast_iters, BK_ORDER_FRONTIER, &mv, &nodes, tm, tv, tq, 1);
             }
         }
         if (mv < 0) { b->cur = (b->cur + 1) & 3; continue; }

@@ -479,6 +479,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     from .. import _native as N
     from ..agents.fast_mcts_agent import _log_table
     from ..gpu import BlokusGPU, empty_state, mcts_log_table, mcts_node_cap
+    from ..mcts.mcts_agent import SEARCH_TOTALS
     from ..mcts.zobrist import hash_states
     mcts, fast, seat_kind, seat_agent = agents_dev
     n = len(idx)
@@ -623,6 +624,13 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                     o = o_d.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(len(ks))
                     prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
                     its = o["iterations_run"].astype(np.int64)
+                    kms, kplies = gpu.last_kernel_ms(), int(o["rollout_plies"].astype(np.int64).sum())
+                    for t in (SEARCH_TOTALS, SEARCH_TOTALS["by_kernel"].setdefault(
+                            gpu.last_kernel(), {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0})):
+                        t["launches"] += 1
+                        t["kernel_ms"] += kms
+                        t["sims"] += int(its.sum())
+                        t["rollout_plies"] += kplies
                     last_iters[aid] = its
                     for k, a, mv, it in zip(ks.tolist(), aid.tolist(), o["best_move"].tolist(), its.tolist()):
                         i = int(stop[k])
