@@ -407,8 +407,11 @@ typedef struct bk_mcts_cfg {
     int32_t resume;            /* 1: continue the searches left in nodes / out / tt /
                                   mt_state by an earlier launch (iter_stop chunks)      */
     int32_t rollout_policy;    /* BK_MCTS_ROLLOUT_*: the rollout_agent                  */
-    int32_t reserved;
+    int32_t flags;             /* BK_MCTS_ASYNC: with BK_MEM_DEVICE, return once the
+                                  launch is enqueued (no wait; a tripped step guard is
+                                  then reported by bk_synchronize)                      */
 } bk_mcts_cfg;
+#define BK_MCTS_ASYNC 1
 #define BK_MCTS_ROLLOUT_RANDOM 0    /* RandomAgent (agents/random_agent.py:49)            */
 #define BK_MCTS_ROLLOUT_HEURISTIC 1 /* HeuristicAgent (agents/heuristic_agent.py:39-244),
                                        MCTSAgent's default (mcts/mcts_agent.py:275-281);

@@ -84,7 +84,8 @@ class BkMctsCfg(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("max_rollout_moves", C.c_int32), ("exploration", C.c_double),
                 ("use_tt", C.c_int32), ("node_cap", C.c_int32), ("tt_cap", C.c_int32),
                 ("time_limit_us", C.c_int32), ("iter_stop", C.c_int32), ("resume", C.c_int32),
-                ("rollout_policy", C.c_int32), ("reserved", C.c_int32)]
+                ("rollout_policy", C.c_int32), ("flags", C.c_int32)]
+MCTS_ASYNC = 1  # bk_mcts_cfg.flags: enqueue only (device buffers)
 
 
 assert C.sizeof(BkMctsCfg) == 48

@@ -536,6 +536,90 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                 uncertified_heuristic=0, device_driver=1)
     forced = np.full(n, -1, np.int32)
     stream = torch.cuda.current_stream(dev)
+    # MCTS searches run on their own streams and handles (BK_ARENA_MCTS_STREAMS, default
+    # 2) and are not waited for: a game whose search is in flight sits at its stop seat
+    # (forced -1, arena_step leaves it there) while the other games play on and launch
+    # their own searches; its move is placed in the first round after the search ends.
+    # BK_ARENA_PIPELINE=0: one search at a time on the main stream, waited for at once.
+    pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
+    n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "2"))) if pipeline else 1
+    engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
+    jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
+    free_slots = list(range(n_slots))
+    jobs: List[Dict[str, Any]] = []
+    inflight = np.zeros(n, bool)
+
+    def mcts_launch(games, pls, aid, iters, roll, c, use_tt, policy):
+        slot = free_slots.pop(0)
+        eng, js = engines[slot], jstreams[slot]
+        gi_d, aid_d = up(games), up(aid)
+        roots_d = states_d.index_select(0, gi_d).contiguous()
+        sets_g = sets_d.index_select(0, gi_d).contiguous()
+        roots_h = roots_d.cpu().numpy().view(N.STATE_DTYPE).reshape(len(games))
+        rh_d = up(hash_states(roots_h, zob_h[aid]).view(np.int64))
+        players = up(pls.astype(np.uint8))
+        zi_d = aid_d.to(torch.int32)
+        mt_g = mtm_d.index_select(0, aid_d).contiguous()
+        if iters not in log_tables:
+            log_tables[iters] = up(mcts_log_table(iters))
+        tt = (ttk_d.index_select(0, aid_d), ttv_d.index_select(0, aid_d), ttc_d.index_select(0, aid_d)) \
+            if use_tt else (None, None, None)
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        js.wait_event(ready)
+        with torch.cuda.stream(js):
+            nodes = torch.empty((len(games), mcts_node_cap(iters) * N.MCTS_NODE_DTYPE.itemsize),
+                                dtype=torch.uint8, device=dev)
+            o_d = torch.zeros((len(games), N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            eng.mcts_device(roots_d, sets_g, players, rh_d, zob_d, zi_d, mt_g, log_tables[iters], nodes, o_d,
+                            iterations=iters, tt_keys=tt[0], tt_vals=tt[1], tt_count=tt[2],
+                            max_rollout_moves=roll, exploration=c, rollout_policy=policy, asynchronous=pipeline)
+            mtm_d.index_copy_(0, aid_d, mt_g)
+            if use_tt:
+                ttk_d.index_copy_(0, aid_d, tt[0])
+                ttv_d.index_copy_(0, aid_d, tt[1])
+                ttc_d.index_copy_(0, aid_d, tt[2])
+            done = torch.cuda.Event()
+            done.record(js)
+        for t in (gi_d, aid_d, roots_d, sets_g, rh_d, players, zi_d, mt_g) + (tt if use_tt else ()):
+            t.record_stream(js)
+        inflight[games] = True
+        jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done})
+        if not pipeline:
+            mcts_finish(jobs.pop(0))
+
+    def mcts_finish(job):
+        job["done"].synchronize()
+        eng = engines[job["slot"]]
+        eng.synchronize()  # sticky launch errors
+        games, aid = job["games"], job["aid"]
+        o = job["o_d"].cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(len(games))
+        bad = o["status"] & ~np.uint32(N.MCTS_EUNCERT)
+        if bad.any():
+            raise RuntimeError(f"bk_mcts: {int(np.count_nonzero(bad))} searches stopped early, status bits "
+                               f"{int(np.bitwise_or.reduce(bad))}")
+        prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
+        its = o["iterations_run"].astype(np.int64)
+        kms, kplies = eng.last_kernel_ms(), int(o["rollout_plies"].astype(np.int64).sum())
+        for t in (SEARCH_TOTALS, SEARCH_TOTALS["by_kernel"].setdefault(
+                eng.last_kernel(), {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0})):
+            t["launches"] += 1
+            t["kernel_ms"] += kms
+            t["sims"] += int(its.sum())
+            t["rollout_plies"] += kplies
+        last_iters[aid] = its
+        for i, a, mv, it in zip(games.tolist(), aid.tolist(), o["best_move"].tolist(), its.tolist()):
+            forced[i] = int(mv)
+            e = per_agent[i][mcts[a]["name"]]
+            e["total_simulations"] += float(it)
+            e["moves_with_simulations"] += 1
+        if job["tc"] is not None and int(job["tc"].max().item()) > 500000:  # mcts_agent.py:338-339
+            full = aid[(job["tc"].cpu().numpy() > 500000)]
+            ttk_d[up(full)] = 0
+            ttv_d[up(full)] = float("nan")
+            ttc_d[up(full)] = 0
+        inflight[games] = False
+        free_slots.append(job["slot"])
     while active.any():
         prof["rounds"] += 1
         if progress is not None:
@@ -547,7 +631,8 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         stops = stop_d.cpu().numpy().view(N.STOP_DTYPE).reshape(n)
         prof["advance_s"] += time.perf_counter() - ta
         status = res["status"].astype(np.int64)
-        act = np.flatnonzero(active)
+        forced[:] = -1
+        act = np.flatnonzero(active & ~inflight)
         tot[act, 0] += res["turns"][act]
         tot[act, 1] += res["passes"][act]
         prof["uncertified_heuristic"] += int(np.count_nonzero(status[act] & N.STATUS_UNCERT))
@@ -569,7 +654,6 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                     passes -= int(r["reserved"][0])
             results[i] = (r, turns, passes, truncated)
             active[i] = False
-        forced[:] = -1
         if len(stop):
             pl = (np.zeros(len(stop), np.int64))
             cur = states_d.index_select(0, up(stop))[:, 241].cpu().numpy().astype(np.int64) & 3
@@ -593,56 +677,11 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                 for k in multi.tolist():
                     a = mcts[int(ag[k])]
                     groups.setdefault((a["iters"], a["roll"], a["c"], a["tt"], a["policy"]), []).append(k)
-                for (iters, roll, c, use_tt, policy), ks in groups.items():
+                for key, ks in groups.items():
                     ks = np.array(ks)
-                    gi_d = up(stop[ks])
-                    aid = ag[ks]
-                    aid_d = up(aid)
-                    roots_d = states_d.index_select(0, gi_d).contiguous()
-                    sets_g = sets_d.index_select(0, gi_d).contiguous()
-                    roots_h = roots_d.cpu().numpy().view(N.STATE_DTYPE).reshape(len(ks))
-                    rh = hash_states(roots_h, zob_h[aid])
-                    players = up(pl[ks].astype(np.uint8))
-                    mt_g = mtm_d.index_select(0, aid_d).contiguous()
-                    if iters not in log_tables:
-                        log_tables[iters] = up(mcts_log_table(iters))
-                    nodes = torch.empty((len(ks), mcts_node_cap(iters) * N.MCTS_NODE_DTYPE.itemsize),
-                                        dtype=torch.uint8, device=dev)
-                    o_d = torch.zeros((len(ks), N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-                    tk = tv = tc = None
-                    if use_tt:
-                        tk, tv, tc = (ttk_d.index_select(0, aid_d), ttv_d.index_select(0, aid_d),
-                                      ttc_d.index_select(0, aid_d))
-                    gpu.mcts_device(roots_d, sets_g, players, up(rh.view(np.int64)), zob_d, aid_d.to(torch.int32),
-                                    mt_g, log_tables[iters], nodes, o_d, iterations=iters, tt_keys=tk, tt_vals=tv,
-                                    tt_count=tc, max_rollout_moves=roll, exploration=c, rollout_policy=policy)
-                    mtm_d.index_copy_(0, aid_d, mt_g)
-                    if use_tt:
-                        ttk_d.index_copy_(0, aid_d, tk)
-                        ttv_d.index_copy_(0, aid_d, tv)
-                        ttc_d.index_copy_(0, aid_d, tc)
-                    o = o_d.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(len(ks))
-                    prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
-                    its = o["iterations_run"].astype(np.int64)
-                    kms, kplies = gpu.last_kernel_ms(), int(o["rollout_plies"].astype(np.int64).sum())
-                    for t in (SEARCH_TOTALS, SEARCH_TOTALS["by_kernel"].setdefault(
-                            gpu.last_kernel(), {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0})):
-                        t["launches"] += 1
-                        t["kernel_ms"] += kms
-                        t["sims"] += int(its.sum())
-                        t["rollout_plies"] += kplies
-                    last_iters[aid] = its
-                    for k, a, mv, it in zip(ks.tolist(), aid.tolist(), o["best_move"].tolist(), its.tolist()):
-                        i = int(stop[k])
-                        forced[i] = int(mv)
-                        e = per_agent[i][mcts[a]["name"]]
-                        e["total_simulations"] += float(it)
-                        e["moves_with_simulations"] += 1
-                    if use_tt and int(tc.max().item()) > 500000:  # mcts_agent.py:338-339
-                        full = aid[(tc.cpu().numpy() > 500000)]
-                        ttk_d[up(full)] = 0
-                        ttv_d[up(full)] = float("nan")
-                        ttc_d[up(full)] = 0
+                    if not free_slots:
+                        mcts_finish(jobs.pop(0))
+                    mcts_launch(stop[ks], pl[ks], ag[ks], *key)
                 prof["mcts_s"] += time.perf_counter() - tm
             # ---- FastMCTS seats (think: a single legal move draws nothing)
             sel = np.flatnonzero(kind == 2)
@@ -671,7 +710,15 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                         e["total_simulations"] += it
                         e["moves_with_simulations"] += 1
                 prof["fast_s"] += time.perf_counter() - tf
+        tm = time.perf_counter()
+        if jobs and not (forced >= 0).any():  # nothing to place: wait for the oldest search
+            mcts_finish(jobs.pop(0))
+        for j in [j for j in jobs if j["done"].query()]:
+            jobs.remove(j)
+            mcts_finish(j)
+        prof["mcts_s"] += time.perf_counter() - tm
         forced_d.copy_(torch.from_numpy(forced))
+    assert not jobs and not inflight.any()
     stream.synchronize()
     dt = time.perf_counter() - t0
     prof["total_s"] = dt

@@ -5122,6 +5122,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;
+    if (mem == BK_MEM_DEVICE && (cfg->flags & BK_MCTS_ASYNC)) return BK_OK;  // errors: bk_synchronize
     uint32_t ctr[4];
     if (mem == BK_MEM_HOST) {
         for (int i = 0; i < NSEC; ++i)

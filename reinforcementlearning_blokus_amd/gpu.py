@@ -439,7 +439,7 @@ class BlokusGPU:
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
                     hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
                     on_chunk=None, stop_after: int | None = None, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM,
-                    resume_from: int | None = None, time_limit_us: int = 0):
+                    resume_from: int | None = None, time_limit_us: int = 0, asynchronous: bool = False):
         """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
@@ -452,7 +452,9 @@ class BlokusGPU:
         called after each; stop_after: run only the first stop_after iterations (they
         can be resumed by no caller here: a warm-up).  time_limit_us: stop each search at
         the first iteration boundary past it (no chunking).  Raises if any search reports
-        a nonzero status."""
+        a nonzero status.  asynchronous: one launch, enqueued on torch's current stream
+        and not waited for (BK_MCTS_ASYNC); the caller checks the statuses in `out` and
+        calls synchronize() once the stream has passed it."""
         import torch
         n = roots.shape[0]
         use_tt = tt_keys is not None
@@ -485,12 +487,15 @@ class BlokusGPU:
             resume = int(j > 0 or resume_from is not None)
             cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
                               tt_keys.shape[1] if use_tt else 0, int(time_limit_us), stop, resume,
-                              int(rollout_policy), 0)
+                              int(rollout_policy), N.MCTS_ASYNC if asynchronous else 0)
             self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
                              d(zobrist_index), d(mt_state), d(tt_keys), d(tt_vals), d(tt_count), d(log_table),
                              log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)
             if on_chunk is not None:
                 on_chunk(stop or iterations)
+        if asynchronous:
+            assert len(stops) == 1, "an asynchronous search is one launch"
+            return
         st = out.view(torch.int32)[:, 6] & ~N.MCTS_EUNCERT
         bad = int((st != 0).sum().item())
         if bad:
