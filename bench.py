@@ -712,13 +712,14 @@ def run_config2(args, world, rank, local, dist):
         barrier_sync(dist)
         elapsed = time.perf_counter() - t0
     kernel_ms = e0.elapsed_time(e1) / args.steps
+    kname = gpu.last_kernel()  # k_movegen_ml (LDS-staged writes) or k_movegen_m (BK_MG_STAGE=0)
     moves = int(cnt.to(torch.int64).sum().item())
     elapsed, (pairs,) = reduce_max_sum(dist, dev, elapsed, [n * args.steps])
     if rank != 0:
         return None
     value = pairs / elapsed
     achieved = n * MOVEGEN_B / (kernel_ms * 1e-3) / 1e9
-    traffic, valu_insts, tsrc = traffic_for("k_movegen_m", n)
+    traffic, valu_insts, tsrc = traffic_for(kname, n)
     line = {
         "metric": "batched legal-move generation (board-players/s, 20x20, 4p)", "value": value,
         "unit": "board-players/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -731,7 +732,7 @@ def run_config2(args, world, rank, local, dist):
                    "legal_moves_per_board_player": moves / n, "us_per_batch": kernel_ms * 1e3,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_movegen_m",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                      "kernel_ms": kernel_ms, "bytes_per_board_player": MOVEGEN_B,
                      "bytes_written_per_board_player": 91 * 7 * 8 + 4, "traffic_profile": tsrc},
         "compute_roofline": compute_roofline(valu_insts, kernel_ms),

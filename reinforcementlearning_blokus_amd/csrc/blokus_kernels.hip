@@ -1122,6 +1122,102 @@ __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
 __global__ void k_movegen_m(MovegenArgs a);
 #endif
 
+// Dense rows of the class's table entries i0 <= i < i1 whose orientation lies in
+// [glo, ghi), every Wp-th of them from wave w on (k_movegen_ml); seen counts the in-range
+// entries of the earlier classes (wave-uniform)
+template <int H, int... T, typename F>
+__device__ __forceinline__ void rows_class_range(int i0, int i1, int glo, int ghi, int w, int Wp, int& seen,
+                                                 const Planes& P, F&& f) {
+#pragma unroll 1
+    for (int i = i0; i < i1; ++i) {
+        const uint32_t w0 = kClass[i][0], w1 = kClass[i][1];
+        const int g = (int)(w0 >> 8);
+        if (g < glo || g >= ghi) continue;
+        if (seen++ % Wp != w) continue;
+        uint32_t ok[20];
+#pragma unroll
+        for (int r = 0; r < 20; ++r) ok[r] = 0u;
+        StencilClass<H, T...>::scan(P, w1, [&](int r, uint32_t v) { ok[r] = v; });
+        f(g, w0 & 0xFFu, ok);
+    }
+}
+
+// k_movegen_m with whole-line writes.  The 91 orientations are split into MG_PARTS
+// contiguous ranges; a block is one (set of 64 board-players, range) pair whose
+// blockDim / 64 waves share the range's stencil entries.  Each board-player's masks for
+// the range are staged in LDS (64 x <= 23 x 7 u64 = 82 KB) and then written as one
+// contiguous segment per board-player with coalesced 8-B stores (512 B per wave
+// instruction), instead of 56-B pieces at a 5,096-B stride.  The MG_PARTS blocks of a
+// set run on the same XCD, so the lines their segments share merge in that L2.
+#define MG_PARTS 4
+#define MG_PART_MAX ((BK_NUM_ORIENTS + MG_PARTS - 1) / MG_PARTS)
+#define MG_PART_WAVES_MAX 8
+#if BK_DEF(BK_U_MOVEGEN)
+__global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml(MovegenArgs a) {
+    __shared__ uint64_t stage[WAVE * MG_PART_MAX * 7];
+    const int Wp = (int)(blockDim.x / WAVE);
+    const int w = (int)(threadIdx.x / WAVE), lane = (int)(threadIdx.x % WAVE);
+    const int xcd = blockIdx.x % MG_XCDS, j = blockIdx.x / MG_XCDS;
+    const int set = xcd + MG_XCDS * (j / MG_PARTS), part = j % MG_PARTS;
+    if (set * WAVE >= a.n) return;  // a grid rounded up to a multiple of 8 sets: whole idle blocks
+    const int glo = part * BK_NUM_ORIENTS / MG_PARTS, ghi = (part + 1) * BK_NUM_ORIENTS / MG_PARTS;
+    const int nw = (ghi - glo) * 7;
+    const int i = set * WAVE + lane;
+    const bool live = i < a.n;
+    const int idx = live ? i : 0;
+    const bk_state* s = a.states + idx;
+    const int p = a.players[idx] & 3;
+    uint32_t own[20], occ[20];
+#pragma unroll
+    for (int R = 0; R < 20; ++R) { occ[R] = 0; own[R] = 0; }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int R = 0; R < 20; ++R) {
+            const uint32_t row = plane_row(s->planes[q], R);
+            occ[R] |= row;
+            own[R] |= (q == p) ? row : 0u;
+        }
+    Planes P;
+    derive_rows(own, occ, (s->first_move >> p) & 1u, p, P);
+    make_pairs(P);
+    const uint32_t avail = live ? (~s->used[p] & 0x1FFFFFu) : 0u;
+    uint32_t total = 0;
+    uint64_t* mine = stage + lane * nw - glo * 7;
+    auto emit = [&](int g, uint32_t piece, const uint32_t (&ok)[20]) {
+        const bool av = (avail >> (piece - 1u)) & 1u;
+        uint64_t wd[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 20; ++r) {
+            const uint32_t v = av ? ok[r] : 0u;
+            total += __builtin_popcount(v);
+            constexpr int kBits = 20;
+            const int off = kBits * r, q = off >> 6, sh = off & 63;  // compile-time per r
+            wd[q] |= (uint64_t)v << sh;
+            if (sh > 64 - kBits) wd[q + 1] |= (uint64_t)v >> (64 - sh);
+        }
+#pragma unroll
+        for (int q = 0; q < 7; ++q) mine[g * 7 + q] = wd[q];
+    };
+    int seen = 0;
+#define BK_ROWS_RANGE(i0, i1, H, ...) rows_class_range<H, __VA_ARGS__>(i0, i1, glo, ghi, w, Wp, seen, P, emit);
+    BK_CLASS_LIST(BK_ROWS_RANGE)
+#undef BK_ROWS_RANGE
+    if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
+    __syncthreads();
+    if (a.out_mask) {
+        const int nb = a.n - set * WAVE < WAVE ? a.n - set * WAVE : WAVE;
+        uint64_t* base = a.out_mask + (size_t)set * WAVE * (BK_NUM_ORIENTS * 7) + glo * 7;
+        for (int k = (int)threadIdx.x; k < nb * nw; k += (int)blockDim.x) {
+            const int b = k / nw, o = k - b * nw;
+            base[(size_t)b * (BK_NUM_ORIENTS * 7) + o] = stage[k];
+        }
+    }
+}
+#else
+__global__ void k_movegen_ml(MovegenArgs a);
+#endif
+
 #if BK_DEF(BK_U_MOVEGEN)
 __global__ __launch_bounds__(BLOCK) void k_has_moves(MovegenArgs a) {
     const int lane = threadIdx.x & (WAVE - 1);
@@ -4446,8 +4542,19 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, nullptr, d_count, nullptr, groups, d_mask};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
-    h->last_kernel = "k_movegen_m";
-    hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);
+    // LDS-staged whole-line writes (k_movegen_ml): the groups' waves split over MG_PARTS
+    // orientation ranges of one set each; BK_MG_STAGE=0 keeps the per-lane stores
+    bool staged = out_mask != nullptr;
+    if (const char* env = getenv("BK_MG_STAGE")) staged = staged && atoi(env) != 0;  // A/B override
+    if (staged) {
+        int wp = groups / MG_PARTS;
+        wp = wp < 1 ? 1 : (wp > MG_PART_WAVES_MAX ? MG_PART_WAVES_MAX : wp);
+        h->last_kernel = "k_movegen_ml";
+        hipLaunchKernelGGL(k_movegen_ml, dim3(sets * MG_PARTS), dim3(wp * WAVE), 0, h->cur, a);
+    } else {
+        h->last_kernel = "k_movegen_m";
+        hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);
+    }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;

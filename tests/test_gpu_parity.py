@@ -189,3 +189,23 @@ def test_movegen_mask_equals_rows_and_oracle(gpu, n):
     assert np.array_equal(md.cpu().numpy().view(np.uint64), masks)
     c0, m0 = gpu.movegen_mask(st, players, masks=False)
     assert m0 is None and np.array_equal(c0, cnt)
+
+
+@pytest.mark.parametrize("groups", ["4", "8", "32", "91"])
+def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups):
+    """k_movegen_ml (LDS-staged whole-line writes, MG_PARTS orientation ranges of
+    groups / 4 waves each, at least 1 and at most 8) writes the same masks and counts as
+    k_movegen_m's per-lane stores (BK_MG_STAGE=0), for ragged sizes; the launch names the
+    staged kernel."""
+    monkeypatch.setenv("BK_MG_GROUPS", groups)
+    for n in (1, 70, 600):
+        boards = oracle_states(n, seed0=7100 + n)
+        st = pack_many(boards)
+        players = np.array([b.cur for b in boards], dtype=np.uint8)
+        monkeypatch.setenv("BK_MG_STAGE", "1")
+        c1, m1 = gpu.movegen_mask(st, players)
+        assert gpu.last_kernel() == "k_movegen_ml"
+        monkeypatch.setenv("BK_MG_STAGE", "0")
+        c0, m0 = gpu.movegen_mask(st, players)
+        assert gpu.last_kernel() == "k_movegen_m"
+        assert np.array_equal(c1, c0) and np.array_equal(m1, m0), n
