@@ -1206,11 +1206,30 @@ __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml(Movegen
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
     __syncthreads();
     if (a.out_mask) {
+        // 16-byte stores (the width WRITE_SIZE reads exactly): unit u of board b covers the
+        // 16-byte-aligned word pair 2u - h, 2u - h + 1 of its segment (h = 1 when the
+        // segment starts at an odd word: 637 and 7 are odd, so h = (b + glo + h0) & 1, h0 =
+        // out_mask's own word parity); a pair half outside the segment is left to the
+        // neighbouring segment's block
         const int nb = a.n - set * WAVE < WAVE ? a.n - set * WAVE : WAVE;
+        const int nu = nw / 2 + 1;
+        const int h0 = (int)(((uintptr_t)a.out_mask >> 3) & 1u);
         uint64_t* base = a.out_mask + (size_t)set * WAVE * (BK_NUM_ORIENTS * 7) + glo * 7;
-        for (int k = (int)threadIdx.x; k < nb * nw; k += (int)blockDim.x) {
-            const int b = k / nw, o = k - b * nw;
-            base[(size_t)b * (BK_NUM_ORIENTS * 7) + o] = stage[k];
+        for (int k = (int)threadIdx.x; k < nb * nu; k += (int)blockDim.x) {
+            const int b = k / nu, u = k - b * nu;
+            const int w0 = 2 * u - ((b + glo + h0) & 1);
+            const bool lo_in = w0 >= 0 && w0 < nw, hi_in = w0 + 1 < nw;
+            uint64_t* dst = base + (size_t)b * (BK_NUM_ORIENTS * 7) + w0;
+            const uint64_t* src = stage + b * nw + w0;
+            if (lo_in && hi_in) {
+                const uint64_t v0 = src[0], v1 = src[1];
+                *reinterpret_cast<uint4*>(dst) = make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1,
+                                                            (uint32_t)(v1 >> 32));
+            } else if (lo_in) {
+                dst[0] = src[0];
+            } else if (hi_in) {
+                dst[1] = src[1];
+            }
         }
     }
 }

@@ -209,3 +209,30 @@ def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups):
         c0, m0 = gpu.movegen_mask(st, players)
         assert gpu.last_kernel() == "k_movegen_m"
         assert np.array_equal(c1, c0) and np.array_equal(m1, m0), n
+
+
+def test_movegen_mask_staged_odd_word_output(gpu):
+    """k_movegen_ml with a device out_mask that starts 8 bytes past a 16-byte boundary
+    (the C-ABI allows 8-byte alignment): the 16-byte stores shift to that parity, the
+    masks equal the aligned call's and the words either side stay untouched."""
+    import torch
+    from reinforcementlearning_blokus_amd import _native as N
+    n = 130
+    boards = oracle_states(n, seed0=7300)
+    st = pack_many(boards)
+    players = np.array([b.cur for b in boards], dtype=np.uint8)
+    cnt, ref = gpu.movegen_mask(st, players)
+    dev = torch.device("cuda", 0)
+    sd = torch.from_numpy(st.view(np.uint8).reshape(n, 256).copy()).to(dev)
+    pd = torch.from_numpy(players).to(dev)
+    words = n * N.N_ORIENTS * 7
+    buf = torch.full((words + 2,), -7, dtype=torch.int64, device=dev)  # word 1 on: 8 B past 16
+    cd = torch.empty(n, dtype=torch.int32, device=dev)
+    gpu._stream_from_torch()
+    gpu.handle.movegen_mask(sd.data_ptr(), pd.data_ptr(), n, buf.data_ptr() + 8, cd.data_ptr(), N.MEM_DEVICE)
+    torch.cuda.synchronize()
+    assert gpu.last_kernel() == "k_movegen_ml"
+    b = buf.cpu().numpy()
+    assert b[0] == -7 and b[-1] == -7
+    assert np.array_equal(b[1:-1].view(np.uint64).reshape(n, N.N_ORIENTS, 7), ref)
+    assert np.array_equal(cd.cpu().numpy().astype(np.uint32), cnt)
