@@ -86,6 +86,12 @@ def parse(argv=None):
     ap.add_argument("--host-cores", type=int, default=None,
                     help="config4: host cores this rank may use (default: the usable cores / local ranks; "
                          "each rank's host phases and worker threads are pinned to its own cores)")
+    ap.add_argument("--search-streams", type=int, default=None,
+                    help="config4: MCTS searches in flight on this many streams while the other games play on "
+                         "(BK_ARENA_MCTS_STREAMS; default: the driver's)")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="config4: HIP hardware queues of this rank (GPU_MAX_HW_QUEUES, <= 32), so the search "
+                         "streams and the main stream do not share in-order queues")
     ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
                     help="config3 in-kernel move order: naive (default) or the reference's frontier order "
                          "(CPython set tables carried per game)")
@@ -608,6 +614,9 @@ def run_config4(args, world, rank, local, dist):
                    "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
                    "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
                    "rank0_phase_seconds": phases, "host_cores_per_rank": host,
+                   "search_streams": os.environ.get("BK_ARENA_MCTS_STREAMS", "default"),
+                   "pipelined": os.environ.get("BK_ARENA_PIPELINE", "1") != "0",
+                   "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default"),
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "kernel_ms": kms,
@@ -844,6 +853,13 @@ def main():
     n = args.gpus or 1
     if "WORLD_SIZE" not in os.environ and n > 1:
         sys.exit(launch_ranks(n, sys.argv[1:]))
+    if args.workload == "config4":  # before the HIP runtime starts (setup imports torch)
+        if args.search_streams is not None:
+            os.environ["BK_ARENA_MCTS_STREAMS"] = str(args.search_streams)
+        if args.hw_queues is not None:
+            if not 1 <= args.hw_queues <= 32:
+                raise SystemExit("bench.py: --hw-queues must be in 1..32")
+            os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     world, rank, local, dist = setup(args)
     run = {"config3": run_config3, "config5": run_config5, "config2": run_config2,
            "config4": run_config4}[args.workload]

@@ -1142,25 +1142,26 @@ __device__ __forceinline__ void rows_class_range(int i0, int i1, int glo, int gh
     }
 }
 
-// k_movegen_m with whole-line writes.  The 91 orientations are split into MG_PARTS
+// k_movegen_m with whole-line writes.  The 91 orientations are split into PARTS
 // contiguous ranges; a block is one (set of 64 board-players, range) pair whose
 // blockDim / 64 waves share the range's stencil entries.  Each board-player's masks for
-// the range are staged in LDS (64 x <= 23 x 7 u64 = 82 KB) and then written as one
-// contiguous segment per board-player with coalesced 8-B stores (512 B per wave
-// instruction), instead of 56-B pieces at a 5,096-B stride.  The MG_PARTS blocks of a
-// set run on the same XCD, so the lines their segments share merge in that L2.
-#define MG_PARTS 4
-#define MG_PART_MAX ((BK_NUM_ORIENTS + MG_PARTS - 1) / MG_PARTS)
+// the range are staged in LDS (64 x ceil(91 / PARTS) x 7 u64: 82 KB at 4 parts, 47 KB at
+// 7, 25 KB at 13) and then written as one contiguous segment per board-player with
+// coalesced 16-B stores, instead of 56-B pieces at a 5,096-B stride.  The PARTS blocks
+// of a set run on the same XCD, so the lines their segments share merge in that L2.
+// Entry points k_movegen_ml4 / 7 / 13 (bk_movegen_mask picks one; BK_MG_PARTS).
 #define MG_PART_WAVES_MAX 8
 #if BK_DEF(BK_U_MOVEGEN)
-__global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml(MovegenArgs a) {
+template <int PARTS>
+__device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
+    constexpr int MG_PART_MAX = (BK_NUM_ORIENTS + PARTS - 1) / PARTS;
     __shared__ uint64_t stage[WAVE * MG_PART_MAX * 7];
     const int Wp = (int)(blockDim.x / WAVE);
     const int w = (int)(threadIdx.x / WAVE), lane = (int)(threadIdx.x % WAVE);
     const int xcd = blockIdx.x % MG_XCDS, j = blockIdx.x / MG_XCDS;
-    const int set = xcd + MG_XCDS * (j / MG_PARTS), part = j % MG_PARTS;
+    const int set = xcd + MG_XCDS * (j / PARTS), part = j % PARTS;
     if (set * WAVE >= a.n) return;  // a grid rounded up to a multiple of 8 sets: whole idle blocks
-    const int glo = part * BK_NUM_ORIENTS / MG_PARTS, ghi = (part + 1) * BK_NUM_ORIENTS / MG_PARTS;
+    const int glo = part * BK_NUM_ORIENTS / PARTS, ghi = (part + 1) * BK_NUM_ORIENTS / PARTS;
     const int nw = (ghi - glo) * 7;
     const int i = set * WAVE + lane;
     const bool live = i < a.n;
@@ -1233,8 +1234,13 @@ __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml(Movegen
         }
     }
 }
+__global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml4(MovegenArgs a) { movegen_ml_body<4>(a); }
+__global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml7(MovegenArgs a) { movegen_ml_body<7>(a); }
+__global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml13(MovegenArgs a) { movegen_ml_body<13>(a); }
 #else
-__global__ void k_movegen_ml(MovegenArgs a);
+__global__ void k_movegen_ml4(MovegenArgs a);
+__global__ void k_movegen_ml7(MovegenArgs a);
+__global__ void k_movegen_ml13(MovegenArgs a);
 #endif
 
 #if BK_DEF(BK_U_MOVEGEN)
@@ -4566,10 +4572,23 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     bool staged = out_mask != nullptr;
     if (const char* env = getenv("BK_MG_STAGE")) staged = staged && atoi(env) != 0;  // A/B override
     if (staged) {
-        int wp = groups / MG_PARTS;
+        int parts = 4;
+        if (const char* env = getenv("BK_MG_PARTS")) parts = atoi(env);  // tuning: 4, 7 or 13
+        if (parts != 7 && parts != 13) parts = 4;
+        int wp = groups / parts;
+        if (const char* env = getenv("BK_MG_PART_WAVES")) wp = atoi(env);  // tuning override
         wp = wp < 1 ? 1 : (wp > MG_PART_WAVES_MAX ? MG_PART_WAVES_MAX : wp);
-        h->last_kernel = "k_movegen_ml";
-        hipLaunchKernelGGL(k_movegen_ml, dim3(sets * MG_PARTS), dim3(wp * WAVE), 0, h->cur, a);
+        const dim3 grid(sets * parts), blk(wp * WAVE);
+        if (parts == 4) {
+            h->last_kernel = "k_movegen_ml4";
+            hipLaunchKernelGGL(k_movegen_ml4, grid, blk, 0, h->cur, a);
+        } else if (parts == 7) {
+            h->last_kernel = "k_movegen_ml7";
+            hipLaunchKernelGGL(k_movegen_ml7, grid, blk, 0, h->cur, a);
+        } else {
+            h->last_kernel = "k_movegen_ml13";
+            hipLaunchKernelGGL(k_movegen_ml13, grid, blk, 0, h->cur, a);
+        }
     } else {
         h->last_kernel = "k_movegen_m";
         hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);

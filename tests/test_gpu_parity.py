@@ -191,20 +191,22 @@ def test_movegen_mask_equals_rows_and_oracle(gpu, n):
     assert m0 is None and np.array_equal(c0, cnt)
 
 
+@pytest.mark.parametrize("parts", ["4", "7", "13"])
 @pytest.mark.parametrize("groups", ["4", "8", "32", "91"])
-def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups):
-    """k_movegen_ml (LDS-staged whole-line writes, MG_PARTS orientation ranges of
-    groups / 4 waves each, at least 1 and at most 8) writes the same masks and counts as
+def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups, parts):
+    """k_movegen_ml4/7/13 (LDS-staged whole-line writes, 4, 7 or 13 orientation ranges of
+    groups / parts waves each, at least 1 and at most 8) writes the same masks and counts as
     k_movegen_m's per-lane stores (BK_MG_STAGE=0), for ragged sizes; the launch names the
     staged kernel."""
     monkeypatch.setenv("BK_MG_GROUPS", groups)
+    monkeypatch.setenv("BK_MG_PARTS", parts)
     for n in (1, 70, 600):
         boards = oracle_states(n, seed0=7100 + n)
         st = pack_many(boards)
         players = np.array([b.cur for b in boards], dtype=np.uint8)
         monkeypatch.setenv("BK_MG_STAGE", "1")
         c1, m1 = gpu.movegen_mask(st, players)
-        assert gpu.last_kernel() == "k_movegen_ml"
+        assert gpu.last_kernel() == "k_movegen_ml" + parts
         monkeypatch.setenv("BK_MG_STAGE", "0")
         c0, m0 = gpu.movegen_mask(st, players)
         assert gpu.last_kernel() == "k_movegen_m"
@@ -231,7 +233,7 @@ def test_movegen_mask_staged_odd_word_output(gpu):
     gpu._stream_from_torch()
     gpu.handle.movegen_mask(sd.data_ptr(), pd.data_ptr(), n, buf.data_ptr() + 8, cd.data_ptr(), N.MEM_DEVICE)
     torch.cuda.synchronize()
-    assert gpu.last_kernel() == "k_movegen_ml"
+    assert gpu.last_kernel().startswith("k_movegen_ml")
     b = buf.cpu().numpy()
     assert b[0] == -7 and b[-1] == -7
     assert np.array_equal(b[1:-1].view(np.uint64).reshape(n, N.N_ORIENTS, 7), ref)
