@@ -532,21 +532,26 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     tot = np.zeros((n, 2), np.int64)  # turn_count, passes so far
     results: List[Optional[Tuple[Any, int, int, bool]]] = [None] * n
     active = np.ones(n, bool)
-    prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0,
-                uncertified_heuristic=0, device_driver=1)
+    prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, wait_s=0.0, host_s=0.0,
+                rounds=0, uncertified_heuristic=0, device_driver=1)
     forced = np.full(n, -1, np.int32)
     stream = torch.cuda.current_stream(dev)
     # MCTS searches run on their own streams and handles (BK_ARENA_MCTS_STREAMS, default
-    # 2) and are not waited for: a game whose search is in flight sits at its stop seat
+    # 8) and are not waited for: a game whose search is in flight sits at its stop seat
     # (forced -1, arena_step leaves it there) while the other games play on and launch
     # their own searches; its move is placed in the first round after the search ends.
-    # BK_ARENA_PIPELINE=0: one search at a time on the main stream, waited for at once.
+    # FastMCTS launches (host-staged bk_fastmcts) run the same way on a worker thread with
+    # its own handle.  BK_ARENA_PIPELINE=0: one search at a time on the main stream,
+    # waited for at once.
     pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
-    n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "2"))) if pipeline else 1
+    n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8"))) if pipeline else 1
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
     jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
     free_slots = list(range(n_slots))
     jobs: List[Dict[str, Any]] = []
+    fjobs: List[Dict[str, Any]] = []
+    fast_eng = BlokusGPU(device) if pipeline else gpu
+    fast_pool = ThreadPoolExecutor(1) if pipeline else None
     inflight = np.zeros(n, bool)
 
     def mcts_launch(games, pls, aid, iters, roll, c, use_tt, policy):
@@ -620,6 +625,43 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             ttc_d[up(full)] = 0
         inflight[games] = False
         free_slots.append(job["slot"])
+    def fast_launch(games, aid, nl, counts, quick, ce):
+        mt = np.ascontiguousarray(mtf[aid])
+        args = (nl.tolist(), counts, quick.tolist(), mt, _log_table(max(counts) + 1), ce)
+        job = {"games": games, "aid": aid, "counts": counts, "mt": mt}
+        if pipeline:
+            job["fut"] = fast_pool.submit(fast_eng.fastmcts, *args)
+            inflight[games] = True
+            fjobs.append(job)
+        else:
+            job["r"] = gpu.fastmcts(*args)
+            fast_finish(job)
+
+    def fast_finish(job):
+        r = job["fut"].result() if "fut" in job else job["r"]
+        games, aid = job["games"], job["aid"]
+        mtf[aid] = job["mt"]
+        for i, a, it_run, bi, nch, it in zip(games.tolist(), aid.tolist(), r["iterations"].tolist(),
+                                              r["best_index"].tolist(), r["n_children"].tolist(), job["counts"]):
+            j = int(stops_q[i]) if it_run < 5 else (int(bi) if nch > 0 else 0)
+            forced[i] = N.FORCE_INDEX | j
+            e = per_agent[i][fast[a]["name"]]
+            e["total_simulations"] += it
+            e["moves_with_simulations"] += 1
+        inflight[games] = False
+
+    def drain():
+        done_m = [j for j in jobs if j["done"].query()]
+        for j in done_m:
+            jobs.remove(j)
+            mcts_finish(j)
+        done_f = [j for j in fjobs if j["fut"].done()]
+        for j in done_f:
+            fjobs.remove(j)
+            fast_finish(j)
+        return bool(done_m or done_f)
+
+    stops_q = np.zeros(n, np.int64)  # the FastMCTS seats' quick_index (stop info)
     while active.any():
         prof["rounds"] += 1
         if progress is not None:
@@ -695,34 +737,26 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                     groups.setdefault(fast[int(ag[k])]["c"], []).append(k)
                 for ce, ks in groups.items():
                     ks = np.array(ks)
+                    games = stop[ks]
                     aid = ag[ks]
-                    counts = [fast[int(a)]["iters"] for a in aid]
-                    mt = np.ascontiguousarray(mtf[aid])
-                    r = gpu.fastmcts(nleg[ks].tolist(), counts, stops["quick_reward"][stop[ks]].tolist(), mt,
-                                     _log_table(max(counts) + 1), ce)
-                    mtf[aid] = mt
-                    for k, a, it_run, bi, nch, it in zip(ks.tolist(), aid.tolist(), r["iterations"].tolist(),
-                                                          r["best_index"].tolist(), r["n_children"].tolist(), counts):
-                        i = int(stop[k])
-                        j = int(stops["quick_index"][i]) if it_run < 5 else (int(bi) if nch > 0 else 0)
-                        forced[i] = N.FORCE_INDEX | j
-                        e = per_agent[i][fast[a]["name"]]
-                        e["total_simulations"] += it
-                        e["moves_with_simulations"] += 1
+                    stops_q[games] = stops["quick_index"][games]
+                    fast_launch(games, aid, nleg[ks], [fast[int(a)]["iters"] for a in aid],
+                                stops["quick_reward"][games], ce)
                 prof["fast_s"] += time.perf_counter() - tf
         tm = time.perf_counter()
-        if jobs and not (forced >= 0).any():  # nothing to place: wait for the oldest search
-            mcts_finish(jobs.pop(0))
-        for j in [j for j in jobs if j["done"].query()]:
-            jobs.remove(j)
-            mcts_finish(j)
-        prof["mcts_s"] += time.perf_counter() - tm
+        drain()
+        while (jobs or fjobs) and not (forced >= 0).any():  # nothing to place: wait for a search
+            if not drain():
+                time.sleep(50e-6)
+        prof["wait_s"] += time.perf_counter() - tm
         forced_d.copy_(torch.from_numpy(forced))
-    assert not jobs and not inflight.any()
+    assert not jobs and not fjobs and not inflight.any()
+    if fast_pool is not None:
+        fast_pool.shutdown()
     stream.synchronize()
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
-    prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"]
+    prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"] - prof["wait_s"]
     if prof["uncertified_heuristic"]:
         warnings.warn(f"run_games_batched: {prof['uncertified_heuristic']} HeuristicAgent draw(s) fell within 2^-40 "
                       "of a probability boundary (choice not certified equal to the reference's on every host)",

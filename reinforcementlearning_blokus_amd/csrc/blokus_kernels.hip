@@ -1152,6 +1152,34 @@ __device__ __forceinline__ void rows_class_range(int i0, int i1, int glo, int gh
 // Entry points k_movegen_ml4 / 7 / 13 (bk_movegen_mask picks one; BK_MG_PARTS).
 #define MG_PART_WAVES_MAX 8
 #if BK_DEF(BK_U_MOVEGEN)
+// The block's staged segments (board-player b: words [0, nw) of stage + b * nw) to
+// base + b * 637 with 16-byte stores (the width WRITE_SIZE reads exactly): unit u of
+// board b covers the 16-byte-aligned word pair 2u - h, 2u - h + 1 of its segment (h = 1
+// when the segment starts at an odd word: 637 is odd, so h = (b + hpar) & 1); a pair half
+// outside the segment belongs to the neighbouring segment's block.  NWC > 0: nw, known.
+template <int NWC>
+__device__ __forceinline__ void ml_write_segments(const uint64_t* stage, uint64_t* base, int nb, int nw_rt, int hpar) {
+    const int nw = NWC > 0 ? NWC : nw_rt;
+    const int nu = nw / 2 + 1;
+#pragma unroll 1
+    for (int k = (int)threadIdx.x; k < nb * nu; k += (int)blockDim.x) {
+        const int b = k / nu, u = k - b * nu;
+        const int w0 = 2 * u - ((b + hpar) & 1);
+        const bool lo_in = w0 >= 0 && w0 < nw, hi_in = w0 + 1 < nw;
+        uint64_t* dst = base + (size_t)b * (BK_NUM_ORIENTS * 7) + w0;
+        const uint64_t* src = stage + b * nw + w0;
+        if (lo_in && hi_in) {
+            const uint64_t v0 = src[0], v1 = src[1];
+            *reinterpret_cast<uint4*>(dst) =
+                make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32));
+        } else if (lo_in) {
+            dst[0] = src[0];
+        } else if (hi_in) {
+            dst[1] = src[1];
+        }
+    }
+}
+
 template <int PARTS>
 __device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
     constexpr int MG_PART_MAX = (BK_NUM_ORIENTS + PARTS - 1) / PARTS;
@@ -1162,7 +1190,7 @@ __device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
     const int set = xcd + MG_XCDS * (j / PARTS), part = j % PARTS;
     if (set * WAVE >= a.n) return;  // a grid rounded up to a multiple of 8 sets: whole idle blocks
     const int glo = part * BK_NUM_ORIENTS / PARTS, ghi = (part + 1) * BK_NUM_ORIENTS / PARTS;
-    const int nw = (ghi - glo) * 7;
+    const int nw = BK_NUM_ORIENTS % PARTS == 0 ? BK_NUM_ORIENTS / PARTS * 7 : (ghi - glo) * 7;
     const int i = set * WAVE + lane;
     const bool live = i < a.n;
     const int idx = live ? i : 0;
@@ -1207,31 +1235,13 @@ __device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
     __syncthreads();
     if (a.out_mask) {
-        // 16-byte stores (the width WRITE_SIZE reads exactly): unit u of board b covers the
-        // 16-byte-aligned word pair 2u - h, 2u - h + 1 of its segment (h = 1 when the
-        // segment starts at an odd word: 637 and 7 are odd, so h = (b + glo + h0) & 1, h0 =
-        // out_mask's own word parity); a pair half outside the segment is left to the
-        // neighbouring segment's block
         const int nb = a.n - set * WAVE < WAVE ? a.n - set * WAVE : WAVE;
-        const int nu = nw / 2 + 1;
-        const int h0 = (int)(((uintptr_t)a.out_mask >> 3) & 1u);
         uint64_t* base = a.out_mask + (size_t)set * WAVE * (BK_NUM_ORIENTS * 7) + glo * 7;
-        for (int k = (int)threadIdx.x; k < nb * nu; k += (int)blockDim.x) {
-            const int b = k / nu, u = k - b * nu;
-            const int w0 = 2 * u - ((b + glo + h0) & 1);
-            const bool lo_in = w0 >= 0 && w0 < nw, hi_in = w0 + 1 < nw;
-            uint64_t* dst = base + (size_t)b * (BK_NUM_ORIENTS * 7) + w0;
-            const uint64_t* src = stage + b * nw + w0;
-            if (lo_in && hi_in) {
-                const uint64_t v0 = src[0], v1 = src[1];
-                *reinterpret_cast<uint4*>(dst) = make_uint4((uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1,
-                                                            (uint32_t)(v1 >> 32));
-            } else if (lo_in) {
-                dst[0] = src[0];
-            } else if (hi_in) {
-                dst[1] = src[1];
-            }
-        }
+        const int hpar = (glo + (int)(((uintptr_t)a.out_mask >> 3) & 1u)) & 1;
+        // equal ranges (7, 13 parts): the segment length is a constant, so the unit -> board
+        // split below is a multiply, not a division
+        constexpr int NWC = BK_NUM_ORIENTS % PARTS == 0 ? BK_NUM_ORIENTS / PARTS * 7 : 0;
+        ml_write_segments<NWC>(stage, base, nb, nw, hpar);
     }
 }
 __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml4(MovegenArgs a) { movegen_ml_body<4>(a); }
