@@ -269,7 +269,9 @@ int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, co
  * forced[i]: the move the agent at game i's stop seat chose in the previous round, placed
  *   first: -1 none (a stopped game stays stopped); g * 400 + 20 r + c a move
  *   (bk_mcts best_move); BK_FORCE_INDEX | k the k-th entry of the mover's legal list in
- *   the reference's order (FastMCTSAgent's child index into get_legal_moves).
+ *   the reference's order (FastMCTSAgent's child index into get_legal_moves);
+ *   BK_FORCE_SKIP: game i is not touched at all (its search is still running: no
+ *   result, no stop info, state and tables unchanged).
  * quick_masks[i] bit p: stop seat p is a FastMCTSAgent; when game i stops there,
  *   stop_out[i] receives its root's FastMCTS inputs: the legal-move count, and
  *   _quick_move_evaluation (agents/fast_mcts_agent.py:285-298: of the first 3 moves by
@@ -277,6 +279,7 @@ int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, co
  *   stable) as its list index and its reward pid * 0.1 + (20 - dist) * 0.05 (:260-283).
  */
 #define BK_FORCE_INDEX 0x40000000
+#define BK_FORCE_SKIP (-2)
 typedef struct bk_stop_info {
     int32_t n_legal;      /* legal moves of the player to move                        */
     int32_t quick_index;  /* list index of _quick_move_evaluation's move              */

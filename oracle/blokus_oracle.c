@@ -144,21 +144,24 @@ static void pyset_clear(or_pyset* s) {
     for (int i = 0; i < 8; ++i) { s->key[i] = K_UNUSED; s->hash[i] = 0; }
 }
 
+/* set_insert_clean: the linear probes advance `entry`; the perturbation step continues
+   from i (not from the last slot probed) */
 static void insert_clean(int16_t* key, int64_t* hash, uint64_t mask, int16_t k, int64_t h) {
-    uint64_t perturb = (uint64_t)h, i = (uint64_t)h & mask;
+    uint64_t perturb = (uint64_t)h, i = (uint64_t)h & mask, e;
     for (;;) {
-        if (key[i] == K_UNUSED) goto found;
+        e = i;
+        if (key[e] == K_UNUSED) goto found;
         if (i + LINEAR_PROBES <= mask) {
             for (int j = 0; j < LINEAR_PROBES; ++j) {
-                ++i;
-                if (key[i] == K_UNUSED) goto found;
+                ++e;
+                if (key[e] == K_UNUSED) goto found;
             }
         }
         perturb >>= PERTURB_SHIFT;
         i = (i * 5 + 1 + perturb) & mask;
     }
 found:
-    key[i] = k; hash[i] = h;
+    key[e] = k; hash[e] = h;
 }
 
 /* set_table_resize */
@@ -448,6 +451,24 @@ int or_set_frontier_table(or_board* b, int p, const int16_t* key, int mask, int 
         s->hash[i] = key[i] >= 0 ? g_cell_hash[key[i]] : key[i] == K_DUMMY ? -1 : 0;
     }
     return 0;
+}
+
+/* set.copy() of a table given slot for slot (test hook): the copy's iteration order into
+   out (<= OR_SET_MAX keys); returns the copy's size, or -1 */
+int or_pyset_copy_list(const int16_t* key, int mask, int fill, int used, int16_t* out) {
+    or_init();
+    if (mask + 1 > OR_SET_MAX || ((mask + 1) & mask) != 0) return -1;
+    or_pyset src, dst;
+    src.mask = mask; src.fill = fill; src.used = used;
+    for (int i = 0; i <= mask; ++i) {
+        src.key[i] = key[i];
+        src.hash[i] = key[i] >= 0 ? g_cell_hash[key[i]] : key[i] == K_DUMMY ? -1 : 0;
+    }
+    pyset_copy(&dst, &src);
+    int n = 0;
+    for (int i = 0; i <= dst.mask; ++i)
+        if (dst.key[i] >= 0) out[n++] = dst.key[i];
+    return n;
 }
 
 int or_unpack_state(or_board* b, const bk_state* s, const int32_t* frontier_lists, const int32_t* frontier_lens) {

@@ -109,6 +109,7 @@ def lib():
             "or_heuristic_score": (C.c_double, [P(Board), C.c_int, C.c_int]),
             "or_arena4_game": (C.c_int, [P(C.c_int32), P(C.c_uint32), C.c_int, C.c_int, P(C.c_int32)]),
             "or_set_frontier_table": (C.c_int, [P(Board), C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int]),
+            "or_pyset_copy_list": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]),
             "or_mcts": (C.c_int, [P(Board), C.c_int, C.c_int, C.c_double, C.c_int, C.c_void_p, C.c_int,
                                   C.c_void_p, P(MT), C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                   P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_void_p, C.c_void_p,
@@ -504,3 +505,16 @@ def arena4_game(kinds, seeds, mcts_iters=64, fast_iters=1000):
     sc = (C.c_int32 * 4)()
     plies = lib().or_arena4_game(k, sd, mcts_iters, fast_iters, sc)
     return plies, list(sc)
+
+
+def pyset_copy_list(key, mask: int, fill: int, used: int) -> list:
+    """set.copy()'s iteration order for a CPython set table given slot for slot (key: int16
+    slots, -1 unused, -2 dummy, else r*20+c); Objects/setobject.c set_merge /
+    set_insert_clean."""
+    import numpy as np
+    k = np.ascontiguousarray(key, dtype=np.int16)
+    out = np.zeros(max(len(k), 1), dtype=np.int16)
+    n = lib().or_pyset_copy_list(k.ctypes.data, int(mask), int(fill), int(used), out.ctypes.data)
+    if n < 0:
+        raise ValueError("or_pyset_copy_list: bad table")
+    return out[:n].tolist()

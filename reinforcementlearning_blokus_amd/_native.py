@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("BK_LIB_PATH") or os.path.join(_HERE, "_lib", "libblok
 OK, EINVAL, EHIP, ENOMEM, EOVERFLOW = 0, -1, -2, -3, -4
 STATUS_CAP, STATUS_UNCERT, STATUS_STOP, STATUS_BADFORCE = 8, 16, 32, 64  # bk_result.status bits
 FORCE_INDEX = 0x40000000  # bk_arena_step forced[i]: the k-th entry of the legal list (BK_FORCE_INDEX | k)
+FORCE_SKIP = -2  # bk_arena_step forced[i]: leave game i untouched (its search is in flight)
 MEM_HOST, MEM_DEVICE = 0, 1
 SEM_ARENA, SEM_ROLLOUT, SEM_ADVANCE = 0, 1, 2
 ORDER_NAIVE, ORDER_FRONTIER = 0, 1

@@ -749,7 +749,8 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             if not drain():
                 time.sleep(50e-6)
         prof["wait_s"] += time.perf_counter() - tm
-        forced_d.copy_(torch.from_numpy(forced))
+        send = np.where(inflight, np.int32(N.FORCE_SKIP), forced)  # in-flight games: not touched
+        forced_d.copy_(torch.from_numpy(send))
     assert not jobs and not fjobs and not inflight.any()
     if fast_pool is not None:
         fast_pool.shutdown()

@@ -973,6 +973,7 @@ struct MovegenArgs {
     uint8_t* out_mask4;      // has_moves mode
     int32_t groups;          // k_movegen_g: orientation groups per board-player
     uint64_t* out_mask;      // k_movegen_m: n x 91 x 7 (bit 20 r + c of the 400-bit mask) or NULL
+    uint32_t part_masks[13][3];  // k_movegen_ml: bit i of part q = stencil entry i's orientation in range q
 };
 
 __device__ __forceinline__ void load_state_rows(const bk_state* s, uint32_t (&own)[4][20], uint32_t (&occ)[20]) {
@@ -1122,34 +1123,29 @@ __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
 __global__ void k_movegen_m(MovegenArgs a);
 #endif
 
-// Dense rows of the class's table entries i0 <= i < i1 whose orientation lies in
-// [glo, ghi), every Wp-th of them from wave w on (k_movegen_ml); seen counts the in-range
-// entries of the earlier classes (wave-uniform)
+// Dense rows of the class's table entries i0 <= i < i1 whose orientation lies in this
+// block's range (bit i of pm, no table loads), every Wp-th of them from wave w on
+// (k_movegen_ml); rr counts the in-range entries of the earlier classes modulo Wp
+// (wave-uniform)
 template <int H, int... T, typename F>
-__device__ __forceinline__ void rows_class_range(int i0, int i1, int glo, int ghi, int w, int Wp, int& seen,
+__device__ __forceinline__ void rows_class_range(int i0, int i1, const uint32_t (&pm)[3], int w, int Wp, int& rr,
                                                  const Planes& P, F&& f) {
 #pragma unroll 1
     for (int i = i0; i < i1; ++i) {
+        const uint32_t word = i < 32 ? pm[0] : i < 64 ? pm[1] : pm[2];
+        if (!((word >> (i & 31)) & 1u)) continue;
+        const bool mine = rr == w;
+        rr = rr + 1 == Wp ? 0 : rr + 1;
+        if (!mine) continue;
         const uint32_t w0 = kClass[i][0], w1 = kClass[i][1];
-        const int g = (int)(w0 >> 8);
-        if (g < glo || g >= ghi) continue;
-        if (seen++ % Wp != w) continue;
         uint32_t ok[20];
 #pragma unroll
         for (int r = 0; r < 20; ++r) ok[r] = 0u;
         StencilClass<H, T...>::scan(P, w1, [&](int r, uint32_t v) { ok[r] = v; });
-        f(g, w0 & 0xFFu, ok);
+        f((int)(w0 >> 8), w0 & 0xFFu, ok);
     }
 }
 
-// k_movegen_m with whole-line writes.  The 91 orientations are split into PARTS
-// contiguous ranges; a block is one (set of 64 board-players, range) pair whose
-// blockDim / 64 waves share the range's stencil entries.  Each board-player's masks for
-// the range are staged in LDS (64 x ceil(91 / PARTS) x 7 u64: 82 KB at 4 parts, 47 KB at
-// 7, 25 KB at 13) and then written as one contiguous segment per board-player with
-// coalesced 16-B stores, instead of 56-B pieces at a 5,096-B stride.  The PARTS blocks
-// of a set run on the same XCD, so the lines their segments share merge in that L2.
-// Entry points k_movegen_ml4 / 7 / 13 (bk_movegen_mask picks one; BK_MG_PARTS).
 #define MG_PART_WAVES_MAX 8
 #if BK_DEF(BK_U_MOVEGEN)
 // The block's staged segments (board-player b: words [0, nw) of stage + b * nw) to
@@ -1228,8 +1224,9 @@ __device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
 #pragma unroll
         for (int q = 0; q < 7; ++q) mine[g * 7 + q] = wd[q];
     };
-    int seen = 0;
-#define BK_ROWS_RANGE(i0, i1, H, ...) rows_class_range<H, __VA_ARGS__>(i0, i1, glo, ghi, w, Wp, seen, P, emit);
+    int rr = 0;
+    const uint32_t pm[3] = {a.part_masks[part][0], a.part_masks[part][1], a.part_masks[part][2]};
+#define BK_ROWS_RANGE(i0, i1, H, ...) rows_class_range<H, __VA_ARGS__>(i0, i1, pm, w, Wp, rr, P, emit);
     BK_CLASS_LIST(BK_ROWS_RANGE)
 #undef BK_ROWS_RANGE
     if (live && a.out_count && total) atomicAdd(a.out_count + i, total);
@@ -1311,10 +1308,10 @@ struct FsetRef {  // one player's table: runs of 2^sh slots, run j at key[j * st
     const uint64_t* hash;  // hash((r, c)) by cell
     int sh = 1;       // log2 of the run length
     uint32_t* dirty = nullptr;  // if set: bit j marks 8-slot chunk j written (all: a resize)
-    __host__ __device__ __forceinline__ int16_t& at(uint64_t i) const {
-        return key[(i >> sh) * (uint64_t)stride + (i & ((1u << sh) - 1u))];
+    __host__ __device__ __forceinline__ int16_t& at(uint32_t i) const {
+        return key[(i >> sh) * (uint32_t)stride + (i & ((1u << sh) - 1u))];
     }
-    __host__ __device__ __forceinline__ void mark(uint64_t i) const {
+    __host__ __device__ __forceinline__ void mark(uint32_t i) const {
         if (dirty) *dirty |= 1u << ((i >> 3) & 31u);
     }
 };
@@ -1323,25 +1320,27 @@ __host__ __device__ __forceinline__ FsetRef fs_ref(bk_fset* s, int p, const uint
     return FsetRef{s->key[p], 2, &s->mask[p], &s->fill[p], &s->used[p], BK_FSET_SLOTS, htab};
 }
 
-// set_insert_clean: first unused slot of the probe sequence
+// set_insert_clean: first unused slot of the probe sequence.  The linear probes walk
+// the slots after i, but the next perturbation step starts from i itself, not from the
+// last slot probed (CPython advances `entry`, not `i`; checked against CPython 3.10's
+// set.copy() in tests/test_fset_copy.py)
 __host__ __device__ inline void fs_insert_clean(FsetRef t, uint32_t mask, int16_t k) {
     const uint64_t h = t.hash[k];
     uint64_t perturb = h;
-    uint64_t i = h & mask;
-    for (;;) {
-        if (t.at(i) == FS_UNUSED) break;
-        bool hit = false;
-        if (i + FS_PROBES <= mask) {
-            for (int j = 0; j < FS_PROBES; ++j) {
-                ++i;
-                if (t.at(i) == FS_UNUSED) { hit = true; break; }
-            }
+    uint32_t i = (uint32_t)h & mask, e = i;
+    uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
+    while (t.at(e) != FS_UNUSED) {
+        if (left > 0u) {
+            --left;
+            ++e;
+        } else {
+            perturb >>= FS_SHIFT;
+            i = (i * 5u + 1u + (uint32_t)perturb) & mask;
+            e = i;
+            left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
         }
-        if (hit) break;
-        perturb >>= FS_SHIFT;
-        i = (i * 5 + 1 + perturb) & mask;
     }
-    t.at(i) = k;
+    t.at(e) = k;
 }
 
 // set_table_resize(minused): fresh table, active entries re-inserted in slot order.
@@ -1369,37 +1368,43 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
     const uint64_t h = t.hash[k];
     const uint32_t mask = *t.mask;
+    // One flat loop over the probe sequence (a divergent nested loop costs the wave far
+    // more exec-mask bookkeeping than its VALU work): from i = hash & mask the 10 slots
+    // i .. i + 9 when they fit below mask (LINEAR_PROBES 9), else slot i alone, then
+    // i = (5 i + 1 + perturb) & mask with perturb >>= 5.  Slot indices stay 32-bit: only
+    // the low bits of 5 i + 1 + perturb survive the mask.
     uint64_t perturb = h;
-    uint64_t i = h & mask, e = 0;
-    int64_t freeslot = -1;
+    uint32_t i = (uint32_t)h & mask, e = i;
+    uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
+    int32_t freeslot = -1;
+    int16_t kk;
     for (;;) {
-        e = i;
-        int probes = (i + FS_PROBES <= mask) ? FS_PROBES : 0;
-        bool unused = false;
-        for (;;) {
-            const int16_t kk = t.at(e);
-            if (kk == FS_UNUSED) { unused = true; break; }
-            if (kk == k) {
-                if (!add) {
-                    t.at(e) = FS_DUMMY;
-                    t.mark(e);
-                    *t.used -= 1;
-                }
-                return true;
-            }
-            if (kk == FS_DUMMY) freeslot = (int64_t)e;
+        kk = t.at(e);
+        if (kk == FS_UNUSED || kk == k) break;
+        if (kk == FS_DUMMY) freeslot = (int32_t)e;
+        if (left > 0u) {
+            --left;
             ++e;
-            if (probes-- == 0) break;
+        } else {
+            perturb >>= FS_SHIFT;
+            i = (i * 5u + 1u + (uint32_t)perturb) & mask;
+            e = i;
+            left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
         }
-        if (unused) break;
-        perturb >>= FS_SHIFT;
-        i = (i * 5 + 1 + perturb) & mask;
+    }
+    if (kk == k) {  // present: discard leaves a dummy, add is a no-op
+        if (!add) {
+            t.at(e) = FS_DUMMY;
+            t.mark(e);
+            *t.used -= 1;
+        }
+        return true;
     }
     if (!add) return true;
     if (freeslot >= 0) {
         *t.used += 1;
-        t.at(freeslot) = k;
-        t.mark((uint64_t)freeslot);
+        t.at((uint32_t)freeslot) = k;
+        t.mark((uint32_t)freeslot);
         return true;
     }
     *t.fill += 1;
@@ -1547,24 +1552,22 @@ struct SlotBits {
 // slots are `o` (marks the slot used)
 __device__ __forceinline__ uint32_t fs_clean_slot(uint64_t h, uint32_t mask, SlotBits& o) {
     uint64_t perturb = h;
-    uint32_t i = (uint32_t)(h & mask);
+    uint32_t i = (uint32_t)h & mask, e = i;
+    uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
 #pragma unroll 1
-    for (;;) {
-        if (!o.test(i)) break;
-        bool hit = false;
-        if (i + FS_PROBES <= mask) {
-#pragma unroll 1
-            for (int j = 0; j < FS_PROBES; ++j) {
-                ++i;
-                if (!o.test(i)) { hit = true; break; }
-            }
+    while (o.test(e)) {  // fs_insert_clean's sequence
+        if (left > 0u) {
+            --left;
+            ++e;
+        } else {
+            perturb >>= FS_SHIFT;
+            i = (i * 5u + 1u + (uint32_t)perturb) & mask;
+            e = i;
+            left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
         }
-        if (hit) break;
-        perturb >>= FS_SHIFT;
-        i = (uint32_t)(((uint64_t)i * 5u + 1u + perturb) & mask);
     }
-    o.set(i);
-    return i;
+    o.set(e);
+    return e;
 }
 
 // fs_copy_dev's size rule: the copy of a table with `used` active keys has newsize
@@ -2501,6 +2504,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 }
                 ++handed;
                 if (next >= a.n_playouts) { done = true; break; }
+                // bk_arena_step: a game whose search is still running is left untouched
+                if (HEUR && a.forced && a.forced[next] == BK_FORCE_SKIP) continue;
                 start_game<FR>(a, g, slab, slot, next, htab);
             }
             if (arena) {
@@ -4589,6 +4594,14 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
         if (const char* env = getenv("BK_MG_PART_WAVES")) wp = atoi(env);  // tuning override
         wp = wp < 1 ? 1 : (wp > MG_PART_WAVES_MAX ? MG_PART_WAVES_MAX : wp);
         const dim3 grid(sets * parts), blk(wp * WAVE);
+        static const uint32_t kClassHost[BK_NUM_ORIENTS][2] = BK_CLASS_TABLE_INIT;
+        memset(a.part_masks, 0, sizeof a.part_masks);
+        for (int i = 0; i < BK_NUM_ORIENTS; ++i) {
+            const int g = (int)(kClassHost[i][0] >> 8);
+            int q = 0;
+            while ((q + 1) * BK_NUM_ORIENTS / parts <= g) ++q;  // range q: [q 91 / parts, (q + 1) 91 / parts)
+            a.part_masks[q][i >> 5] |= 1u << (i & 31);
+        }
         if (parts == 4) {
             h->last_kernel = "k_movegen_ml4";
             hipLaunchKernelGGL(k_movegen_ml4, grid, blk, 0, h->cur, a);
@@ -4872,7 +4885,7 @@ int bk_arena_step(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const
         return set_err(h, BK_EINVAL, "bk_arena_step: quick_masks goes with stop_out%s", "");
     if (mem == BK_MEM_HOST && forced)
         for (int32_t i = 0; i < n; ++i)
-            if (forced[i] < -1 || (forced[i] >= 0 && !(forced[i] & BK_FORCE_INDEX) && forced[i] >= BK_NUM_ORIENTS * 400))
+            if (forced[i] < BK_FORCE_SKIP || (forced[i] >= 0 && !(forced[i] & BK_FORCE_INDEX) && forced[i] >= BK_NUM_ORIENTS * 400))
                 return set_err(h, BK_EINVAL, "bk_arena_step: forced move out of range%s", "");
     if (n == 0) return BK_OK;
     return launch_playouts(h, states, n, nullptr, n, cfg, nullptr, out, states, mem, sets, sets, seat_masks,

@@ -1,0 +1,153 @@
+"""set.copy() of the frontier tables (set_merge into an empty set -> set_insert_clean),
+against CPython itself (this interpreter is the reference's 3.10).  CPU only.
+
+A Python restatement of Objects/setobject.c (add / discard / resize / copy) builds each
+table slot for slot and is pinned first: its iteration order equals list(s) and
+list(s.copy()) for every trial.  Its tables then go through the library's host
+restatement (bk_fset_copy, the code the kernels run) and the oracle's (or_pyset_copy_list),
+and both copies must list the keys in CPython's order.  The trials include copies whose
+clean re-insert meets a run of 10 occupied slots, where set_insert_clean's next
+perturbation step starts from i, not from the last slot probed (the case a restatement
+that advanced i got wrong)."""
+import random
+
+import numpy as np
+
+from oracle import pyoracle as O
+from reinforcementlearning_blokus_amd import _native as N
+
+M64 = (1 << 64) - 1
+DUMMY = "dummy"
+
+
+class PySet:
+    """Objects/setobject.c (3.10) tables over (r, c) keys; `advance_i` reproduces the old,
+    wrong clean insert (the perturbation step continuing from the last slot probed)."""
+
+    def __init__(self, advance_i=False):
+        self.adv = advance_i
+        self.mask, self.tab, self.fill, self.used = 7, [None] * 8, 0, 0
+
+    def _insert_clean(self, tab, mask, k):
+        h = hash(k) & M64
+        perturb, i = h, h & mask
+        while True:
+            if tab[i] is None:
+                tab[i] = k
+                return
+            if i + 9 <= mask:
+                e = i
+                for _ in range(9):
+                    e += 1
+                    if tab[e] is None:
+                        tab[e] = k
+                        return
+                if self.adv:
+                    i = e
+            perturb >>= 5
+            i = (i * 5 + 1 + perturb) & mask
+
+    def _resize(self, minused):
+        size = 8
+        while size <= minused:
+            size <<= 1
+        old, self.tab, self.mask, self.fill = self.tab, [None] * size, size - 1, self.used
+        for k in old:
+            if k is not None and k is not DUMMY:
+                self._insert_clean(self.tab, self.mask, k)
+
+    def _probe(self, k):
+        h = hash(k) & M64
+        perturb, i, mask = h, h & self.mask, self.mask
+        while True:
+            e, probes = i, (9 if i + 9 <= mask else 0)
+            while True:
+                yield e
+                e += 1
+                if probes == 0:
+                    break
+                probes -= 1
+            perturb >>= 5
+            i = (i * 5 + 1 + perturb) & mask
+
+    def add(self, k):
+        free = None
+        for e in self._probe(k):
+            v = self.tab[e]
+            if v is None:
+                if free is not None:
+                    self.tab[free] = k
+                    self.used += 1
+                    return
+                self.tab[e] = k
+                self.fill += 1
+                self.used += 1
+                if self.fill * 5 >= self.mask * 3:
+                    self._resize(self.used * 4)
+                return
+            if v is DUMMY:
+                free = e
+            elif v == k:
+                return
+
+    def discard(self, k):
+        for e in self._probe(k):
+            v = self.tab[e]
+            if v is None:
+                return
+            if v is not DUMMY and v == k:
+                self.tab[e] = DUMMY
+                self.used -= 1
+                return
+
+    def copy(self):
+        d = PySet(self.adv)
+        if self.used == 0:
+            return d
+        if self.used * 5 >= 7 * 3:
+            d._resize(self.used * 2)
+        if d.mask == self.mask and self.fill == self.used:
+            d.tab, d.fill, d.used = list(self.tab), self.fill, self.used
+            return d
+        d.fill = d.used = self.used
+        for k in self.tab:
+            if k is not None and k is not DUMMY:
+                d._insert_clean(d.tab, d.mask, k)
+        return d
+
+    def order(self):
+        return [k for k in self.tab if k is not None and k is not DUMMY]
+
+    def slots(self):
+        return [-1 if k is None else -2 if k is DUMMY else k[0] * 20 + k[1] for k in self.tab]
+
+
+def test_set_copy_matches_cpython():
+    rnd = random.Random(20260301)
+    cells = [(r, c) for r in range(20) for c in range(20)]
+    runs = trials = 0
+    for _ in range(4000):
+        s, e, old = set(), PySet(), PySet(advance_i=True)
+        for _ in range(rnd.randint(20, 220)):
+            k = rnd.choice(cells)
+            if rnd.random() < 0.6:
+                s.add(k), e.add(k), old.add(k)
+            else:
+                s.discard(k), e.discard(k), old.discard(k)
+        if e.mask + 1 > N.FSET_SLOTS:
+            continue
+        trials += 1
+        ref = [r * 20 + c for r, c in s.copy()]
+        assert e.order() == list(s)
+        assert [r * 20 + c for r, c in e.copy().order()] == ref
+        runs += [r * 20 + c for r, c in old.copy().order()] != ref
+        fs = N.fset_new(1)
+        slots = np.array(e.slots(), dtype=np.int16)
+        fs["key"][0, 0, : len(slots)] = slots
+        fs["mask"][0, 0], fs["fill"][0, 0], fs["used"][0, 0] = e.mask, e.fill, e.used
+        dst = N.fset_new(1)
+        N.fset_copy(dst, fs)
+        assert N.fset_list(dst, 0) == ref
+        assert O.pyset_copy_list(slots, e.mask, e.fill, e.used) == ref
+    assert trials > 2000
+    assert runs > 0  # the linear-run case is exercised
