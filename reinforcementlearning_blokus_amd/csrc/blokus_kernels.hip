@@ -529,13 +529,18 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     BK_ENTRY_LIST(BK_COUNT_ENTRY)
 #undef BK_COUNT_ENTRY
 #else
+    // the running total is pinned after every class (the empty asm): left to itself the
+    // compiler keeps the 49 class totals live to the end of the stencil and sums them
+    // there, ~40 VGPRs that spilled in the frontier-order kernel
     if constexpr (PAIR) {
         const bool odd = (lane & 1) != 0;
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd, L);
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd, L); \
+        asm volatile("" : "+v"(t));
         BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     } else {
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, L);
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, L); \
+        asm volatile("" : "+v"(t));
         BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     }
