@@ -71,6 +71,11 @@
 // 1: the stencil skips anchor rows no lane of the wave can use (live_anchor_rows) --
 // measured no faster: the per-row branches cost the kernel spills;
 // 0: the round-3 stencil (every anchor row), a build for the A/B measurement
+// locate pass 2 skips frontier cells with no anchor row within the piece's height (A/B
+// build: -DBK_LOCATE_SKIP=0)
+#ifndef BK_LOCATE_SKIP
+#define BK_LOCATE_SKIP 1
+#endif
 #ifndef BK_ROWSKIP_BUILD
 #define BK_ROWSKIP_BUILD 0
 #endif
@@ -352,12 +357,15 @@ __device__ __forceinline__ LiveRows live_anchor_rows(const Planes& P) {
 // dead once the move's orientation is picked; the same bytes then hold the mover's
 // B/C rows 0..19 as [row][lane]{B, C} pairs for locate_move_lds.
 #define ROLL_WORDS_PER_WAVE (40 * WAVE)
-// resident 256-lane blocks per CU for k_rollout / k_advance (the launch bound).  3 (168
-// VGPRs): with the vertical-pair planes (tools/gen_tables.py BK_GEN_VPAIR=1, 243
-// instead of 287 terms) the kernel needs 2 (226 VGPRs) and measured 42.2 M vs 48.7 M
-// playouts/s -- the lost latency hiding costs more than the 15 % fewer stencil ops
+// resident 256-lane blocks per CU for k_rollout / k_advance (the launch bound).  4 (128
+// VGPRs, 8 B/lane of scratch; 4 x 40 KB fills the CU's LDS exactly): config 3's 262,144
+// playouts are then one per resident slot, 62.3 M vs 61.0 M playouts/s at 3 (168 VGPRs;
+// profiles/r04/sweeps/r04i).  With the vertical-pair planes (tools/gen_tables.py
+// BK_GEN_VPAIR=1, 243 instead of 287 terms) the kernel needs 2 (226 VGPRs) and measured
+// 42.2 M vs 48.7 M playouts/s -- the lost latency hiding costs more than the 15 % fewer
+// stencil ops
 #ifndef ROLL_BLOCKS_PER_CU
-#define ROLL_BLOCKS_PER_CU 3
+#define ROLL_BLOCKS_PER_CU 4
 #endif
 // frontier tables smaller than this many slots are staged in LDS for place_frontier
 // (0: probe the table in global memory).  k_rollout_fr: 64, so its area stays at the 40
@@ -756,6 +764,7 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
         sh[k] = cell & 0xFFu;
         cd[k] = (int)(cell >> 8);
     }
+    uint32_t arows = 0;  // bit r + 4: anchor row r holds a legal anchor (a superset later)
 #pragma unroll
     for (int r = 0; r < 20; ++r) {
         const int rr = r < rlim ? r : rlim;
@@ -768,7 +777,9 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
         ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
         // the anchors go to the C half: row r's C word is not read again (later rows
         // read rows >= r + 1), and the B half stays intact for frontier_ops
-        rows[r * WAVE].y = r <= rlim ? (ac & ~ab) : 0u;
+        const uint32_t okr = r <= rlim ? (ac & ~ab) : 0u;
+        rows[r * WAVE].y = okr;
+        arows |= okr ? (1u << (r + 4)) : 0u;
     }
     // Pass 2 reads the table 16 slots per pair of uint4 loads into registers, all
     // indices static (a dynamically indexed key array would live in scratch memory); the
@@ -780,6 +791,7 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
     // anchors of one frontier cell are distinct, and counting them as a set keeps every
     // other slot's contribution exact).
     const int H = (int)((info >> 16) & 0xFFu);
+    const uint32_t hmask = (1u << H) - 1u;
     uint32_t rev[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
     for (int k = 0; k < 5; ++k)
@@ -799,6 +811,9 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
             const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
             if (hit_f >= 0 || f < 0 || b0 + j > mask) continue;
             const int fr = f / 20, fc = f - 20 * fr;
+            // no anchor row among fr - H + 1 .. fr: this cell adds no anchors (skip the
+            // row reads); anchors counted later only clear bits, so arows stays a superset
+            if (BK_LOCATE_SKIP && !((arows >> (fr + 5 - H)) & hmask)) continue;
             uint32_t hm[5], tot = 0;
 #pragma unroll
             for (int d = 0; d < 5; ++d) {
@@ -1158,16 +1173,18 @@ __device__ __forceinline__ void rows_class_range(int i0, int i1, const uint32_t 
 // board b covers the 16-byte-aligned word pair 2u - h, 2u - h + 1 of its segment (h = 1
 // when the segment starts at an odd word: 637 is odd, so h = (b + hpar) & 1); a pair half
 // outside the segment belongs to the neighbouring segment's block.  NWC > 0: nw, known.
-template <int NWC>
-__device__ __forceinline__ void ml_write_segments(const uint64_t* stage, uint64_t* base, int nb, int nw_rt, int hpar) {
-    const int nw = NWC > 0 ? NWC : nw_rt;
-    const int nu = nw / 2 + 1;
+template <int NU>
+__device__ __forceinline__ void ml_write_segments(const uint64_t* stage, uint64_t* base, int nb, int nw, int hpar) {
+    // NU = the most units a segment of this kernel's ranges needs (a compile-time
+    // constant, so the unit -> board split is a multiply); units past a shorter
+    // segment's end write nothing
 #pragma unroll 1
-    for (int k = (int)threadIdx.x; k < nb * nu; k += (int)blockDim.x) {
-        const int b = k / nu, u = k - b * nu;
+    for (int k = (int)threadIdx.x; k < nb * NU; k += (int)blockDim.x) {
+        const int b = k / NU, u = k - b * NU;
         const int w0 = 2 * u - ((b + hpar) & 1);
         const bool lo_in = w0 >= 0 && w0 < nw, hi_in = w0 + 1 < nw;
-        uint64_t* dst = base + (size_t)b * (BK_NUM_ORIENTS * 7) + w0;
+        const uint32_t off = (uint32_t)b * (BK_NUM_ORIENTS * 7) + (uint32_t)w0;  // words, < 2^31
+        uint64_t* dst = base + off;
         const uint64_t* src = stage + b * nw + w0;
         if (lo_in && hi_in) {
             const uint64_t v0 = src[0], v1 = src[1];
@@ -1240,10 +1257,7 @@ __device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
         const int nb = a.n - set * WAVE < WAVE ? a.n - set * WAVE : WAVE;
         uint64_t* base = a.out_mask + (size_t)set * WAVE * (BK_NUM_ORIENTS * 7) + glo * 7;
         const int hpar = (glo + (int)(((uintptr_t)a.out_mask >> 3) & 1u)) & 1;
-        // equal ranges (7, 13 parts): the segment length is a constant, so the unit -> board
-        // split below is a multiply, not a division
-        constexpr int NWC = BK_NUM_ORIENTS % PARTS == 0 ? BK_NUM_ORIENTS / PARTS * 7 : 0;
-        ml_write_segments<NWC>(stage, base, nb, nw, hpar);
+        ml_write_segments<MG_PART_MAX * 7 / 2 + 1>(stage, base, nb, nw, hpar);
     }
 }
 __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml4(MovegenArgs a) { movegen_ml_body<4>(a); }
