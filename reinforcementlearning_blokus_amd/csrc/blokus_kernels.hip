@@ -846,6 +846,115 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
     out_c = found_c;
 }
 
+// locate_move_frontier for a lane PAIR holding one search (k_mcts_pair): both lanes call
+// it with the even lane's orientation, rank, table and LDS row column (rows).  Pass 1:
+// the even lane computes anchor rows 0..9 and the odd lane rows 10..19 (all reads before
+// the writes, so no lane overwrites a C row the other still reads).  Pass 2: both walk
+// the same table slots; the even lane tests piece rows d = 0..2 and the odd lane d = 3, 4,
+// and the two partial counts are added across the pair (one DPP move), so a slot costs
+// three row reads instead of five.  Anchors are cleared by the lane that counted them
+// (different rows), so the walk sees exactly the single-lane state.  Same result as
+// locate_move_frontier in both lanes.
+template <int RS = 2>
+__device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2* rows, const int16_t* key, int mask,
+                                                     bool odd, int& out_r, int& out_c) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    const int rlim = 20 - (int)((info >> 16) & 0xFFu);
+    const uint2* base[5];
+    uint32_t sh[5];
+    int cd[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        base[k] = rows + (cell >> 8) * WAVE;
+        sh[k] = cell & 0xFFu;
+        cd[k] = (int)(cell >> 8);
+    }
+    const int r0 = odd ? 10 : 0;
+    uint32_t okv[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const int r = r0 + i;
+        const int rr = r < rlim ? r : rlim;
+        uint2 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) v[k] = base[k][rr * WAVE];
+        uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
+        uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
+        ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
+        ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
+        okv[i] = r <= rlim ? (ac & ~ab) : 0u;
+    }
+    uint32_t arows = 0;  // bit r + 4: anchor row r holds a legal anchor (a superset later)
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        rows[(r0 + i) * WAVE].y = okv[i];
+        arows |= okv[i] ? (1u << (r0 + i + 4)) : 0u;
+    }
+    arows |= (uint32_t)__shfl_xor((int)arows, 1);
+    const int H = (int)((info >> 16) & 0xFFu);
+    const uint32_t hmask = (1u << H) - 1u;
+    uint32_t rev[5] = {0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+#pragma unroll
+        for (int d = 0; d < 5; ++d) rev[d] |= (k < n && cd[k] == d) ? (1u << (4 - (int)sh[k])) : 0u;
+    // this lane's piece rows d = d0 + t (t < 3 even, t < 2 odd)
+    const int d0 = odd ? 3 : 0;
+    uint32_t rt[3];
+    rt[0] = odd ? rev[3] : rev[0];
+    rt[1] = odd ? rev[4] : rev[1];
+    rt[2] = odd ? 0u : rev[2];
+    uint32_t cnt = 0;
+    int hit_f = -1;
+    const bk_u4_alias* k4 = reinterpret_cast<const bk_u4_alias*>(key);
+    uint4 qa = k4[0], qb = k4[1];  // tables hold >= 8 slots; the storage has 256
+#pragma unroll 1
+    for (int b0 = 0; b0 <= mask && hit_f < 0; b0 += 16) {
+        const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
+        const uint4 na = k4[(nb0 >> 4) * RS], nb = k4[(nb0 >> 4) * RS + 1];
+        const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            if (hit_f >= 0 || f < 0 || b0 + j > mask) continue;
+            const int fr = f / 20, fc = f - 20 * fr;
+            if (BK_LOCATE_SKIP && !((arows >> (fr + 5 - H)) & hmask)) continue;
+            uint32_t hm[3], tot = 0;
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                const int d = d0 + t;
+                const int ar = fr - d;
+                hm[t] = (d < H && ar >= 0) ? (rows[(ar < 0 ? 0 : ar) * WAVE].y & ((rt[t] << fc) >> 4)) : 0u;
+                tot += __builtin_popcount(hm[t]);
+            }
+            const uint32_t both = tot + (uint32_t)__shfl_xor((int)tot, 1);
+            if (cnt + both > kk) { hit_f = f; continue; }
+#pragma unroll
+            for (int t = 0; t < 3; ++t)
+                if (hm[t]) rows[(fr - d0 - t) * WAVE].y &= ~hm[t];
+            cnt += both;
+        }
+        qa = na; qb = nb;
+    }
+    int found_r = -1, found_c = 0;
+    if (hit_f >= 0) {  // the (kk - cnt)-th new anchor of frontier cell hit_f, in cell order
+        const int fr = hit_f / 20, fc = hit_f - 20 * fr;
+        uint32_t rem = kk - cnt;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            if (k >= n || found_r >= 0) continue;
+            const int ar = fr - cd[k], acl = fc - (int)sh[k];
+            if (ar < 0 || acl < 0) continue;
+            if (!((rows[ar * WAVE].y >> acl) & 1u)) continue;
+            if (rem == 0u) { found_r = ar; found_c = acl; } else { --rem; }
+        }
+    }
+    out_r = found_r;
+    out_c = found_c;
+}
+
 // The set operations of update_frontier_after_move that CHANGE the mover's set.  The
 // reference runs 9 ops per placed cell q (o = 0: discard the cell, 1..4: add the
 // diagonals (-1,-1) (-1,1) (1,-1) (1,1) when addable, 5..8: discard the orthogonals
@@ -3538,37 +3647,41 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         uint32_t total = movegen_counts<true, PAIR>(P, avail, my, lane);
         if constexpr (PAIR) total += (uint32_t)__shfl_xor((int)total, 1);
         SECT(9);
-        if (idle) continue;
-        bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
-        uint32_t k;
-        if (m.mode == MC_EXPAND) {
-            bk_mcts_node* nd = pool + m.node;
-            uint32_t n_legal = nd->n_legal, n_exp = nd->n_exp;
-            if (!(nd->flags & BK_MCTS_NODE_EVALUATED)) {  // MCTSNode._initialize_untried_moves
-                n_legal = total;
-                nd->n_legal = (uint16_t)n_legal;
-                nd->child0 = -1;
-                nd->flags = BK_MCTS_NODE_EVALUATED;
-            }
-            if (n_legal != total) {  // an evaluated node's list cannot change
-                m.status |= BK_MCTS_EINTERNAL;
-                m.mode = MC_SELECT;
-                continue;
-            }
-            if (n_legal == n_exp) {  // no legal move: terminal leaf
-                mc_sim_terminal(a, m, L);
-                continue;
-            }
-            k = n_legal - n_exp - 1u;  // untried_moves.pop(): the last list entry
-        } else {
-            if (total == 0u) {  // _rollout: no legal move -> break
+        // PAIR: the odd lane of a busy pair stays for the pair's locate (below)
+        if (!PAIR && idle) continue;
+        bool act = !idle;
+        bk_mcts_node* pool = a.nodes + (size_t)(act ? m.game : 0) * a.cfg.node_cap;
+        uint32_t k = 0;
+        if (act) {
+            if (m.mode == MC_EXPAND) {
+                bk_mcts_node* nd = pool + m.node;
+                uint32_t n_legal = nd->n_legal, n_exp = nd->n_exp;
+                if (!(nd->flags & BK_MCTS_NODE_EVALUATED)) {  // MCTSNode._initialize_untried_moves
+                    n_legal = total;
+                    nd->n_legal = (uint16_t)n_legal;
+                    nd->child0 = -1;
+                    nd->flags = BK_MCTS_NODE_EVALUATED;
+                }
+                if (n_legal != total) {  // an evaluated node's list cannot change
+                    m.status |= BK_MCTS_EINTERNAL;
+                    m.mode = MC_SELECT;
+                    act = false;
+                } else if (n_legal == n_exp) {  // no legal move: terminal leaf
+                    mc_sim_terminal(a, m, L);
+                    act = false;
+                } else {
+                    k = n_legal - n_exp - 1u;  // untried_moves.pop(): the last list entry
+                }
+            } else if (total == 0u) {  // _rollout: no legal move -> break
                 mc_complete(a, m, L, (double)(mc_score(m, m.player) - m.score0), false);
-                continue;
+                act = false;
+            } else {
+                k = HEUR ? 0u : mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
             }
-            k = HEUR ? 0u : mc_randint(a.mt + (size_t)m.game * (FM_N + 1), m.mt_pos, total);
         }
-        uint32_t kk;
-        int gs = pick_orient<PAIR>(my, lane, k, kk);
+        if (!PAIR && !act) continue;
+        uint32_t kk = 0;
+        int gs = act ? pick_orient<PAIR>(my, lane, k, kk) : 0;
         // HEUR: a rollout ply's move is HeuristicAgent.select_action's (heur_* above)
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         double h_target = 0.0, h_R = 0.0, h_total = 0.0;
@@ -3595,9 +3708,22 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
         FsLane* T = &L->A;  // the node board at expansion, the rollout's sim board after it
-        int ar, ac;
+        int ar = -1, ac = 0;
         SECT(10);
-        if (hroll) {
+        if constexpr (PAIR) {
+            // both lanes of a busy pair: the even lane's orientation, rank and table
+            const int o = lane & ~1;
+            const bool pact = __shfl((int)act, o) != 0;
+            const int pgs = __shfl(gs, o);
+            const uint32_t pkk = (uint32_t)__shfl((int)kk, o);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
+            if (pact) {
+                uint2* prow = reinterpret_cast<uint2*>(my) + o;
+                if (staged) locate_frontier_pair<DMA_RUN_DWORDS / 4>(pgs, pkk, prow, stage_q, (int)omask, (lane & 1) != 0, ar, ac);
+                else locate_frontier_pair(pgs, pkk, prow, ofs->key[cp], (int)omask, (lane & 1) != 0, ar, ac);
+            }
+            if (!act) continue;
+        } else if (hroll) {
             if (gs < 0) {
                 ar = -1;
                 ac = 0;
@@ -3606,10 +3732,6 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
                                    ar, ac, h_unc);
             }
             if (h_unc) m.status |= BK_MCTS_EUNCERT;
-        } else if (PAIR) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
-            if (staged) locate_move_frontier<DMA_RUN_DWORDS / 4>(gs, kk, rows_lds, stage_q, (int)omask, ar, ac);
-            else locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
         } else {
             locate_move_frontier(gs, kk, rows_lds, T->s.key[p], T->s.mask[p], ar, ac);
         }
