@@ -1292,7 +1292,7 @@ __device__ __forceinline__ void ml_write_segments(const uint64_t* stage, uint64_
         const int b = k / NU, u = k - b * NU;
         const int w0 = 2 * u - ((b + hpar) & 1);
         const bool lo_in = w0 >= 0 && w0 < nw, hi_in = w0 + 1 < nw;
-        const uint32_t off = (uint32_t)b * (BK_NUM_ORIENTS * 7) + (uint32_t)w0;  // words, < 2^31
+        const int off = b * (BK_NUM_ORIENTS * 7) + w0;  // words (w0 may be -1: signed)
         uint64_t* dst = base + off;
         const uint64_t* src = stage + b * nw + w0;
         if (lo_in && hi_in) {
