@@ -257,7 +257,8 @@ int bk_rollout_frontier(bk_handle h, const bk_state* roots, const bk_fset* root_
  * across calls (0 at the start).  out[i]: status BK_STATUS_STOP (32) = stopped at a stop
  * seat (current_player of states[i]), else the finished game's result (status bit 3: cut
  * by max_plies; passes / turns in out count this call only).  cfg: BK_SEM_ARENA,
- * BK_ORDER_FRONTIER, BK_RNG_NUMPY_MT, seats_share_stream 0.
+ * BK_ORDER_FRONTIER, BK_RNG_NUMPY_MT, seats_share_stream 0.  Device pointers: rng_state
+ * 16-byte aligned.
  */
 #define BK_STATUS_STOP 32
 int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const bk_rollout_cfg* cfg,

@@ -2337,8 +2337,11 @@ __device__ __forceinline__ bool fs_copy_dev(bk_fset* d, int q, const bk_fset* s,
 template <bool FR>
 __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const Slab& slab, uint32_t slot) {
     if (a.rng_io) {  // the seats' streams go on in the next call
+        uint4 t[4];  // 16-byte copies, loads first
 #pragma unroll
-        for (int w = 0; w < 16; ++w) a.rng_io[(size_t)g.pid * 16 + w] = slab.word(SLAB_RNG_BASE + w);
+        for (int q = 0; q < 4; ++q) t[q] = reinterpret_cast<const uint4*>(&slab.word(SLAB_RNG_BASE))[q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(a.rng_io + (size_t)g.pid * 16)[q] = t[q];
     }
     if (a.out_states != nullptr) {  // BK_SEM_ADVANCE, or an arena run that wants final states
         store_state(a, g, slab);
@@ -2468,8 +2471,13 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
     g.cap = a.cfg.max_plies - (int32_t)g.turns0;  // arena_runner max_turns over the whole game
     g.forced = a.forced ? a.forced[pid] : -1;
     if (a.rng_io) {  // seats' streams carried over from the previous call
+        {  // 16-byte copies, loads first (the two pointers may alias as far as the compiler knows)
+            uint4 t[4];
 #pragma unroll
-        for (int w = 0; w < 16; ++w) slab.word(SLAB_RNG_BASE + w) = a.rng_io[(size_t)pid * 16 + w];
+            for (int q = 0; q < 4; ++q) t[q] = reinterpret_cast<const uint4*>(a.rng_io + (size_t)pid * 16)[q];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) reinterpret_cast<uint4*>(&slab.word(SLAB_RNG_BASE))[q] = t[q];
+        }
     } else if (a.cfg.rng == BK_RNG_NUMPY_MT) {
         const int nstreams = a.cfg.seats_share_stream ? 1 : 4;
         for (int q = 0; q < nstreams; ++q) {
@@ -5019,6 +5027,8 @@ int bk_arena_advance(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, co
     if (cfg->semantics != BK_SEM_ARENA || cfg->order != BK_ORDER_FRONTIER || cfg->rng != BK_RNG_NUMPY_MT ||
         cfg->seats_share_stream)
         return set_err(h, BK_EINVAL, "bk_arena_advance: needs ARENA, FRONTIER order, NUMPY_MT per-seat streams%s", "");
+    if (mem == BK_MEM_DEVICE && ((uintptr_t)rng_state & 15))
+        return set_err(h, BK_EINVAL, "bk_arena_advance: rng_state must be 16-byte aligned%s", "");
     if (n == 0) return BK_OK;
     return launch_playouts(h, states, n, nullptr, n, cfg, nullptr, out, states, mem, sets, sets, seat_masks,
                            rng_state);
@@ -5034,6 +5044,8 @@ int bk_arena_step(bk_handle h, bk_state* states, bk_fset* sets, int32_t n, const
         return set_err(h, BK_EINVAL, "bk_arena_step: needs ARENA, FRONTIER order, NUMPY_MT per-seat streams%s", "");
     if (quick_masks && !stop_out)
         return set_err(h, BK_EINVAL, "bk_arena_step: quick_masks goes with stop_out%s", "");
+    if (mem == BK_MEM_DEVICE && ((uintptr_t)rng_state & 15))
+        return set_err(h, BK_EINVAL, "bk_arena_step: rng_state must be 16-byte aligned%s", "");
     if (mem == BK_MEM_HOST && forced)
         for (int32_t i = 0; i < n; ++i)
             if (forced[i] < BK_FORCE_SKIP || (forced[i] >= 0 && !(forced[i] & BK_FORCE_INDEX) && forced[i] >= BK_NUM_ORIENTS * 400))
