@@ -1236,9 +1236,19 @@ __global__ __launch_bounds__(WAVE) void k_movegen_m(MovegenArgs a) {
             if (sh > 64 - kBits) w[q + 1] |= (uint64_t)v >> (64 - sh);
         }
         if (live && a.out_mask) {
-            uint64_t* dst = a.out_mask + ((size_t)idx * BK_NUM_ORIENTS + g) * 7;
-#pragma unroll
-            for (int q = 0; q < 7; ++q) dst[q] = w[q];
+            // 16-byte-aligned stores (the width WRITE_SIZE counts exactly): the 56-byte
+            // piece starts at an even or odd word (637 and 7 are odd), so it is three
+            // 16-byte stores and one 8-byte store at the front or the back
+            const size_t o = ((size_t)idx * BK_NUM_ORIENTS + g) * 7;
+            uint64_t* dst = a.out_mask + o;
+            const bool odd = ((o + ((uintptr_t)a.out_mask >> 3)) & 1u) != 0;
+            uint64_t* d16 = odd ? dst + 1 : dst;
+            const uint64_t p0 = odd ? w[1] : w[0], p1 = odd ? w[2] : w[1], p2 = odd ? w[3] : w[2];
+            const uint64_t p3 = odd ? w[4] : w[3], p4 = odd ? w[5] : w[4], p5 = odd ? w[6] : w[5];
+            reinterpret_cast<uint4*>(d16)[0] = make_uint4((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32));
+            reinterpret_cast<uint4*>(d16)[1] = make_uint4((uint32_t)p2, (uint32_t)(p2 >> 32), (uint32_t)p3, (uint32_t)(p3 >> 32));
+            reinterpret_cast<uint4*>(d16)[2] = make_uint4((uint32_t)p4, (uint32_t)(p4 >> 32), (uint32_t)p5, (uint32_t)(p5 >> 32));
+            *(odd ? dst : dst + 6) = odd ? w[0] : w[6];
         }
     };
     if (set * WAVE < a.n) {  // a grid rounded up to a multiple of 8 sets has idle blocks

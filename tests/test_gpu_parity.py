@@ -213,11 +213,14 @@ def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups, pa
         assert np.array_equal(c1, c0) and np.array_equal(m1, m0), n
 
 
-def test_movegen_mask_staged_odd_word_output(gpu):
-    """k_movegen_ml with a device out_mask that starts 8 bytes past a 16-byte boundary
-    (the C-ABI allows 8-byte alignment): the 16-byte stores shift to that parity, the
-    masks equal the aligned call's and the words either side stay untouched."""
+@pytest.mark.parametrize("stage", ["1", "0"])
+def test_movegen_mask_staged_odd_word_output(gpu, monkeypatch, stage):
+    """k_movegen_ml (staged) and k_movegen_m (per-lane pieces), with a device out_mask
+    that starts 8 bytes past a 16-byte boundary (the C-ABI allows 8-byte alignment): the
+    16-byte stores shift to that parity, the masks equal the aligned call's and the words
+    either side stay untouched."""
     import torch
+    monkeypatch.setenv("BK_MG_STAGE", stage)
     from reinforcementlearning_blokus_amd import _native as N
     n = 130
     boards = oracle_states(n, seed0=7300)
@@ -233,7 +236,7 @@ def test_movegen_mask_staged_odd_word_output(gpu):
     gpu._stream_from_torch()
     gpu.handle.movegen_mask(sd.data_ptr(), pd.data_ptr(), n, buf.data_ptr() + 8, cd.data_ptr(), N.MEM_DEVICE)
     torch.cuda.synchronize()
-    assert gpu.last_kernel().startswith("k_movegen_ml")
+    assert gpu.last_kernel().startswith("k_movegen_ml") == (stage == "1")
     b = buf.cpu().numpy()
     assert b[0] == -7 and b[-1] == -7
     assert np.array_equal(b[1:-1].view(np.uint64).reshape(n, N.N_ORIENTS, 7), ref)
