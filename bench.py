@@ -89,9 +89,10 @@ def parse(argv=None):
     ap.add_argument("--search-streams", type=int, default=None,
                     help="config4: MCTS searches in flight on this many streams while the other games play on "
                          "(BK_ARENA_MCTS_STREAMS; default: the driver's)")
-    ap.add_argument("--hw-queues", type=int, default=None,
-                    help="config4: HIP hardware queues of this rank (GPU_MAX_HW_QUEUES, <= 32), so the search "
-                         "streams and the main stream do not share in-order queues")
+    ap.add_argument("--hw-queues", type=int, default=16,
+                    help="config4: HIP hardware queues of this rank (GPU_MAX_HW_QUEUES, <= 32; default 16), so the "
+                         "search streams, the FastMCTS handle and the main stream do not share in-order queues "
+                         "(HIP's default is 4); 0 leaves the environment's setting")
     ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
                     help="config3 in-kernel move order: naive (default) or the reference's frontier order "
                          "(CPython set tables carried per game)")
@@ -614,7 +615,7 @@ def run_config4(args, world, rank, local, dist):
                    "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
                    "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
                    "rank0_phase_seconds": phases, "host_cores_per_rank": host,
-                   "search_streams": os.environ.get("BK_ARENA_MCTS_STREAMS", "default"),
+                   "search_streams": os.environ.get("BK_ARENA_MCTS_STREAMS", "8"),
                    "pipelined": os.environ.get("BK_ARENA_PIPELINE", "1") != "0",
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default"),
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
@@ -856,9 +857,9 @@ def main():
     if args.workload == "config4":  # before the HIP runtime starts (setup imports torch)
         if args.search_streams is not None:
             os.environ["BK_ARENA_MCTS_STREAMS"] = str(args.search_streams)
-        if args.hw_queues is not None:
+        if args.hw_queues:
             if not 1 <= args.hw_queues <= 32:
-                raise SystemExit("bench.py: --hw-queues must be in 1..32")
+                raise SystemExit("bench.py: --hw-queues must be in 0..32")
             os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     world, rank, local, dist = setup(args)
     run = {"config3": run_config3, "config5": run_config5, "config2": run_config2,
