@@ -134,6 +134,12 @@ int bk_destroy(bk_handle h);
    torch's default stream); BK_STREAM_OWN restores the handle's own stream. */
 #define BK_STREAM_OWN ((void*)~(uintptr_t)0)
 int bk_set_stream(bk_handle h, void* stream);
+/* A stream owned by the handle (destroyed by bk_destroy), usable with bk_set_stream or by
+   the caller: cu_mask[mask_words] (bit i = compute unit i may run its work; NULL / 0 words
+   = all units) via hipExtStreamCreateWithCUMask.  The config-4 driver keeps a few CUs
+   free of its long search kernels this way, so the short per-round kernels never queue
+   behind them. */
+int bk_stream_create(bk_handle h, const uint32_t* cu_mask, int32_t mask_words, void** out_stream);
 /* Wait for the handle's stream.  Device-path launches (BK_MEM_DEVICE) return before the
    kernel ends, so their input errors and guard trips surface here: BK_EOVERFLOW if a
    persistent kernel's iteration guard tripped (results incomplete), BK_EINVAL if a

@@ -29,7 +29,7 @@ STREAM_OWN = (1 << 64) - 1  # BK_STREAM_OWN
 
 # every symbol include/blokus_hip.h declares
 EXPORTS = (
-    "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream",
+    "bk_abi_version", "bk_tables_version", "bk_create", "bk_destroy", "bk_set_stream", "bk_stream_create",
     "bk_synchronize", "bk_last_error", "bk_orient_info", "bk_movegen", "bk_movegen_mask", "bk_has_moves",
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms", "bk_last_kernel",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
@@ -151,6 +151,7 @@ def load():
             "bk_create": (C.c_int, [C.c_int, C.c_uint32, P(vp)]),
             "bk_destroy": (C.c_int, [vp]),
             "bk_set_stream": (C.c_int, [vp, vp]),
+            "bk_stream_create": (C.c_int, [vp, vp, C.c_int32, C.POINTER(C.c_void_p)]),
             "bk_synchronize": (C.c_int, [vp]),
             "bk_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
             "bk_orient_info": (C.c_int, [C.c_int, P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
@@ -325,6 +326,18 @@ class Handle:
         """stream_ptr: a hipStream_t value (0 = null stream) or None for the handle's own."""
         v = STREAM_OWN if stream_ptr is None else stream_ptr
         self.check(self._L.bk_set_stream(self._h, C.c_void_p(v)), "bk_set_stream")
+
+    def stream_create(self, cu_mask=None) -> int:
+        """A new stream owned by this handle (bk_stream_create); cu_mask: uint32 words,
+        bit i = compute unit i allowed (None = all).  Returns the hipStream_t value."""
+        out = C.c_void_p()
+        if cu_mask is None:
+            rc = self._L.bk_stream_create(self._h, None, 0, C.byref(out))
+        else:
+            m = np.ascontiguousarray(cu_mask, dtype=np.uint32)
+            rc = self._L.bk_stream_create(self._h, m.ctypes.data, len(m), C.byref(out))
+        self.check(rc, "bk_stream_create")
+        return int(out.value)
 
     def synchronize(self):
         self.check(self._L.bk_synchronize(self._h), "bk_synchronize")

@@ -547,6 +547,15 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8"))) if pipeline else 1
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
     jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
+    reserve = int(os.environ.get("BK_ARENA_RESERVE_CUS", "0")) if pipeline else 0
+    if reserve > 0:  # search streams may not use `reserve` CUs, spread over the chip (bk_stream_create)
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        step = max(1, n_cu // reserve)
+        mask = np.zeros((n_cu + 31) // 32, np.uint32)
+        for cu in range(n_cu):
+            if cu % step != 0 or cu // step >= reserve:
+                mask[cu // 32] |= np.uint32(1 << (cu % 32))
+        jstreams = [torch.cuda.ExternalStream(e.handle.stream_create(mask), device=dev) for e in engines]
     free_slots = list(range(n_slots))
     jobs: List[Dict[str, Any]] = []
     fjobs: List[Dict[str, Any]] = []
@@ -589,12 +598,16 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         for t in (gi_d, aid_d, roots_d, sets_g, rh_d, players, zi_d, mt_g) + (tt if use_tt else ()):
             t.record_stream(js)
         inflight[games] = True
-        jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done})
+        jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done,
+                     "t0": time.perf_counter()})
         if not pipeline:
             mcts_finish(jobs.pop(0))
 
     def mcts_finish(job):
         job["done"].synchronize()
+        tl["mcts_jobs"] += 1
+        tl["mcts_job_s"] += time.perf_counter() - job["t0"]
+        tl["mcts_job_games"] += len(job["games"])
         eng = engines[job["slot"]]
         eng.synchronize()  # sticky launch errors
         games, aid = job["games"], job["aid"]
@@ -628,7 +641,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     def fast_launch(games, aid, nl, counts, quick, ce):
         mt = np.ascontiguousarray(mtf[aid])
         args = (nl.tolist(), counts, quick.tolist(), mt, _log_table(max(counts) + 1), ce)
-        job = {"games": games, "aid": aid, "counts": counts, "mt": mt}
+        job = {"games": games, "aid": aid, "counts": counts, "mt": mt, "t0": time.perf_counter()}
         if pipeline:
             job["fut"] = fast_pool.submit(fast_eng.fastmcts, *args)
             inflight[games] = True
@@ -639,6 +652,8 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
 
     def fast_finish(job):
         r = job["fut"].result() if "fut" in job else job["r"]
+        tl["fast_jobs"] += 1
+        tl["fast_job_s"] += time.perf_counter() - job["t0"]
         games, aid = job["games"], job["aid"]
         mtf[aid] = job["mt"]
         for i, a, it_run, bi, nch, it in zip(games.tolist(), aid.tolist(), r["iterations"].tolist(),
@@ -662,8 +677,12 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         return bool(done_m or done_f)
 
     stops_q = np.zeros(n, np.int64)  # the FastMCTS seats' quick_index (stop info)
+    # host-side timeline: jobs' launch -> completion seen, games inside a search per step
+    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "fast_jobs": 0, "fast_job_s": 0.0,
+          "search_games_per_step": 0}
     while active.any():
         prof["rounds"] += 1
+        tl["search_games_per_step"] += sum(len(j["games"]) for j in jobs)
         if progress is not None:
             progress(prof["rounds"], int(active.sum()), prof)
         ta = time.perf_counter()
@@ -752,6 +771,11 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         send = np.where(inflight, np.int32(N.FORCE_SKIP), forced)  # in-flight games: not touched
         forced_d.copy_(torch.from_numpy(send))
     assert not jobs and not fjobs and not inflight.any()
+    prof["timeline"] = {"mcts_jobs": tl["mcts_jobs"],
+                        "mcts_job_ms_mean": 1e3 * tl["mcts_job_s"] / max(1, tl["mcts_jobs"]),
+                        "mcts_games_per_job": tl["mcts_job_games"] / max(1, tl["mcts_jobs"]),
+                        "fast_jobs": tl["fast_jobs"], "fast_job_ms_mean": 1e3 * tl["fast_job_s"] / max(1, tl["fast_jobs"]),
+                        "games_in_search_per_step": tl["search_games_per_step"] / max(1, prof["rounds"])}
     if fast_pool is not None:
         fast_pool.shutdown()
     stream.synchronize()

@@ -4463,6 +4463,7 @@ __global__ void k_mcts_coop_h(MctsArgs a);
 struct bk_handle_s {
     int device = 0;
     hipStream_t own = nullptr, cur = nullptr;
+    std::vector<hipStream_t> extra;  // bk_stream_create's streams, destroyed with the handle
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool timed = false;
     char err[512] = {0};
@@ -4587,7 +4588,23 @@ int bk_destroy(bk_handle h) {
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
     if (h->own) (void)hipStreamDestroy(h->own);
+    for (hipStream_t x : h->extra) (void)hipStreamDestroy(x);
     delete h;
+    return BK_OK;
+}
+
+int bk_stream_create(bk_handle h, const uint32_t* cu_mask, int32_t mask_words, void** out_stream) {
+    if (!h || !out_stream || mask_words < 0 || (mask_words > 0 && !cu_mask))
+        return set_err(h, BK_EINVAL, "bk_stream_create: invalid arguments%s", "");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t st = nullptr;
+    if (mask_words > 0) {
+        HIPCHK(h, hipExtStreamCreateWithCUMask(&st, (uint32_t)mask_words, cu_mask));
+    } else {
+        HIPCHK(h, hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    }
+    h->extra.push_back(st);
+    *out_stream = (void*)st;
     return BK_OK;
 }
 

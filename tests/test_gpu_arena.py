@@ -173,7 +173,8 @@ def test_batched_arena_matches_bench_strength_reference_records(coop, monkeypatc
 
 
 @pytest.mark.parametrize("seed,policy,streams", [(99173, "randomized", "2"), (20260301, "round_robin", "2"),
-                                                 (99173, "randomized", "0"), (99173, "randomized", "3")])
+                                                 (99173, "randomized", "0"), (99173, "randomized", "3"),
+                                                 (99173, "randomized", "2r")])
 def test_device_driver_equals_host_staged_batches(monkeypatch, seed, policy, streams):
     """run_games_batched's device-resident driver (bk_arena_step: positions, tables and
     agent streams stay in HBM; search moves go back as forced moves, FastMCTS inputs come
@@ -191,7 +192,8 @@ def test_device_driver_equals_host_staged_batches(monkeypatch, seed, policy, str
         "num_games": 24, "seed": seed, "seat_policy": policy})
     monkeypatch.setenv("BK_ARENA_DEVICE", "1")
     monkeypatch.setenv("BK_ARENA_PIPELINE", "0" if streams == "0" else "1")
-    monkeypatch.setenv("BK_ARENA_MCTS_STREAMS", streams if streams != "0" else "1")
+    monkeypatch.setenv("BK_ARENA_MCTS_STREAMS", streams.rstrip("r") if streams != "0" else "1")
+    monkeypatch.setenv("BK_ARENA_RESERVE_CUS", "16" if streams.endswith("r") else "0")
     dev = run_games_batched(cfg, range(24))
     monkeypatch.setenv("BK_ARENA_DEVICE", "0")
     host = run_games_batched(cfg, range(24))
