@@ -480,7 +480,6 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     from ..agents.fast_mcts_agent import _log_table
     from ..gpu import BlokusGPU, empty_state, mcts_log_table, mcts_node_cap
     from ..mcts.mcts_agent import SEARCH_TOTALS
-    from ..mcts.zobrist import hash_states
     mcts, fast, seat_kind, seat_agent = agents_dev
     n = len(idx)
     cfgs = {a.name: a for a in run_config.agents}
@@ -566,12 +565,12 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     def mcts_launch(games, pls, aid, iters, roll, c, use_tt, policy):
         slot = free_slots.pop(0)
         eng, js = engines[slot], jstreams[slot]
-        gi_d, aid_d = up(games), up(aid)
+        ga_d = up(np.stack([games, aid]).astype(np.int64))  # one copy in; nothing comes back
+        gi_d, aid_d = ga_d[0], ga_d[1]
         roots_d = states_d.index_select(0, gi_d).contiguous()
         sets_g = sets_d.index_select(0, gi_d).contiguous()
-        roots_h = roots_d.cpu().numpy().view(N.STATE_DTYPE).reshape(len(games))
-        rh_d = up(hash_states(roots_h, zob_h[aid]).view(np.int64))
-        players = up(pls.astype(np.uint8))
+        players = roots_d[:, 241] & 3  # bk_state.current_player: the searching seat
+        rh_d = None  # ZobristHash.hash_board on the device (bk_mcts, k_root_hash)
         zi_d = aid_d.to(torch.int32)
         mt_g = mtm_d.index_select(0, aid_d).contiguous()
         if iters not in log_tables:
@@ -595,7 +594,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                 ttc_d.index_copy_(0, aid_d, tt[2])
             done = torch.cuda.Event()
             done.record(js)
-        for t in (gi_d, aid_d, roots_d, sets_g, rh_d, players, zi_d, mt_g) + (tt if use_tt else ()):
+        for t in (ga_d, roots_d, sets_g, players, zi_d, mt_g) + (tt if use_tt else ()):
             t.record_stream(js)
         inflight[games] = True
         jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done,
@@ -688,8 +687,11 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         ta = time.perf_counter()
         gpu.arena_step(states_d, sets_d, masks_d, rng_d, quick_d, forced_d, out_d, stop_d,
                        max_turns=run_config.max_turns)
-        res = out_d.cpu().numpy().view(N.RESULT_DTYPE).reshape(n)
-        stops = stop_d.cpu().numpy().view(N.STOP_DTYPE).reshape(n)
+        # one copy back per step: results, stop infos, the player to move
+        step_h = torch.cat([out_d, stop_d, states_d[:, 240:244]], dim=1).cpu().numpy()
+        res = np.ascontiguousarray(step_h[:, :32]).view(N.RESULT_DTYPE).reshape(n)
+        stops = np.ascontiguousarray(step_h[:, 32:32 + N.STOP_DTYPE.itemsize]).view(N.STOP_DTYPE).reshape(n)
+        to_move = step_h[:, 32 + N.STOP_DTYPE.itemsize + 1].astype(np.int64) & 3  # bk_state byte 241
         prof["advance_s"] += time.perf_counter() - ta
         status = res["status"].astype(np.int64)
         forced[:] = -1
@@ -717,8 +719,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             active[i] = False
         if len(stop):
             pl = (np.zeros(len(stop), np.int64))
-            cur = states_d.index_select(0, up(stop))[:, 241].cpu().numpy().astype(np.int64) & 3
-            pl[:] = cur
+            pl[:] = to_move[stop]
             kind = seat_kind[stop, pl]
             ag = seat_agent[stop, pl]
             nleg = stops["n_legal"][stop].astype(np.int64)

@@ -444,7 +444,8 @@ class BlokusGPU:
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
         Layouts as in mcts(): roots uint8[n,256], root_sets uint8[n,2080], players
-        uint8[n], root_hash/zobrist int64, zobrist_index int32[n], mt_state int32[n,625],
+        uint8[n], root_hash (None: computed on the device) / zobrist int64, zobrist_index
+        int32[n], mt_state int32[n,625],
         log_table float64, nodes uint8[n, node_cap*24], out uint8[n,32], tt_keys int64 /
         tt_vals float64 [n, tt_cap] (NaN = empty) + tt_count int32[n] (all or none),
         rewards float64 / hit_flags uint8 [n, iterations] (optional).  chunk > 0 splits
@@ -460,10 +461,12 @@ class BlokusGPU:
         use_tt = tt_keys is not None
         node_cap = nodes.shape[1] // N.MCTS_NODE_DTYPE.itemsize
         tensors = dict(roots=(roots, torch.uint8, (n, 256)), root_sets=(root_sets, torch.uint8, (n, N.FSET_DTYPE.itemsize)),
-                       players=(players, torch.uint8, (n,)), root_hash=(root_hash, torch.int64, (n,)),
+                       players=(players, torch.uint8, (n,)),
                        zobrist_index=(zobrist_index, torch.int32, (n,)), mt_state=(mt_state, torch.int32, (n, 625)),
                        nodes=(nodes, torch.uint8, (n, node_cap * N.MCTS_NODE_DTYPE.itemsize)),
                        out=(out, torch.uint8, (n, N.MCTS_OUT_DTYPE.itemsize)))
+        if root_hash is not None:  # None: ZobristHash.hash_board computed on the device (k_root_hash)
+            tensors.update(root_hash=(root_hash, torch.int64, (n,)))
         if use_tt:
             cap = tt_keys.shape[1]
             tensors.update(tt_keys=(tt_keys, torch.int64, (n, cap)), tt_vals=(tt_vals, torch.float64, (n, cap)),
