@@ -373,7 +373,8 @@ int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, con
  * key[624] then pos; in/out), TT hits reusing the cached reward.
  *
  * Inputs per game: roots[g] / root_sets[g] (the position), players[g] (the searching
- * player, MCTSNode.player), root_hash[g] (ZobristHash.hash_board of the position),
+ * player, MCTSNode.player), root_hash[g] (ZobristHash.hash_board of the position; NULL:
+ * computed on the device from roots and the game's key table),
  * zobrist_index[g] (which 2088-entry key table of `zobrist` the agent uses: 20*20*5 cell
  * keys, 4 turn keys, 4*21 piece keys, mcts/zobrist.py:41-68).
  * TT per game: tt_keys/tt_vals[g * cfg.tt_cap ...] open addressing (linear probing,

@@ -480,7 +480,6 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     from ..agents.fast_mcts_agent import _log_table
     from ..gpu import BlokusGPU, empty_state, mcts_log_table, mcts_node_cap
     from ..mcts.mcts_agent import SEARCH_TOTALS
-    from ..mcts.zobrist import hash_states
     mcts, fast, seat_kind, seat_agent = agents_dev
     n = len(idx)
     cfgs = {a.name: a for a in run_config.agents}
@@ -527,6 +526,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         last_iters = np.zeros(am, np.int64)
         log_tables = {}
     mtf = np.stack([a["mt"] for a in fast]) if fast else np.zeros((0, 625), np.uint32)
+    fast_tabs: Dict[int, Tuple[Any, Any, Any]] = {}  # iterations -> device log table, pow-fix rows
     per_agent = [{nm: {"moves": 0.0, "total_time_ms": 0.0, "total_simulations": 0.0, "moves_with_simulations": 0.0,
                        "move_times_ms": []} for nm in set(seats[i].values())} for i in range(n)]
     tot = np.zeros((n, 2), np.int64)  # turn_count, passes so far
@@ -538,11 +538,11 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     stream = torch.cuda.current_stream(dev)
     # MCTS searches run on their own streams and handles (BK_ARENA_MCTS_STREAMS, default
     # 8) and are not waited for: a game whose search is in flight sits at its stop seat
-    # (forced -1, arena_step leaves it there) while the other games play on and launch
-    # their own searches; its move is placed in the first round after the search ends.
-    # FastMCTS launches (host-staged bk_fastmcts) run the same way on a worker thread with
-    # its own handle.  BK_ARENA_PIPELINE=0: one search at a time on the main stream,
-    # waited for at once.
+    # (BK_FORCE_SKIP: arena_step does not touch it) while the other games play on and
+    # launch their own searches; its move is placed in the first step after the search
+    # ends.  FastMCTS seats are decided on the device in the step that stops at them
+    # (fast_on_device), so the next step places their move.  BK_ARENA_PIPELINE=0: one
+    # search at a time on the main stream, waited for at once, FastMCTS host-staged.
     pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
     n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8"))) if pipeline else 1
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
@@ -558,20 +558,18 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         jstreams = [torch.cuda.ExternalStream(e.handle.stream_create(mask), device=dev) for e in engines]
     free_slots = list(range(n_slots))
     jobs: List[Dict[str, Any]] = []
-    fjobs: List[Dict[str, Any]] = []
     fast_eng = BlokusGPU(device) if pipeline else gpu
-    fast_pool = ThreadPoolExecutor(1) if pipeline else None
     inflight = np.zeros(n, bool)
 
     def mcts_launch(games, pls, aid, iters, roll, c, use_tt, policy):
         slot = free_slots.pop(0)
         eng, js = engines[slot], jstreams[slot]
-        gi_d, aid_d = up(games), up(aid)
+        ga_d = up(np.stack([games, aid]).astype(np.int64))  # one copy in; nothing comes back
+        gi_d, aid_d = ga_d[0], ga_d[1]
         roots_d = states_d.index_select(0, gi_d).contiguous()
         sets_g = sets_d.index_select(0, gi_d).contiguous()
-        roots_h = roots_d.cpu().numpy().view(N.STATE_DTYPE).reshape(len(games))
-        rh_d = up(hash_states(roots_h, zob_h[aid]).view(np.int64))
-        players = up(pls.astype(np.uint8))
+        players = roots_d[:, 241] & 3  # bk_state.current_player: the searching seat
+        rh_d = None  # ZobristHash.hash_board on the device (bk_mcts, k_root_hash)
         zi_d = aid_d.to(torch.int32)
         mt_g = mtm_d.index_select(0, aid_d).contiguous()
         if iters not in log_tables:
@@ -595,7 +593,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                 ttc_d.index_copy_(0, aid_d, tt[2])
             done = torch.cuda.Event()
             done.record(js)
-        for t in (gi_d, aid_d, roots_d, sets_g, rh_d, players, zi_d, mt_g) + (tt if use_tt else ()):
+        for t in (ga_d, roots_d, sets_g, players, zi_d, mt_g) + (tt if use_tt else ()):
             t.record_stream(js)
         inflight[games] = True
         jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done,
@@ -638,48 +636,65 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             ttc_d[up(full)] = 0
         inflight[games] = False
         free_slots.append(job["slot"])
-    def fast_launch(games, aid, nl, counts, quick, ce):
-        mt = np.ascontiguousarray(mtf[aid])
-        args = (nl.tolist(), counts, quick.tolist(), mt, _log_table(max(counts) + 1), ce)
-        job = {"games": games, "aid": aid, "counts": counts, "mt": mt, "t0": time.perf_counter()}
-        if pipeline:
-            job["fut"] = fast_pool.submit(fast_eng.fastmcts, *args)
-            inflight[games] = True
-            fjobs.append(job)
-        else:
-            job["r"] = gpu.fastmcts(*args)
-            fast_finish(job)
+    mtf_d = up(mtf.view(np.int32)) if (pipeline and len(fast)) else None
+    fast_dev: List[Tuple[Any, Any]] = []  # this step's (games, forced values) computed on the device
 
-    def fast_finish(job):
-        r = job["fut"].result() if "fut" in job else job["r"]
-        tl["fast_jobs"] += 1
-        tl["fast_job_s"] += time.perf_counter() - job["t0"]
-        games, aid = job["games"], job["aid"]
-        mtf[aid] = job["mt"]
+    def fast_on_device(games, aid, nl, counts, ce):
+        """FastMCTSAgent.think for these stopped games on the main stream, inputs from the
+        step's stop infos on the device; the chosen list index becomes the game's forced
+        move on the device (FastMCTSAgent: quick move below 5 iterations, else the best
+        child, else index 0), so the next step places it with no host round trip."""
+        k = len(games)
+        need = max(counts) + 1
+        if need not in fast_tabs:
+            lt = _log_table(need)
+            fo, fe = N.pow_half_fix(lt, rows=need)
+            fast_tabs[need] = (up(lt), up(fo), up(fe if len(fe) else np.zeros(1, np.int32)))
+        lt_d, fo_d, fe_d = fast_tabs[need]
+        off = np.zeros(k + 1, np.int32)
+        np.cumsum(nl.astype(np.int32), out=off[1:])
+        meta = up(np.concatenate([off, np.asarray(counts, np.int32), games.astype(np.int32),
+                                  aid.astype(np.int32)]))
+        off_d, it_d = meta[:k + 1], meta[k + 1:2 * k + 1]
+        g_d, a_d = meta[2 * k + 1:3 * k + 1].long(), meta[3 * k + 1:].long()
+        st = stop_d.index_select(0, g_d)  # bk_stop_info rows: n_legal, quick_index, quick_reward
+        base = st[:, 8:16].contiguous().view(torch.float64).reshape(k)
+        quick_i = st[:, 4:8].contiguous().view(torch.int32).reshape(k)
+        mt_g = mtf_d.index_select(0, a_d).contiguous()
+        o = torch.empty((k, N.FASTMCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        fast_eng.fastmcts_device(off_d, it_d, base, mt_g, lt_d, fo_d, fe_d, ce, o)
+        mtf_d.index_copy_(0, a_d, mt_g)
+        w = o[:, :12].contiguous().view(torch.int32)  # best_index, iterations, n_children
+        j = torch.where(w[:, 1] < 5, quick_i, torch.where(w[:, 2] > 0, w[:, 0], torch.zeros_like(w[:, 0])))
+        fast_dev.append((g_d, (j | N.FORCE_INDEX).to(torch.int32)))
+        for i, a, it in zip(games.tolist(), aid.tolist(), counts):
+            forced[i] = N.FORCE_INDEX  # placeholder: the device value replaces it
+            e = per_agent[i][fast[a]["name"]]
+            e["total_simulations"] += it
+            e["moves_with_simulations"] += 1
+
+    def fast_launch(games, aid, nl, counts, quick, ce):  # BK_ARENA_PIPELINE=0: host-staged, waited for
+        mt = np.ascontiguousarray(mtf[aid])
+        r = gpu.fastmcts(nl.tolist(), counts, quick.tolist(), mt, _log_table(max(counts) + 1), ce)
+        mtf[aid] = mt
         for i, a, it_run, bi, nch, it in zip(games.tolist(), aid.tolist(), r["iterations"].tolist(),
-                                              r["best_index"].tolist(), r["n_children"].tolist(), job["counts"]):
+                                              r["best_index"].tolist(), r["n_children"].tolist(), counts):
             j = int(stops_q[i]) if it_run < 5 else (int(bi) if nch > 0 else 0)
             forced[i] = N.FORCE_INDEX | j
             e = per_agent[i][fast[a]["name"]]
             e["total_simulations"] += it
             e["moves_with_simulations"] += 1
-        inflight[games] = False
 
     def drain():
         done_m = [j for j in jobs if j["done"].query()]
         for j in done_m:
             jobs.remove(j)
             mcts_finish(j)
-        done_f = [j for j in fjobs if j["fut"].done()]
-        for j in done_f:
-            fjobs.remove(j)
-            fast_finish(j)
-        return bool(done_m or done_f)
+        return bool(done_m)
 
     stops_q = np.zeros(n, np.int64)  # the FastMCTS seats' quick_index (stop info)
     # host-side timeline: jobs' launch -> completion seen, games inside a search per step
-    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "fast_jobs": 0, "fast_job_s": 0.0,
-          "search_games_per_step": 0}
+    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "search_games_per_step": 0}
     while active.any():
         prof["rounds"] += 1
         tl["search_games_per_step"] += sum(len(j["games"]) for j in jobs)
@@ -688,8 +703,11 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         ta = time.perf_counter()
         gpu.arena_step(states_d, sets_d, masks_d, rng_d, quick_d, forced_d, out_d, stop_d,
                        max_turns=run_config.max_turns)
-        res = out_d.cpu().numpy().view(N.RESULT_DTYPE).reshape(n)
-        stops = stop_d.cpu().numpy().view(N.STOP_DTYPE).reshape(n)
+        # one copy back per step: results, stop infos, the player to move
+        step_h = torch.cat([out_d, stop_d, states_d[:, 240:244]], dim=1).cpu().numpy()
+        res = np.ascontiguousarray(step_h[:, :32]).view(N.RESULT_DTYPE).reshape(n)
+        stops = np.ascontiguousarray(step_h[:, 32:32 + N.STOP_DTYPE.itemsize]).view(N.STOP_DTYPE).reshape(n)
+        to_move = step_h[:, 32 + N.STOP_DTYPE.itemsize + 1].astype(np.int64) & 3  # bk_state byte 241
         prof["advance_s"] += time.perf_counter() - ta
         status = res["status"].astype(np.int64)
         forced[:] = -1
@@ -717,8 +735,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             active[i] = False
         if len(stop):
             pl = (np.zeros(len(stop), np.int64))
-            cur = states_d.index_select(0, up(stop))[:, 241].cpu().numpy().astype(np.int64) & 3
-            pl[:] = cur
+            pl[:] = to_move[stop]
             kind = seat_kind[stop, pl]
             ag = seat_agent[stop, pl]
             nleg = stops["n_legal"][stop].astype(np.int64)
@@ -758,26 +775,29 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                     ks = np.array(ks)
                     games = stop[ks]
                     aid = ag[ks]
-                    stops_q[games] = stops["quick_index"][games]
-                    fast_launch(games, aid, nleg[ks], [fast[int(a)]["iters"] for a in aid],
-                                stops["quick_reward"][games], ce)
+                    counts = [fast[int(a)]["iters"] for a in aid]
+                    if pipeline:
+                        fast_on_device(games, aid, nleg[ks], counts, ce)
+                    else:
+                        stops_q[games] = stops["quick_index"][games]
+                        fast_launch(games, aid, nleg[ks], counts, stops["quick_reward"][games], ce)
                 prof["fast_s"] += time.perf_counter() - tf
         tm = time.perf_counter()
         drain()
-        while (jobs or fjobs) and not (forced >= 0).any():  # nothing to place: wait for a search
+        while jobs and not (forced >= 0).any():  # nothing to place: wait for a search
             if not drain():
                 time.sleep(50e-6)
         prof["wait_s"] += time.perf_counter() - tm
         send = np.where(inflight, np.int32(N.FORCE_SKIP), forced)  # in-flight games: not touched
         forced_d.copy_(torch.from_numpy(send))
-    assert not jobs and not fjobs and not inflight.any()
+        for g_d, v_d in fast_dev:  # FastMCTS choices made on the device this step
+            forced_d.index_copy_(0, g_d, v_d)
+        fast_dev.clear()
+    assert not jobs and not inflight.any()
     prof["timeline"] = {"mcts_jobs": tl["mcts_jobs"],
                         "mcts_job_ms_mean": 1e3 * tl["mcts_job_s"] / max(1, tl["mcts_jobs"]),
                         "mcts_games_per_job": tl["mcts_job_games"] / max(1, tl["mcts_jobs"]),
-                        "fast_jobs": tl["fast_jobs"], "fast_job_ms_mean": 1e3 * tl["fast_job_s"] / max(1, tl["fast_jobs"]),
                         "games_in_search_per_step": tl["search_games_per_step"] / max(1, prof["rounds"])}
-    if fast_pool is not None:
-        fast_pool.shutdown()
     stream.synchronize()
     dt = time.perf_counter() - t0
     prof["total_s"] = dt

@@ -3821,8 +3821,38 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
 
 #if BK_DEF(BK_U_MCTS)
 __global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts(MctsArgs a) { mcts_body<false>(a); }
+// ZobristHash.hash_board (mcts/zobrist.py:70-99) of each root, one lane per root: the
+// cell keys (cell * 5 + occupant, 0 = empty), the side to move, the used pieces -- what
+// mcts/zobrist.py hash_states computes on the host (bk_mcts with root_hash NULL)
+__global__ __launch_bounds__(BLOCK) void k_root_hash(const bk_state* roots, const uint64_t* zob,
+                                                     const int32_t* zidx, uint64_t* out, int32_t n) {
+    const int32_t g = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (g >= n) return;
+    const bk_state* s = roots + g;
+    const uint64_t* Z = zob + (size_t)zidx[g] * MC_ZOB;
+    uint64_t h = 0;
+#pragma unroll 1
+    for (int w = 0; w < 7; ++w) {
+        const uint64_t p0 = s->planes[0][w], p1 = s->planes[1][w], p2 = s->planes[2][w], p3 = s->planes[3][w];
+        const int nb = w < 6 ? 64 : BK_CELLS - 6 * 64;
+#pragma unroll 1
+        for (int b = 0; b < nb; ++b) {
+            const int o = ((p0 >> b) & 1u) ? 1 : ((p1 >> b) & 1u) ? 2 : ((p2 >> b) & 1u) ? 3 : ((p3 >> b) & 1u) ? 4 : 0;
+            h ^= Z[(w * 64 + b) * 5 + o];
+        }
+    }
+    h ^= Z[2000 + (s->current_player & 3)];
+#pragma unroll 1
+    for (int p = 0; p < 4; ++p)
+#pragma unroll 1
+        for (int i = 0; i < BK_PIECES; ++i)
+            if ((s->used[p] >> i) & 1u) h ^= Z[2004 + p * BK_PIECES + i];
+    out[g] = h;
+}
 #else
 __global__ void k_mcts(MctsArgs a);
+__global__ void k_root_hash(const bk_state* roots, const uint64_t* zob, const int32_t* zidx, uint64_t* out,
+                            int32_t n);
 #endif
 #if BK_DEF(BK_U_MCTS_PAIR)
 __global__ __launch_bounds__(BLOCK, MCTS_BLOCKS_PER_CU) void k_mcts_pair(MctsArgs a) { mcts_body<false, true>(a); }
@@ -4478,6 +4508,7 @@ struct bk_handle_s {
     void* d_fslab = nullptr; size_t d_fslab_cap = 0; // frontier: per-slot records
     void* d_mc = nullptr; size_t d_mc_cap = 0;       // bk_mcts: staged inputs/outputs
     void* d_mclane = nullptr; size_t d_mclane_cap = 0; // bk_mcts: per-slot records
+    void* d_rh = nullptr; size_t d_rh_cap = 0;       // bk_mcts: root hashes computed on the device
     void* d_step = nullptr; size_t d_step_cap = 0;   // bk_arena_step: staged extras
     uint32_t* d_counter = nullptr;
     int num_cu = 0;
@@ -4583,7 +4614,7 @@ int bk_destroy(bk_handle h) {
     (void)hipSetDevice(h->device);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_mc, h->d_mclane, h->d_step, h->d_counter};
+                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -5332,7 +5363,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     if (!h || !cfg || n_games < 0 || (mem != BK_MEM_HOST && mem != BK_MEM_DEVICE))
         return set_err(h, BK_EINVAL, "bk_mcts: invalid arguments%s", "");
     if (n_games == 0) return BK_OK;
-    if (!roots || !root_sets || !players || !root_hash || !zobrist || n_zobrist < 1 || !zobrist_index ||
+    if (!roots || !root_sets || !players || !zobrist || n_zobrist < 1 || !zobrist_index ||
         !mt_state || !log_table || log_len < 1 || !out || (rewards == nullptr) != (hit_flags == nullptr))
         return set_err(h, BK_EINVAL, "bk_mcts: missing buffer%s", "");
     if (cfg->iterations < 0 || cfg->max_rollout_moves <= 0 || cfg->node_cap < 1 || cfg->time_limit_us < 0 ||
@@ -5394,6 +5425,15 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         if ((sec[i].dir & 1) && sec[i].host)
             HIPCHK(h, hipMemcpyAsync(p, sec[i].host, sec[i].bytes, hipMemcpyHostToDevice, h->cur));
         p += al(sec[i].bytes);
+    }
+    if (!root_hash) {  // ZobristHash.hash_board of every root, on the device
+        rc = grow(h, &h->d_rh, &h->d_rh_cap, sizeof(uint64_t) * n);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_root_hash, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, h->cur,
+                           (const bk_state*)sec[0].dev, (const uint64_t*)sec[4].dev, (const int32_t*)sec[5].dev,
+                           (uint64_t*)h->d_rh, n_games);
+        HIPCHK(h, hipGetLastError());
+        sec[3].dev = h->d_rh;
     }
     // persistent grid: every resident slot pulls whole searches from the counter
     const bool heur = cfg->rollout_policy == BK_MCTS_ROLLOUT_HEURISTIC;

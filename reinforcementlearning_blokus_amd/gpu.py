@@ -354,6 +354,31 @@ class BlokusGPU:
                              exploration, out.ctypes.data, vis.ctypes.data if vis is not None else 0, N.MEM_HOST)
         return (out, vis[: int(off[-1])]) if want_visits else out
 
+    def fastmcts_device(self, legal_offset, iterations, base, mt_state, log_table, pow_fix_offsets, pow_fix_entries,
+                        exploration: float, out):
+        """bk_fastmcts on torch CUDA tensors (BK_MEM_DEVICE, torch's current stream, not
+        waited for): legal_offset int32[n+1] (0, cumulative legal counts), iterations
+        int32[n], base float64[n], mt_state int32[n,625] (advanced in place), log_table
+        float64, pow-fix offsets / entries int32 (N.pow_half_fix of the same log_table),
+        out uint8[n, FASTMCTS_OUT_DTYPE.itemsize].  The caller validates the counts
+        (iterations < len(log_table)); the config-4 driver's FastMCTS seats."""
+        import torch
+        n = iterations.shape[0]
+        for t, name, dt, shape in ((legal_offset, "legal_offset", torch.int32, (n + 1,)),
+                                   (iterations, "iterations", torch.int32, (n,)), (base, "base", torch.float64, (n,)),
+                                   (mt_state, "mt_state", torch.int32, (n, 625)),
+                                   (out, "out", torch.uint8, (n, N.FASTMCTS_OUT_DTYPE.itemsize))):
+            _check_device_tensor(t, name, dt, shape, self.device)
+        _check_device_tensor(log_table, "log_table", torch.float64, (log_table.shape[0],), self.device)
+        rows = pow_fix_offsets.shape[0] - 1
+        if n == 0:
+            return
+        self._stream_from_torch()
+        self.handle.fastmcts(n, legal_offset.data_ptr(), iterations.data_ptr(), base.data_ptr(), mt_state.data_ptr(),
+                             log_table.data_ptr(), log_table.shape[0], pow_fix_offsets.data_ptr(),
+                             pow_fix_entries.data_ptr() if pow_fix_entries.numel() else 0, rows, exploration,
+                             out.data_ptr(), 0, N.MEM_DEVICE)
+
     def fastmcts_select(self, visits, totals, root_visits: int, log_table, exploration: float) -> int:
         """Diagnostic: k_fastmcts's UCB1 argmax (FastMCTSNode.select_child,
         fast_mcts_agent.py:45-56) over children with these visits / total rewards."""
@@ -444,7 +469,8 @@ class BlokusGPU:
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
         Layouts as in mcts(): roots uint8[n,256], root_sets uint8[n,2080], players
-        uint8[n], root_hash/zobrist int64, zobrist_index int32[n], mt_state int32[n,625],
+        uint8[n], root_hash (None: computed on the device) / zobrist int64, zobrist_index
+        int32[n], mt_state int32[n,625],
         log_table float64, nodes uint8[n, node_cap*24], out uint8[n,32], tt_keys int64 /
         tt_vals float64 [n, tt_cap] (NaN = empty) + tt_count int32[n] (all or none),
         rewards float64 / hit_flags uint8 [n, iterations] (optional).  chunk > 0 splits
@@ -460,10 +486,12 @@ class BlokusGPU:
         use_tt = tt_keys is not None
         node_cap = nodes.shape[1] // N.MCTS_NODE_DTYPE.itemsize
         tensors = dict(roots=(roots, torch.uint8, (n, 256)), root_sets=(root_sets, torch.uint8, (n, N.FSET_DTYPE.itemsize)),
-                       players=(players, torch.uint8, (n,)), root_hash=(root_hash, torch.int64, (n,)),
+                       players=(players, torch.uint8, (n,)),
                        zobrist_index=(zobrist_index, torch.int32, (n,)), mt_state=(mt_state, torch.int32, (n, 625)),
                        nodes=(nodes, torch.uint8, (n, node_cap * N.MCTS_NODE_DTYPE.itemsize)),
                        out=(out, torch.uint8, (n, N.MCTS_OUT_DTYPE.itemsize)))
+        if root_hash is not None:  # None: ZobristHash.hash_board computed on the device (k_root_hash)
+            tensors.update(root_hash=(root_hash, torch.int64, (n,)))
         if use_tt:
             cap = tt_keys.shape[1]
             tensors.update(tt_keys=(tt_keys, torch.int64, (n, cap)), tt_vals=(tt_vals, torch.float64, (n, cap)),

@@ -109,3 +109,27 @@ def test_coop_balanced_heuristic_pass_equals_per_lane_sums(gpu, monkeypatch, n, 
     assert np.array_equal(mta, mtb)
     assert np.array_equal(tta.keys, ttb.keys) and np.array_equal(tta.count, ttb.count)
     assert a["nodes"].tobytes() == b["nodes"].tobytes()
+
+
+@pytest.mark.parametrize("coop", ["1", "0"])
+def test_device_root_hash_equals_host_hash(monkeypatch, coop):
+    """bk_mcts with root_hash NULL hashes the roots on the device (k_root_hash,
+    ZobristHash.hash_board): the searches -- results, rewards, TT, RNG states -- equal the
+    ones given the host's hash_states values, per-agent key tables included."""
+    import torch
+
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch, frontier_roots
+    monkeypatch.setenv("BK_MCTS_COOP", coop)
+    gpu = BlokusGPU(0)
+    roots, sets = frontier_roots(gpu, 48, 18, seed=77)
+    outs = []
+    for host_hash in (True, False):
+        b = MctsBatch(gpu, roots, sets, iterations=24, seed0=5, n_tables=3, want_rewards=True)
+        if not host_hash:
+            b.root_hash = None
+        b.run()
+        torch.cuda.synchronize()
+        outs.append((b.results().copy(), b.mt.cpu().numpy(), b.tt_keys.cpu().numpy(), b.rewards.cpu().numpy()))
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y)
