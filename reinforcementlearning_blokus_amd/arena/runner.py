@@ -535,7 +535,14 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, wait_s=0.0, host_s=0.0,
                 rounds=0, uncertified_heuristic=0, device_driver=1)
     forced = np.full(n, -1, np.int32)
-    stream = torch.cuda.current_stream(dev)
+    caller = torch.cuda.current_stream(dev)
+    stream = caller
+    if os.environ.get("BK_ARENA_DEVICE_PRIORITY", "1") != "0":
+        # the per-step kernels (bk_arena_step, FastMCTS, gathers) on a high-priority stream:
+        # when a search block frees a CU they are dispatched before queued search blocks
+        stream = torch.cuda.Stream(dev, priority=-1)
+        stream.wait_stream(caller)
+        torch.cuda.set_stream(stream)
     # MCTS searches run on their own streams and handles (BK_ARENA_MCTS_STREAMS, default
     # 8) and are not waited for: a game whose search is in flight sits at its stop seat
     # (BK_FORCE_SKIP: arena_step does not touch it) while the other games play on and
@@ -695,110 +702,115 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     stops_q = np.zeros(n, np.int64)  # the FastMCTS seats' quick_index (stop info)
     # host-side timeline: jobs' launch -> completion seen, games inside a search per step
     tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "search_games_per_step": 0}
-    while active.any():
-        prof["rounds"] += 1
-        tl["search_games_per_step"] += sum(len(j["games"]) for j in jobs)
-        if progress is not None:
-            progress(prof["rounds"], int(active.sum()), prof)
-        ta = time.perf_counter()
-        gpu.arena_step(states_d, sets_d, masks_d, rng_d, quick_d, forced_d, out_d, stop_d,
-                       max_turns=run_config.max_turns)
-        # one copy back per step: results, stop infos, the player to move
-        step_h = torch.cat([out_d, stop_d, states_d[:, 240:244]], dim=1).cpu().numpy()
-        res = np.ascontiguousarray(step_h[:, :32]).view(N.RESULT_DTYPE).reshape(n)
-        stops = np.ascontiguousarray(step_h[:, 32:32 + N.STOP_DTYPE.itemsize]).view(N.STOP_DTYPE).reshape(n)
-        to_move = step_h[:, 32 + N.STOP_DTYPE.itemsize + 1].astype(np.int64) & 3  # bk_state byte 241
-        prof["advance_s"] += time.perf_counter() - ta
-        status = res["status"].astype(np.int64)
-        forced[:] = -1
-        act = np.flatnonzero(active & ~inflight)
-        tot[act, 0] += res["turns"][act]
-        tot[act, 1] += res["passes"][act]
-        prof["uncertified_heuristic"] += int(np.count_nonzero(status[act] & N.STATUS_UNCERT))
-        bad = status[act] & ~(N.STATUS_CAP | N.STATUS_STOP | N.STATUS_UNCERT)
-        if bad.any():
-            j = int(act[np.flatnonzero(bad)[0]])
-            raise RuntimeError(f"game {idx[j]}: kernel status {int(status[j])}")
-        stop = act[(status[act] & N.STATUS_STOP) != 0]
-        fin = act[(status[act] & N.STATUS_STOP) == 0]
-        for i in fin.tolist():
-            r = res[i].copy()
-            turns, passes, truncated = int(tot[i, 0]), int(tot[i, 1]), False
-            if status[i] & N.STATUS_CAP:  # cut by max_turns: over or not (arena_runner.py:702)
-                st_i = states_d[i:i + 1].cpu().numpy().view(N.STATE_DTYPE)
-                if int(gpu.has_moves(st_i)[0]) != 0:
-                    truncated = True
-                else:
-                    turns -= int(r["reserved"][0])
-                    passes -= int(r["reserved"][0])
-            results[i] = (r, turns, passes, truncated)
-            active[i] = False
-        if len(stop):
-            pl = (np.zeros(len(stop), np.int64))
-            pl[:] = to_move[stop]
-            kind = seat_kind[stop, pl]
-            ag = seat_agent[stop, pl]
-            nleg = stops["n_legal"][stop].astype(np.int64)
-            # ---- MCTS seats (select_action answers a single legal move without a search)
-            sel = np.flatnonzero(kind == 1)
-            if len(sel):
-                tm = time.perf_counter()
-                one = sel[nleg[sel] == 1]
-                for k in one.tolist():
-                    i, a = int(stop[k]), int(ag[k])
-                    forced[i] = N.FORCE_INDEX
-                    e = per_agent[i][mcts[a]["name"]]
-                    e["total_simulations"] += float(last_iters[a])  # the agent's stale iterations_run
-                    e["moves_with_simulations"] += 1
-                multi = sel[nleg[sel] > 1]
-                groups: Dict[Tuple, List[int]] = {}
-                for k in multi.tolist():
-                    a = mcts[int(ag[k])]
-                    groups.setdefault((a["iters"], a["roll"], a["c"], a["tt"], a["policy"]), []).append(k)
-                for key, ks in groups.items():
-                    ks = np.array(ks)
-                    if not free_slots:
-                        mcts_finish(jobs.pop(0))
-                    mcts_launch(stop[ks], pl[ks], ag[ks], *key)
-                prof["mcts_s"] += time.perf_counter() - tm
-            # ---- FastMCTS seats (think: a single legal move draws nothing)
-            sel = np.flatnonzero(kind == 2)
-            if len(sel):
-                tf = time.perf_counter()
-                for k in sel[nleg[sel] == 1].tolist():
-                    forced[int(stop[k])] = N.FORCE_INDEX
-                multi = sel[nleg[sel] > 1]
-                groups = {}
-                for k in multi.tolist():
-                    groups.setdefault(fast[int(ag[k])]["c"], []).append(k)
-                for ce, ks in groups.items():
-                    ks = np.array(ks)
-                    games = stop[ks]
-                    aid = ag[ks]
-                    counts = [fast[int(a)]["iters"] for a in aid]
-                    if pipeline:
-                        fast_on_device(games, aid, nleg[ks], counts, ce)
+    try:
+        while active.any():
+            prof["rounds"] += 1
+            tl["search_games_per_step"] += sum(len(j["games"]) for j in jobs)
+            if progress is not None:
+                progress(prof["rounds"], int(active.sum()), prof)
+            ta = time.perf_counter()
+            gpu.arena_step(states_d, sets_d, masks_d, rng_d, quick_d, forced_d, out_d, stop_d,
+                           max_turns=run_config.max_turns)
+            # one copy back per step: results, stop infos, the player to move
+            step_h = torch.cat([out_d, stop_d, states_d[:, 240:244]], dim=1).cpu().numpy()
+            res = np.ascontiguousarray(step_h[:, :32]).view(N.RESULT_DTYPE).reshape(n)
+            stops = np.ascontiguousarray(step_h[:, 32:32 + N.STOP_DTYPE.itemsize]).view(N.STOP_DTYPE).reshape(n)
+            to_move = step_h[:, 32 + N.STOP_DTYPE.itemsize + 1].astype(np.int64) & 3  # bk_state byte 241
+            prof["advance_s"] += time.perf_counter() - ta
+            status = res["status"].astype(np.int64)
+            forced[:] = -1
+            act = np.flatnonzero(active & ~inflight)
+            tot[act, 0] += res["turns"][act]
+            tot[act, 1] += res["passes"][act]
+            prof["uncertified_heuristic"] += int(np.count_nonzero(status[act] & N.STATUS_UNCERT))
+            bad = status[act] & ~(N.STATUS_CAP | N.STATUS_STOP | N.STATUS_UNCERT)
+            if bad.any():
+                j = int(act[np.flatnonzero(bad)[0]])
+                raise RuntimeError(f"game {idx[j]}: kernel status {int(status[j])}")
+            stop = act[(status[act] & N.STATUS_STOP) != 0]
+            fin = act[(status[act] & N.STATUS_STOP) == 0]
+            for i in fin.tolist():
+                r = res[i].copy()
+                turns, passes, truncated = int(tot[i, 0]), int(tot[i, 1]), False
+                if status[i] & N.STATUS_CAP:  # cut by max_turns: over or not (arena_runner.py:702)
+                    st_i = states_d[i:i + 1].cpu().numpy().view(N.STATE_DTYPE)
+                    if int(gpu.has_moves(st_i)[0]) != 0:
+                        truncated = True
                     else:
-                        stops_q[games] = stops["quick_index"][games]
-                        fast_launch(games, aid, nleg[ks], counts, stops["quick_reward"][games], ce)
-                prof["fast_s"] += time.perf_counter() - tf
-        tm = time.perf_counter()
-        drain()
-        while jobs and not (forced >= 0).any():  # nothing to place: wait for a search
-            if not drain():
-                time.sleep(50e-6)
-        prof["wait_s"] += time.perf_counter() - tm
-        send = np.where(inflight, np.int32(N.FORCE_SKIP), forced)  # in-flight games: not touched
-        forced_d.copy_(torch.from_numpy(send))
-        for g_d, v_d in fast_dev:  # FastMCTS choices made on the device this step
-            forced_d.index_copy_(0, g_d, v_d)
-        fast_dev.clear()
-    assert not jobs and not inflight.any()
-    prof["timeline"] = {"mcts_jobs": tl["mcts_jobs"],
-                        "mcts_job_ms_mean": 1e3 * tl["mcts_job_s"] / max(1, tl["mcts_jobs"]),
-                        "mcts_games_per_job": tl["mcts_job_games"] / max(1, tl["mcts_jobs"]),
-                        "games_in_search_per_step": tl["search_games_per_step"] / max(1, prof["rounds"])}
-    stream.synchronize()
+                        turns -= int(r["reserved"][0])
+                        passes -= int(r["reserved"][0])
+                results[i] = (r, turns, passes, truncated)
+                active[i] = False
+            if len(stop):
+                pl = (np.zeros(len(stop), np.int64))
+                pl[:] = to_move[stop]
+                kind = seat_kind[stop, pl]
+                ag = seat_agent[stop, pl]
+                nleg = stops["n_legal"][stop].astype(np.int64)
+                # ---- MCTS seats (select_action answers a single legal move without a search)
+                sel = np.flatnonzero(kind == 1)
+                if len(sel):
+                    tm = time.perf_counter()
+                    one = sel[nleg[sel] == 1]
+                    for k in one.tolist():
+                        i, a = int(stop[k]), int(ag[k])
+                        forced[i] = N.FORCE_INDEX
+                        e = per_agent[i][mcts[a]["name"]]
+                        e["total_simulations"] += float(last_iters[a])  # the agent's stale iterations_run
+                        e["moves_with_simulations"] += 1
+                    multi = sel[nleg[sel] > 1]
+                    groups: Dict[Tuple, List[int]] = {}
+                    for k in multi.tolist():
+                        a = mcts[int(ag[k])]
+                        groups.setdefault((a["iters"], a["roll"], a["c"], a["tt"], a["policy"]), []).append(k)
+                    for key, ks in groups.items():
+                        ks = np.array(ks)
+                        if not free_slots:
+                            mcts_finish(jobs.pop(0))
+                        mcts_launch(stop[ks], pl[ks], ag[ks], *key)
+                    prof["mcts_s"] += time.perf_counter() - tm
+                # ---- FastMCTS seats (think: a single legal move draws nothing)
+                sel = np.flatnonzero(kind == 2)
+                if len(sel):
+                    tf = time.perf_counter()
+                    for k in sel[nleg[sel] == 1].tolist():
+                        forced[int(stop[k])] = N.FORCE_INDEX
+                    multi = sel[nleg[sel] > 1]
+                    groups = {}
+                    for k in multi.tolist():
+                        groups.setdefault(fast[int(ag[k])]["c"], []).append(k)
+                    for ce, ks in groups.items():
+                        ks = np.array(ks)
+                        games = stop[ks]
+                        aid = ag[ks]
+                        counts = [fast[int(a)]["iters"] for a in aid]
+                        if pipeline:
+                            fast_on_device(games, aid, nleg[ks], counts, ce)
+                        else:
+                            stops_q[games] = stops["quick_index"][games]
+                            fast_launch(games, aid, nleg[ks], counts, stops["quick_reward"][games], ce)
+                    prof["fast_s"] += time.perf_counter() - tf
+            tm = time.perf_counter()
+            drain()
+            while jobs and not (forced >= 0).any():  # nothing to place: wait for a search
+                if not drain():
+                    time.sleep(50e-6)
+            prof["wait_s"] += time.perf_counter() - tm
+            send = np.where(inflight, np.int32(N.FORCE_SKIP), forced)  # in-flight games: not touched
+            forced_d.copy_(torch.from_numpy(send))
+            for g_d, v_d in fast_dev:  # FastMCTS choices made on the device this step
+                forced_d.index_copy_(0, g_d, v_d)
+            fast_dev.clear()
+        assert not jobs and not inflight.any()
+        prof["timeline"] = {"mcts_jobs": tl["mcts_jobs"],
+                            "mcts_job_ms_mean": 1e3 * tl["mcts_job_s"] / max(1, tl["mcts_jobs"]),
+                            "mcts_games_per_job": tl["mcts_job_games"] / max(1, tl["mcts_jobs"]),
+                            "games_in_search_per_step": tl["search_games_per_step"] / max(1, prof["rounds"])}
+        stream.synchronize()
+    finally:
+        if stream is not caller:
+            stream.synchronize()
+            torch.cuda.set_stream(caller)
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
     prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"] - prof["wait_s"]
