@@ -1380,10 +1380,12 @@ __device__ __forceinline__ void movegen_ml_body(const MovegenArgs& a) {
     }
 }
 __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml4(MovegenArgs a) { movegen_ml_body<4>(a); }
+__global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml5(MovegenArgs a) { movegen_ml_body<5>(a); }
 __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml7(MovegenArgs a) { movegen_ml_body<7>(a); }
 __global__ __launch_bounds__(MG_PART_WAVES_MAX * WAVE) void k_movegen_ml13(MovegenArgs a) { movegen_ml_body<13>(a); }
 #else
 __global__ void k_movegen_ml4(MovegenArgs a);
+__global__ void k_movegen_ml5(MovegenArgs a);
 __global__ void k_movegen_ml7(MovegenArgs a);
 __global__ void k_movegen_ml13(MovegenArgs a);
 #endif
@@ -4795,8 +4797,8 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     if (const char* env = getenv("BK_MG_STAGE")) staged = staged && atoi(env) != 0;  // A/B override
     if (staged) {
         int parts = 4;
-        if (const char* env = getenv("BK_MG_PARTS")) parts = atoi(env);  // tuning: 4, 7 or 13
-        if (parts != 7 && parts != 13) parts = 4;
+        if (const char* env = getenv("BK_MG_PARTS")) parts = atoi(env);  // tuning: 4, 5, 7 or 13
+        if (parts != 5 && parts != 7 && parts != 13) parts = 4;
         int wp = groups / parts;
         if (const char* env = getenv("BK_MG_PART_WAVES")) wp = atoi(env);  // tuning override
         wp = wp < 1 ? 1 : (wp > MG_PART_WAVES_MAX ? MG_PART_WAVES_MAX : wp);
@@ -4812,6 +4814,9 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
         if (parts == 4) {
             h->last_kernel = "k_movegen_ml4";
             hipLaunchKernelGGL(k_movegen_ml4, grid, blk, 0, h->cur, a);
+        } else if (parts == 5) {
+            h->last_kernel = "k_movegen_ml5";
+            hipLaunchKernelGGL(k_movegen_ml5, grid, blk, 0, h->cur, a);
         } else if (parts == 7) {
             h->last_kernel = "k_movegen_ml7";
             hipLaunchKernelGGL(k_movegen_ml7, grid, blk, 0, h->cur, a);

@@ -191,7 +191,7 @@ def test_movegen_mask_equals_rows_and_oracle(gpu, n):
     assert m0 is None and np.array_equal(c0, cnt)
 
 
-@pytest.mark.parametrize("parts", ["4", "7", "13"])
+@pytest.mark.parametrize("parts", ["4", "5", "7", "13"])
 @pytest.mark.parametrize("groups", ["4", "8", "32", "91"])
 def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups, parts):
     """k_movegen_ml4/7/13 (LDS-staged whole-line writes, 4, 7 or 13 orientation ranges of
