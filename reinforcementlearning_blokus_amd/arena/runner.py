@@ -552,6 +552,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     # search at a time on the main stream, waited for at once, FastMCTS host-staged.
     pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
     n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8"))) if pipeline else 1
+    job_games = max(1, int(os.environ.get("BK_ARENA_JOB_GAMES", "1000000"))) if pipeline else 1 << 30
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
     jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
     reserve = int(os.environ.get("BK_ARENA_RESERVE_CUS", "0")) if pipeline else 0
@@ -764,10 +765,13 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
                         a = mcts[int(ag[k])]
                         groups.setdefault((a["iters"], a["roll"], a["c"], a["tt"], a["policy"]), []).append(k)
                     for key, ks in groups.items():
-                        ks = np.array(ks)
-                        if not free_slots:
-                            mcts_finish(jobs.pop(0))
-                        mcts_launch(stop[ks], pl[ks], ag[ks], *key)
+                        # launches of at most job_games searches: a launch ends with its
+                        # slowest search, so smaller ones hand finished games back sooner
+                        for c0 in range(0, len(ks), job_games):
+                            kc = np.array(ks[c0:c0 + job_games])
+                            if not free_slots:
+                                mcts_finish(jobs.pop(0))
+                            mcts_launch(stop[kc], pl[kc], ag[kc], *key)
                     prof["mcts_s"] += time.perf_counter() - tm
                 # ---- FastMCTS seats (think: a single legal move draws nothing)
                 sel = np.flatnonzero(kind == 2)
