@@ -551,7 +551,10 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     # (fast_on_device), so the next step places their move.  BK_ARENA_PIPELINE=0: one
     # search at a time on the main stream, waited for at once, FastMCTS host-staged.
     pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
-    n_slots = max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8"))) if pipeline else 1
+    # at most 16: 24 search streams with 32 HIP queues returned searches with
+    # BK_MCTS_ELOG statuses in one measurement (profiles/r04/sweeps/r04n, not understood
+    # yet); 8..16 are validated and no slower
+    n_slots = min(16, max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8")))) if pipeline else 1
     job_games = max(1, int(os.environ.get("BK_ARENA_JOB_GAMES", "1000000"))) if pipeline else 1 << 30
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
     jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
