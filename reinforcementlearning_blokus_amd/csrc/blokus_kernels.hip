@@ -78,6 +78,11 @@
 #endif
 // ... and compacts each 16-slot batch to the slots that can add an anchor before the
 // row reads (A/B build: -DBK_LOCATE_COMPACT=1)
+// place_frontier loads a <= 64-slot stage alongside the table's mask (A/B build:
+// -DBK_STAGE_EAGER=1; the 32 VGPRs cost k_rollout_fr 96 B/lane of spills)
+#ifndef BK_STAGE_EAGER
+#define BK_STAGE_EAGER 0
+#endif
 #ifndef BK_LOCATE_COMPACT
 #define BK_LOCATE_COMPACT 0
 #endif
@@ -1810,14 +1815,23 @@ template <int STAGE, bool RECOPY = false>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
                                                const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
+    // BK_STAGE_EAGER: stages of <= 64 slots load all STAGE slots at once, alongside the
+    // mask (the storage holds BK_FSET_SLOTS >= STAGE): one memory latency instead of the
+    // mask's, then the table's
+    constexpr bool EAGER = BK_STAGE_EAGER && STAGE > 0 && STAGE <= 64;
+    const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
+    uint4 pre[EAGER ? STAGE / 8 : 1];
+    if constexpr (EAGER) {
+#pragma unroll
+        for (int i = 0; i < STAGE / 8; ++i) pre[i] = src4[i];
+    }
     const uint32_t gmask = gfs->mask[p];
     bk_u32_alias* lw = reinterpret_cast<bk_u32_alias*>(lk);
     if (STAGE > 0 && gmask < (uint32_t)STAGE) {
-        const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
         for (int i = 0; i < STAGE / 8; ++i) {
             if ((uint32_t)(8 * i) <= gmask) {
-                const uint4 v = src4[i];
+                const uint4 v = EAGER ? pre[EAGER ? i : 0] : src4[i];
                 lw[(4 * i + 0) * WAVE] = v.x;
                 lw[(4 * i + 1) * WAVE] = v.y;
                 lw[(4 * i + 2) * WAVE] = v.z;
