@@ -83,6 +83,9 @@
 #ifndef BK_STAGE_EAGER
 #define BK_STAGE_EAGER 0
 #endif
+#ifndef BK_STAGE_EAGER_MAX
+#define BK_STAGE_EAGER_MAX 64
+#endif
 #ifndef BK_LOCATE_COMPACT
 #define BK_LOCATE_COMPACT 0
 #endif
@@ -1818,7 +1821,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     // BK_STAGE_EAGER: stages of <= 64 slots load all STAGE slots at once, alongside the
     // mask (the storage holds BK_FSET_SLOTS >= STAGE): one memory latency instead of the
     // mask's, then the table's
-    constexpr bool EAGER = BK_STAGE_EAGER && STAGE > 0 && STAGE <= 64;
+    constexpr bool EAGER = BK_STAGE_EAGER && STAGE > 0 && STAGE <= BK_STAGE_EAGER_MAX;
     const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
     uint4 pre[EAGER ? STAGE / 8 : 1];
     if constexpr (EAGER) {
