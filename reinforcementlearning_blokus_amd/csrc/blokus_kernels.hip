@@ -76,6 +76,19 @@
 #ifndef BK_LOCATE_SKIP
 #define BK_LOCATE_SKIP 1
 #endif
+// ... and compacts each 16-slot batch to the slots that can add an anchor before the
+// row reads (A/B build: -DBK_LOCATE_COMPACT=1)
+// place_frontier loads a <= 64-slot stage alongside the table's mask (A/B build:
+// -DBK_STAGE_EAGER=1; the 32 VGPRs cost k_rollout_fr 96 B/lane of spills)
+#ifndef BK_STAGE_EAGER
+#define BK_STAGE_EAGER 0
+#endif
+#ifndef BK_STAGE_EAGER_MAX
+#define BK_STAGE_EAGER_MAX 64
+#endif
+#ifndef BK_LOCATE_COMPACT
+#define BK_LOCATE_COMPACT 0
+#endif
 #ifndef BK_ROWSKIP_BUILD
 #define BK_ROWSKIP_BUILD 0
 #endif
@@ -806,6 +819,26 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
         const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
         const uint4 na = k4[(nb0 >> 4) * RS], nb = k4[(nb0 >> 4) * RS + 1];
         const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#if BK_LOCATE_COMPACT
+        // the batch's slots that can add an anchor, then one divergent pass over just
+        // those: the wave runs the row reads max-over-lanes-of-relevant-slots times
+        uint32_t rel = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            const int fr = f >= 0 ? f / 20 : 0;
+            rel |= (f >= 0 && b0 + j <= mask && ((arows >> (fr + 5 - H)) & hmask)) ? (1u << j) : 0u;
+        }
+#pragma unroll 1
+        while (rel && hit_f < 0) {
+            const int j = __builtin_ctz(rel);
+            rel &= rel - 1u;
+            uint32_t wj = w[0];
+#pragma unroll
+            for (int q = 1; q < 8; ++q) wj = (j >> 1) == q ? w[q] : wj;
+            const int f = (int)(int16_t)((j & 1) ? (wj >> 16) : (wj & 0xFFFFu));
+            const int fr = f / 20, fc = f - 20 * fr;
+#else
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
@@ -814,6 +847,7 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
             // no anchor row among fr - H + 1 .. fr: this cell adds no anchors (skip the
             // row reads); anchors counted later only clear bits, so arows stays a superset
             if (BK_LOCATE_SKIP && !((arows >> (fr + 5 - H)) & hmask)) continue;
+#endif
             uint32_t hm[5], tot = 0;
 #pragma unroll
             for (int d = 0; d < 5; ++d) {
@@ -915,12 +949,31 @@ __device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2*
         const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
         const uint4 na = k4[(nb0 >> 4) * RS], nb = k4[(nb0 >> 4) * RS + 1];
         const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+#if BK_LOCATE_COMPACT
+        uint32_t rel = 0;  // as locate_move_frontier (the pair's lanes hold the same mask)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
+            const int fr = f >= 0 ? f / 20 : 0;
+            rel |= (f >= 0 && b0 + j <= mask && ((arows >> (fr + 5 - H)) & hmask)) ? (1u << j) : 0u;
+        }
+#pragma unroll 1
+        while (rel && hit_f < 0) {
+            const int j = __builtin_ctz(rel);
+            rel &= rel - 1u;
+            uint32_t wj = w[0];
+#pragma unroll
+            for (int q = 1; q < 8; ++q) wj = (j >> 1) == q ? w[q] : wj;
+            const int f = (int)(int16_t)((j & 1) ? (wj >> 16) : (wj & 0xFFFFu));
+            const int fr = f / 20, fc = f - 20 * fr;
+#else
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
             if (hit_f >= 0 || f < 0 || b0 + j > mask) continue;
             const int fr = f / 20, fc = f - 20 * fr;
             if (BK_LOCATE_SKIP && !((arows >> (fr + 5 - H)) & hmask)) continue;
+#endif
             uint32_t hm[3], tot = 0;
 #pragma unroll
             for (int t = 0; t < 3; ++t) {
@@ -1765,14 +1818,23 @@ template <int STAGE, bool RECOPY = false>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
                                                const int32_t (&cells)[5], uint64_t real) {
     bk_fset* gfs = &fl->s;
+    // BK_STAGE_EAGER: stages of <= 64 slots load all STAGE slots at once, alongside the
+    // mask (the storage holds BK_FSET_SLOTS >= STAGE): one memory latency instead of the
+    // mask's, then the table's
+    constexpr bool EAGER = BK_STAGE_EAGER && STAGE > 0 && STAGE <= BK_STAGE_EAGER_MAX;
+    const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
+    uint4 pre[EAGER ? STAGE / 8 : 1];
+    if constexpr (EAGER) {
+#pragma unroll
+        for (int i = 0; i < STAGE / 8; ++i) pre[i] = src4[i];
+    }
     const uint32_t gmask = gfs->mask[p];
     bk_u32_alias* lw = reinterpret_cast<bk_u32_alias*>(lk);
     if (STAGE > 0 && gmask < (uint32_t)STAGE) {
-        const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
 #pragma unroll
         for (int i = 0; i < STAGE / 8; ++i) {
             if ((uint32_t)(8 * i) <= gmask) {
-                const uint4 v = src4[i];
+                const uint4 v = EAGER ? pre[EAGER ? i : 0] : src4[i];
                 lw[(4 * i + 0) * WAVE] = v.x;
                 lw[(4 * i + 1) * WAVE] = v.y;
                 lw[(4 * i + 2) * WAVE] = v.z;
