@@ -68,27 +68,30 @@
 #define BK_TU 0
 #endif
 #define BK_DEF(u) (BK_TU == 0 || BK_TU == (u))
-// 1: the stencil skips anchor rows no lane of the wave can use (live_anchor_rows) --
-// measured no faster: the per-row branches cost the kernel spills (DESIGN.md 4);
-// 0: the round-3 stencil (every anchor row), a build for the A/B measurement
 // locate pass 2 skips frontier cells with no anchor row within the piece's height (A/B
 // build: -DBK_LOCATE_SKIP=0)
 #ifndef BK_LOCATE_SKIP
 #define BK_LOCATE_SKIP 1
 #endif
 // ... and compacts each 16-slot batch to the slots that can add an anchor before the
-// row reads (A/B build: -DBK_LOCATE_COMPACT=1)
-// place_frontier loads a <= 64-slot stage alongside the table's mask (A/B build:
-// -DBK_STAGE_EAGER=1; the 32 VGPRs cost k_rollout_fr 96 B/lane of spills)
+// row reads, so the wave runs them max-over-lanes-of-relevant-slots times instead of 16:
+// frontier-order config 3 25.8 -> 27.9 M playouts/s, config 5 16.2 -> 17.2 M sims/s
+// (profiles/r04/sweeps/r04p; -DBK_LOCATE_COMPACT=0 for the per-slot walk)
+#ifndef BK_LOCATE_COMPACT
+#define BK_LOCATE_COMPACT 1
+#endif
+// place_frontier loads a <= BK_STAGE_EAGER_MAX-slot stage alongside the table's mask
+// (A/B build: -DBK_STAGE_EAGER=1; the 32 VGPRs cost k_rollout_fr 96 B/lane of spills and
+// measured within noise, profiles/r04/sweeps/r04p)
 #ifndef BK_STAGE_EAGER
 #define BK_STAGE_EAGER 0
 #endif
 #ifndef BK_STAGE_EAGER_MAX
 #define BK_STAGE_EAGER_MAX 64
 #endif
-#ifndef BK_LOCATE_COMPACT
-#define BK_LOCATE_COMPACT 0
-#endif
+// 1: the stencil skips anchor rows no lane of the wave can use (live_anchor_rows) --
+// measured no faster: the per-row branches cost the kernel spills (DESIGN.md 4);
+// 0: the round-3 stencil (every anchor row), a build for the A/B measurement
 #ifndef BK_ROWSKIP_BUILD
 #define BK_ROWSKIP_BUILD 0
 #endif
