@@ -385,7 +385,7 @@ __device__ __forceinline__ LiveRows live_anchor_rows(const Planes& P) {
 #endif
 // frontier tables smaller than this many slots are staged in LDS for place_frontier
 // (0: probe the table in global memory).  k_rollout_fr: 64, so its area stays at the 40
-// dwords per lane the counts and rows need and 3 blocks of 256 lanes fit a CU's LDS (3
+// dwords per lane the counts and rows need and 4 blocks of 256 lanes fill a CU's LDS (4
 // waves/SIMD); the ~12 % of plies whose mover has a 128-slot table probe it in place.
 // k_mcts (config 5: 65,536 searches = one 256-lane block per CU, LDS to spare): 128.
 #ifndef BK_FS_STAGE_FR
@@ -398,9 +398,17 @@ __device__ __forceinline__ LiveRows live_anchor_rows(const Planes& P) {
 // the area also stages the mover's frontier table ([slot pair][lane])
 #define ROLL_WORDS_STAGE(S) (((S) / 2 > 40 ? (S) / 2 : 40) * WAVE)
 #define ROLL_WORDS_FR ROLL_WORDS_STAGE(BK_FS_STAGE_FR)
-// resident 256-lane blocks per CU of k_rollout_fr / k_mcts (the launch bound; <= 168 VGPRs at 3)
+// resident 256-lane blocks per CU of k_rollout_fr (the launch bound).  The kernel reads
+// the CPython cell hashes (3.2 KB) from global memory through the L1, so 4 blocks x 40 KB
+// of areas fill the CU's LDS: at 4 blocks/CU (128 VGPRs, 256 B/lane of scratch, spills
+// mostly on the cold paths) 31.8 M playouts/s vs 27.9 M at 3 blocks with the hashes in
+// LDS, 26.8 M at 3 blocks with them in global memory (profiles/r04/sweeps/r04r).
+// A/B: -DBK_FR_HTAB_LDS=1 -DFR_BLOCKS_PER_CU=3
+#ifndef BK_FR_HTAB_LDS
+#define BK_FR_HTAB_LDS 0
+#endif
 #ifndef FR_BLOCKS_PER_CU
-#define FR_BLOCKS_PER_CU 3
+#define FR_BLOCKS_PER_CU 4
 #endif
 #ifndef MCTS_BLOCKS_PER_CU
 #define MCTS_BLOCKS_PER_CU 2
@@ -2676,20 +2684,23 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     constexpr int BLK = HEUR ? HBLOCK : BLOCK;
     constexpr int AREA = HEUR ? HEUR_WORDS : FR ? ROLL_WORDS_FR : ROLL_WORDS_PER_WAVE;
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
-    // FR: + the CPython cell hashes (shared by the block) for the frontier tables;
-    // HEUR: + the policy's exp tables
-    __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + (FR ? 2 * BK_CELLS : 0) + HS_WORDS];
+    // FR: + the CPython cell hashes (shared by the block) for the frontier tables (or,
+    // BK_FR_HTAB_LDS=0, read from global memory through the L1: k_rollout_fr's LDS then
+    // fits 4 blocks per CU); HEUR: + the policy's exp tables
+    constexpr bool HT_LDS = FR && (HEUR || BK_FR_HTAB_LDS);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + (HT_LDS ? 2 * BK_CELLS : 0) + HS_WORDS];
     const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
     uint32_t* my = lds + wv * AREA;
     uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * AREA) + lane;  // + R * WAVE
-    uint64_t* htab = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
-    HeurShared* hs = reinterpret_cast<HeurShared*>(lds + AREA * (BLK / WAVE) + (FR ? 2 * BK_CELLS : 0));
+    uint64_t* htab_lds = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
+    const uint64_t* htab = HT_LDS ? htab_lds : kCellHash;
+    HeurShared* hs = reinterpret_cast<HeurShared*>(lds + AREA * (BLK / WAVE) + (HT_LDS ? 2 * BK_CELLS : 0));
     double* psum = reinterpret_cast<double*>(lds + wv * AREA + HEUR_PSUM * WAVE) + lane;  // + piece * WAVE
-    if constexpr (FR) {
-        for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab[i] = kCellHash[i];
+    if constexpr (HT_LDS) {
+        for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab_lds[i] = kCellHash[i];
     }
     if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
-    if constexpr (FR || HEUR) __syncthreads();
+    if constexpr (HT_LDS || HEUR) __syncthreads();
     const uint32_t slot = blockIdx.x * BLK + threadIdx.x;
     const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
