@@ -80,11 +80,12 @@
 #ifndef BK_LOCATE_COMPACT
 #define BK_LOCATE_COMPACT 1
 #endif
-// place_frontier loads a <= BK_STAGE_EAGER_MAX-slot stage alongside the table's mask
-// (A/B build: -DBK_STAGE_EAGER=1; the 32 VGPRs cost k_rollout_fr 96 B/lane of spills and
-// measured within noise, profiles/r04/sweeps/r04p)
+// place_frontier loads a <= BK_STAGE_EAGER_MAX-slot stage alongside the table's mask:
+// one memory latency instead of two.  Within noise for the 3-block k_rollout_fr
+// (profiles/r04/sweeps/r04p); +1.0 % for the 4-block one, 31.73 -> 32.03 M playouts/s
+// over three pairs of runs (profiles/r04/sweeps/r04v).  A/B: -DBK_STAGE_EAGER=0
 #ifndef BK_STAGE_EAGER
-#define BK_STAGE_EAGER 0
+#define BK_STAGE_EAGER 1
 #endif
 #ifndef BK_STAGE_EAGER_MAX
 #define BK_STAGE_EAGER_MAX 64
