@@ -84,6 +84,11 @@
 // one memory latency instead of two.  Within noise for the 3-block k_rollout_fr
 // (profiles/r04/sweeps/r04p); +1.0 % for the 4-block one, 31.73 -> 32.03 M playouts/s
 // over three pairs of runs (profiles/r04/sweeps/r04v).  A/B: -DBK_STAGE_EAGER=0
+// fs_run_ops loads the next op's cell hash while the current op probes (A/B: -DBK_OPS_PREFETCH=1
+// measured 0.4 % slower for frontier-order config 3, 1.8 % for config 5; profiles/r04/sweeps/r04z)
+#ifndef BK_OPS_PREFETCH
+#define BK_OPS_PREFETCH 0
+#endif
 #ifndef BK_STAGE_EAGER
 #define BK_STAGE_EAGER 1
 #endif
@@ -1570,8 +1575,7 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 //   chain, else the unused slot that ended the search (then maybe resize);
 // * discard: the key's slot becomes a dummy (absent key: no-op).
 // false: the table outgrew its storage (add only).
-__host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
-    const uint64_t h = t.hash[k];
+__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h) {
     const uint32_t mask = *t.mask;
     // One flat loop over the probe sequence (a divergent nested loop costs the wave far
     // more exec-mask bookkeeping than its VALU work): from i = hash & mask the 10 slots
@@ -1621,6 +1625,9 @@ __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool a
     return fs_resize(t, tmp, *t.used > 50000 ? *t.used * 2u : *t.used * 4u);
 }
 
+__host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
+    return fs_op_h(t, tmp, k, add, t.hash[k]);
+}
 __host__ __device__ inline bool fs_add(FsetRef t, int16_t* tmp, int16_t k) { return fs_op(t, tmp, k, true); }
 __host__ __device__ inline void fs_discard(FsetRef t, int16_t k) { fs_op(t, nullptr, k, false); }
 
@@ -1708,15 +1715,29 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
     // key offset + 21 of op o, 6 bits each: 0, -21, -19, 19, 21, -20, 20, -1, 1
     constexpr uint64_t KD = (21ull << 0) | (0ull << 6) | (2ull << 12) | (40ull << 18) | (42ull << 24) |
                             (1ull << 30) | (41ull << 36) | (20ull << 42) | (22ull << 48);
+    auto key_of = [&](int s) {
+        const int q = (s * 57) >> 9;  // s / 9 for s < 45
+        const int op = s - 9 * q;
+        const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
+        return cell + (int)((KD >> (6 * op)) & 63ull) - 21;
+    };
+#if BK_OPS_PREFETCH
+    // the next op's cell hash is loaded while this op probes the table
+    uint64_t hn = real ? t.hash[key_of((int)__builtin_ctzll(real))] : 0ull;
+#endif
 #pragma unroll 1
     while (real) {
         const int s = (int)__builtin_ctzll(real);
         real &= real - 1ull;
-        const int q = (s * 57) >> 9;  // s / 9 for s < 45
-        const int op = s - 9 * q;
-        const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
-        const int key = cell + (int)((KD >> (6 * op)) & 63ull) - 21;
-        if (!fs_op(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u)) return false;
+        const int op = s - 9 * ((s * 57) >> 9);
+        const int key = key_of(s);
+#if BK_OPS_PREFETCH
+        const uint64_t h = hn;
+        if (real) hn = t.hash[key_of((int)__builtin_ctzll(real))];
+#else
+        const uint64_t h = t.hash[key];
+#endif
+        if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h)) return false;
     }
     return true;
 }
