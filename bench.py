@@ -94,8 +94,11 @@ def parse(argv=None):
                          "search streams, the FastMCTS handle and the main stream do not share in-order queues "
                          "(HIP's default is 4); 0 leaves the environment's setting")
     ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
-                    help="config3 in-kernel move order: naive (default) or the reference's frontier order "
-                         "(CPython set tables carried per game)")
+                    help="config3 in-kernel move order of the line's value: naive (default) or the reference's "
+                         "frontier order (CPython set tables carried per game)")
+    ap.add_argument("--no-frontier-order", action="store_true",
+                    help="config3, naive order: skip the line's frontier_order object (the same measurement in the "
+                         "reference's default move order)")
     a = ap.parse_args(argv)
     if a.steps is None:
         a.steps = 1 if a.workload in ("config5", "config4") else (200 if a.workload == "config2" else 20)
@@ -171,6 +174,43 @@ def cpu_baseline_playouts(roots_np, seconds, order, rollouts, seed=None, gpu_out
         out["sample"] += "; the GPU's own games (same roots and Philox streams as the last timed step)"
         out["same_games_bit_identical"] = g == bytes(res)
     return out
+
+
+def cpu_baseline_frontier(roots_np, sets_np, seconds, rollouts, seed, gpu_out):
+    """The frontier-order config-3 CPU baseline: oracle/blokus_oracle.c plays the GPU's own
+    games of the last timed step -- same roots with the same CPython frontier-set tables
+    (root i // rollouts), same Philox streams (seed, playout id), the reference's default
+    move order -- on this host's cores (one playout per thread at a time; ctypes releases
+    the GIL inside or_playout_arena_philox), and compares the result records."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import pyoracle as O
+    cpu = host_cpu()
+    threads = cpu["cores"]
+    # raw clones of the root boards (a Board.copy() would re-lay the set tables out)
+    raw = [bytes(O.board_from(roots_np[g].tobytes(), sets_np[g])) for g in range(len(roots_np))]
+
+    def one(pid):
+        b = O.Board.from_buffer_copy(raw[pid // rollouts])
+        r, _ = O.playout_arena_philox(b, seed, pid, O.ORDER_FRONTIER)
+        return bytes(r)
+
+    n = 8 * threads
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(one, range(n)))
+        dt = time.perf_counter() - t0
+        n2 = min(len(roots_np) * rollouts, max(n, int(n * seconds / max(dt, 1e-3))))
+        t0 = time.perf_counter()
+        res = list(ex.map(one, range(n2)))
+        dt = time.perf_counter() - t0
+    g = gpu_out[:n2].cpu().numpy().tobytes()
+    return {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
+            "host": cpu, "order": "frontier",
+            "sample": f"the GPU's own first {n2} playouts of the last timed step (same roots and CPython "
+                      f"frontier tables, same Philox streams), oracle/blokus_oracle.c in frontier move order, "
+                      f"{threads} threads (one per usable core), {dt:.1f} s",
+            "same_games_bit_identical": g == b"".join(res)}
 
 
 def pin_host_cores(k=None):
@@ -306,23 +346,21 @@ def compute_roofline(valu_insts, avg_ms):
 
 
 # ------------------------------------------------------------------ config 3
-def run_config3(args, world, rank, local, dist):
+def _config3_measure(args, order, gpu, plan, dev, dist):
+    """W untimed + K timed config-3 steps in one move order on this rank: 256 synthetic
+    20-ply roots made on the GPU from the plan's root streams (naive order: bk_advance;
+    frontier order: bk_rollout_frontier SEM_ADVANCE, which also builds each root's four
+    CPython frontier-set tables), then per step 262,144 arena playouts (k_rollout /
+    k_rollout_fr) on the plan's playout streams.  Timed region: barrier + synchronize on
+    both sides; HIP events on the launching stream around every launch."""
     import numpy as np
     import torch
 
     from reinforcementlearning_blokus_amd import _native as N
-    from reinforcementlearning_blokus_amd.gpu import BlokusGPU, empty_state
-
-    from reinforcementlearning_blokus_amd.workloads import Config3Plan
-    games = args.games or 256
-    gpu = BlokusGPU(local)
-    dev = torch.device("cuda", local)
-    # every stream is a function of the global game index: rank r plays global games
-    # r * games .. (r + 1) * games - 1 (workloads.Config3Plan), so the N-rank job's
-    # gathered records equal a 1-rank run of the same N * games games
-    plan = Config3Plan(args.seed, games, args.rollouts, rank)
-    # synthetic mid-game roots, generated on the GPU (BK_SEM_ADVANCE from the empty board)
-    if args.order == "frontier":
+    from reinforcementlearning_blokus_amd.gpu import empty_state
+    games = plan.games
+    sets_np = sets = None
+    if order == "frontier":
         roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), games,
                                                  semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=plan.seed,
                                                  max_plies=args.root_plies,
@@ -341,7 +379,7 @@ def run_config3(args, world, rank, local, dist):
     plies_acc = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def step(k):
-        if args.order == "frontier":
+        if order == "frontier":
             gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k),
                                  root_index=idx, out=out, stream_base=plan.playout_stream_base)
         else:
@@ -369,40 +407,96 @@ def run_config3(args, world, rank, local, dist):
         elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in events]
     elapsed, (sims, all_plies) = reduce_max_sum(dist, dev, elapsed, [n * args.steps, int(plies_acc.item())])
-    if dist:
-        # RCCL gather of the last step's terminal results (32 B per playout) over xGMI,
-        # outside the timed region; rank r's playouts are the global block r
-        from reinforcementlearning_blokus_amd.shard import gather_blocks
-        gather_blocks(out, rank, world, dist)
-    value = sims / elapsed
-    if rank != 0:
-        return None
-    avg_ms = sum(kernel_ms) / len(kernel_ms)
-    plies_per_sim = all_plies / sims
-    bytes_per_sim = 2.0 * STATE_B * plies_per_sim + RESULT_B  # 256 B read + write per ply
+    return {"elapsed": elapsed, "sims": sims, "plies": all_plies, "kernel_ms": kernel_ms, "out": out,
+            "roots_np": roots_np, "sets_np": sets_np, "n": n}
+
+
+def _config3_fields(args, order, m, world):
+    """value / roofline / compute_roofline of one config-3 measurement (SURVEY 8(d) bytes:
+    256 B state read + write per ply plus the 32 B result, over the HIP-event launch time)."""
+    n = m["n"]
+    value = m["sims"] / m["elapsed"]
+    avg_ms = sum(m["kernel_ms"]) / len(m["kernel_ms"])
+    plies_per_sim = m["plies"] / m["sims"]
+    bytes_per_sim = 2.0 * STATE_B * plies_per_sim + RESULT_B
     achieved = (n * bytes_per_sim) / (avg_ms * 1e-3) / 1e9
-    kname = "k_rollout_fr" if args.order == "frontier" else "k_rollout"
+    kname = "k_rollout_fr" if order == "frontier" else "k_rollout"
     traffic, valu_insts, tsrc = traffic_for(kname, n)
-    line = {
-        "metric": METRIC, "value": value, "unit": "sims/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
-        "config": {"workload": "config3: 256 concurrent games x 1024 random rollouts (arena semantics, "
-                               f"{args.order} move order, Philox RNG) from GPU-generated 20-ply positions",
-                   "games": games, "rollouts_per_game": args.rollouts, "root_plies": args.root_plies,
-                   "playouts_per_step": n, "parallelism": f"dp{world} (independent games per rank)"},
+    return {
+        "value": value, "unit": "sims/s", "ms_per_step": m["elapsed"] / args.steps * 1e3,
+        "workload": f"config3: {args.games or 256} concurrent games x {args.rollouts} random rollouts (arena "
+                    f"semantics, {order} move order, Philox RNG) from GPU-generated {args.root_plies}-ply positions",
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname, "kernel_ms": avg_ms,
                      "plies_per_sim": plies_per_sim, "bytes_per_sim": bytes_per_sim, "traffic_profile": tsrc},
         "compute_roofline": compute_roofline(valu_insts, avg_ms),
     }
+
+
+def _config3_cpu(args, order, m, plan, value):
+    if order == "frontier":
+        cb = cpu_baseline_frontier(m["roots_np"], m["sets_np"], args.cpu_seconds, args.rollouts,
+                                   plan.step_seed(1000 + args.steps - 1), m["out"])
+    else:
+        cb = cpu_baseline_playouts(m["roots_np"], args.cpu_seconds, order, args.rollouts,
+                                   seed=plan.step_seed(1000 + args.steps - 1), gpu_out=m["out"])
+    cb["gpu_over_cpu"] = value / cb["value"]
+    cb["reference_python"] = ref_python(value, REF_PY_ARENA_SIMS_PER_CORE, cb["cores"],
+                                        "terminal random playout from ply 20, telemetry off")
+    return cb
+
+
+def run_config3(args, world, rank, local, dist):
+    """The default line.  Its value is the --order run (default naive: the reference with
+    BLOKUS_USE_FRONTIER_MOVEGEN=0); with the default order the line also carries a
+    `frontier_order` object, the same measurement in the reference's DEFAULT move order
+    (engine/move_generator.py:261-559 over the CPython frontier sets of
+    engine/board.py:315-367, k_rollout_fr) on the same plan (seeds, streams, steps), with
+    its own value, roofline and same-games CPU baseline."""
+    import torch
+
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    from reinforcementlearning_blokus_amd.workloads import Config3Plan
+    games = args.games or 256
+    gpu = BlokusGPU(local)
+    dev = torch.device("cuda", local)
+    # every stream is a function of the global game index: rank r plays global games
+    # r * games .. (r + 1) * games - 1 (workloads.Config3Plan), so the N-rank job's
+    # gathered records equal a 1-rank run of the same N * games games
+    plan = Config3Plan(args.seed, games, args.rollouts, rank)
+    m = _config3_measure(args, args.order, gpu, plan, dev, dist)
+    mf = None
+    if args.order == "naive" and not args.no_frontier_order:
+        mf = _config3_measure(args, "frontier", gpu, plan, dev, dist)
+    if dist:
+        # RCCL gather of the last step's terminal results (32 B per playout) over xGMI,
+        # outside the timed region; rank r's playouts are the global block r
+        from reinforcementlearning_blokus_amd.shard import gather_blocks
+        gather_blocks(m["out"], rank, world, dist)
+    if rank != 0:
+        return None
+    f = _config3_fields(args, args.order, m, world)
+    line = {
+        "metric": METRIC, "value": f["value"], "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": f["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": f["workload"], "games": games, "rollouts_per_game": args.rollouts,
+                   "root_plies": args.root_plies, "playouts_per_step": m["n"],
+                   "parallelism": f"dp{world} (independent games per rank)"},
+        "roofline": f["roofline"], "compute_roofline": f["compute_roofline"],
+    }
     if not args.no_cpu_baseline and world == 1:
-        cb = cpu_baseline_playouts(roots_np, args.cpu_seconds, args.order, args.rollouts,
-                                   seed=plan.step_seed(1000 + args.steps - 1), gpu_out=out)
-        cb["gpu_over_cpu"] = value / cb["value"]
-        cb["reference_python"] = ref_python(value, REF_PY_ARENA_SIMS_PER_CORE, cb["cores"],
-                                            "terminal random playout from ply 20, telemetry off")
-        line["cpu_baseline"] = cb
+        line["cpu_baseline"] = _config3_cpu(args, args.order, m, plan, f["value"])
+    if mf is not None:
+        ff = _config3_fields(args, "frontier", mf, world)
+        fo = {"value": ff["value"], "unit": "sims/s", "ms_per_step": ff["ms_per_step"], "steps": args.steps,
+              "warmup": args.warmup, "workload": ff["workload"],
+              "order": "the reference's default (BLOKUS_USE_FRONTIER_MOVEGEN=1): per (piece, orientation), "
+                       "anchors by the CPython iteration rank of the mover's frontier set",
+              "roofline": ff["roofline"], "compute_roofline": ff["compute_roofline"]}
+        if not args.no_cpu_baseline and world == 1:
+            fo["cpu_baseline"] = _config3_cpu(args, "frontier", mf, plan, ff["value"])
+        line["frontier_order"] = fo
     return line
 
 

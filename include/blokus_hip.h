@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 4
+#define BK_ABI_VERSION 5
 #define BK_BOARD 20
 #define BK_CELLS 400
 #define BK_PLAYERS 4
@@ -147,6 +147,30 @@ int bk_stream_create(bk_handle h, const uint32_t* cu_mask, int32_t mask_words, v
    bit 2); both cleared once reported. */
 int bk_synchronize(bk_handle h);
 int bk_last_error(bk_handle h, char* buf, size_t len);
+
+/* Tuning and test overrides (ABI 5; no reference counterpart).  bk_create reads each
+   from the environment variable of the same name once (BK_MG_GROUPS, ...); later changes
+   of the environment do not reach an existing handle, and no entry point reads the
+   environment.  bk_set_tuning sets one for this handle (-1 = automatic: the library's
+   measured choice).  Values are range-checked where they are used, as before. */
+enum {
+    BK_TUNE_MG_GROUPS = 0,       /* movegen orientation groups per board-player set      */
+    BK_TUNE_MG_STAGE,            /* bk_movegen_mask: 0 = per-lane stores (k_movegen_m)    */
+    BK_TUNE_MG_PARTS,            /* k_movegen_ml orientation ranges: 4, 5, 7 or 13        */
+    BK_TUNE_MG_PART_WAVES,       /* waves per k_movegen_ml block                          */
+    BK_TUNE_DEBUG_MAX_ITERS,     /* playout kernels' step guard (tests force a trip)      */
+    BK_TUNE_HANDOUT,             /* playout hand-out 0..2                   */
+    BK_TUNE_MCTS_COOP,           /* bk_mcts: 1 = one wave per search, 0 = one lane        */
+    BK_TUNE_COOP_BLOCKS_PER_CU,  /* k_mcts_coop(_h) resident blocks per CU                */
+    BK_TUNE_MCTS_SPREAD,         /* bk_mcts per-lane kernels: searches every spread lanes */
+    BK_TUNE_TREE_BATCH,          /* bk_mcts lockstep tree-phase threshold                 */
+    BK_TUNE_COOP_WALK,           /* k_mcts_coop(_h): 0 = serial frontier walks            */
+    BK_TUNE_COOP_BAL,            /* k_mcts_coop_h: 0 = per-lane HeuristicAgent sums       */
+    BK_TUNE_MCTS_PAIR,           /* bk_mcts spread 2: 0 = unsplit lanes (k_mcts)          */
+    BK_TUNE_COUNT
+};
+int bk_set_tuning(bk_handle h, int32_t key, int64_t value);
+int bk_get_tuning(bk_handle h, int32_t key, int64_t* value);
 
 /* ---- tables ------------------------------------------------------------------------ */
 /* Orientation table, global orientation id g in [0, 91): piece_id, orientation index,
@@ -420,7 +444,11 @@ typedef struct bk_mcts_cfg {
     int32_t rollout_policy;    /* BK_MCTS_ROLLOUT_*: the rollout_agent                  */
     int32_t flags;             /* BK_MCTS_ASYNC: with BK_MEM_DEVICE, return once the
                                   launch is enqueued (no wait; a tripped step guard is
-                                  then reported by bk_synchronize)                      */
+                                  then reported by bk_synchronize).  The running search
+                                  uses the handle's scratch, so the handle takes no other
+                                  launch (BK_EINVAL) until bk_synchronize, which waits
+                                  on the stream the search was launched on: one
+                                  asynchronous search per handle at a time            */
 } bk_mcts_cfg;
 #define BK_MCTS_ASYNC 1
 #define BK_MCTS_ROLLOUT_RANDOM 0    /* RandomAgent (agents/random_agent.py:49)            */

@@ -34,8 +34,14 @@ EXPORTS = (
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms", "bk_last_kernel",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
-    "bk_arena_step", "bk_mt_cursor_init",
+    "bk_arena_step", "bk_mt_cursor_init", "bk_set_tuning", "bk_get_tuning",
 )
+# bk_set_tuning keys (include/blokus_hip.h BK_TUNE_*), by the environment variable name
+# bk_create reads each from once
+TUNE_KEYS = {name: i for i, name in enumerate((
+    "BK_MG_GROUPS", "BK_MG_STAGE", "BK_MG_PARTS", "BK_MG_PART_WAVES", "BK_DEBUG_MAX_ITERS", "BK_HANDOUT",
+    "BK_MCTS_COOP", "BK_COOP_BLOCKS_PER_CU", "BK_MCTS_SPREAD", "BK_TREE_BATCH", "BK_COOP_WALK", "BK_COOP_BAL",
+    "BK_MCTS_PAIR"))}
 FSET_SLOTS = 256
 # bk_fset: the 4 players' CPython frontier-set tables (include/blokus_hip.h)
 FSET_DTYPE = np.dtype([("key", "<i2", (4, FSET_SLOTS)), ("mask", "<u2", (4,)), ("fill", "<u2", (4,)),
@@ -113,7 +119,7 @@ RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("statu
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
 assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
 
-ABI_VERSION = 4  # include/blokus_hip.h BK_ABI_VERSION
+ABI_VERSION = 5  # include/blokus_hip.h BK_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -179,6 +185,8 @@ def load():
             "bk_mcts": (C.c_int, [vp, vp, vp, vp, vp, C.c_int32, P(BkMctsCfg), vp, C.c_int32, vp, vp, vp, vp,
                                   vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int]),
             "bk_debug_sections": (C.c_int, [vp, vp, C.c_int32, C.c_int32]),
+            "bk_set_tuning": (C.c_int, [vp, C.c_int32, C.c_int64]),
+            "bk_get_tuning": (C.c_int, [vp, C.c_int32, P(C.c_int64)]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -341,6 +349,16 @@ class Handle:
 
     def synchronize(self):
         self.check(self._L.bk_synchronize(self._h), "bk_synchronize")
+
+    def set_tuning(self, name: str, value: int | None):
+        """bk_set_tuning by environment-variable name (TUNE_KEYS); None = automatic."""
+        self.check(self._L.bk_set_tuning(self._h, TUNE_KEYS[name], -1 if value is None else int(value)),
+                   "bk_set_tuning")
+
+    def get_tuning(self, name: str) -> int | None:
+        v = C.c_int64()
+        self.check(self._L.bk_get_tuning(self._h, TUNE_KEYS[name], C.byref(v)), "bk_get_tuning")
+        return None if v.value < 0 else int(v.value)
 
     def last_kernel_ms(self) -> float:
         ms = C.c_float()

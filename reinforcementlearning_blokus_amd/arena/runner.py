@@ -462,6 +462,73 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
     return mcts, fast, seat_kind, seat_agent
 
 
+def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, log_tables) -> str:
+    """Diagnostics for a search launch that returned a failed search (BK_ARENA_CAPTURE).
+    Saves the launch's inputs as the kernel saw them, its outputs and the failed searches'
+    node pools, then replays on a fresh handle and stream with nothing else running:
+    (a) the whole launch, (b) the failed searches alone, (c) the whole launch over node
+    pools pre-filled with the failed run's final pools (a dirty pool).  A clean (a)/(b)
+    points at the concurrent run (another writer, a buffer lifetime); a replay that fails
+    the same way points at the kernel and its inputs.  Returns the file prefix."""
+    import json
+
+    import torch
+
+    from .. import _native as N
+    from ..gpu import BlokusGPU
+    os.makedirs(capture_dir, exist_ok=True)
+    base = os.path.join(capture_dir, f"mcts_fail_job{job['seq']}")
+    cap = job["cap"]
+    iters, roll, c, use_tt, policy = job["key"]
+    dev = cap["roots"].device
+    torch.cuda.synchronize(dev)
+    n = cap["roots"].shape[0]
+    bad_idx = np.flatnonzero(bad)
+    arrs = {k: v.cpu().numpy() for k, v in cap.items()}
+    arrs.update(out=job["o_d"].cpu().numpy(), nodes_bad=job["nodes"][bad_idx].cpu().numpy(), bad_idx=bad_idx,
+                games=np.asarray(job["games"]), aid=np.asarray(job["aid"]),
+                zob=zob_d.index_select(0, cap["zidx"].long()).cpu().numpy(),
+                key=np.array([iters, roll, use_tt, policy], np.int64), c=np.array([c]))
+
+    def replay(sel, dirty=False):
+        s = torch.as_tensor(np.asarray(sel, np.int64), device=dev)
+        k = len(sel)
+        g = BlokusGPU(dev.index)
+        st = torch.cuda.Stream(dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(st):
+            pick = lambda t: t.index_select(0, s).contiguous()  # noqa: E731
+            nodes = pick(job["nodes"]) if dirty else torch.zeros((k, job["nodes"].shape[1]), dtype=torch.uint8,
+                                                                 device=dev)
+            out = torch.zeros((k, N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            tt = (pick(cap["ttk"]), pick(cap["ttv"]), pick(cap["ttc"])) if use_tt else (None, None, None)
+            g.mcts_device(pick(cap["roots"]), pick(cap["sets"]), pick(cap["players"]), None, zob_d,
+                          pick(cap["zidx"]), pick(cap["mt"]), log_tables[iters], nodes, out, iterations=iters,
+                          tt_keys=tt[0], tt_vals=tt[1], tt_count=tt[2], max_rollout_moves=roll, exploration=c,
+                          rollout_policy=policy, asynchronous=True)
+        st.synchronize()
+        g.synchronize()
+        return out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(k), g.last_kernel()
+
+    orig = o
+    fields = ["best_move", "iterations_run", "tt_hits", "rollouts", "nodes_used", "status"]
+    report = {"seq": job["seq"], "n": int(n), "bad_idx": bad_idx.tolist(), "slot": job["slot"],
+              "inflight_at_launch": job["inflight_at_launch"], "key": [iters, roll, c, use_tt, policy],
+              "orig_status": orig["status"][bad_idx].tolist()}
+    for name, sel, dirty in (("whole", np.arange(n), False), ("bad_alone", bad_idx, False),
+                             ("whole_dirty_pool", np.arange(n), True)):
+        r, kname = replay(sel, dirty)
+        arrs["replay_" + name] = r.view(np.uint8)
+        ref = orig[sel]
+        diff = [int(i) for i in range(len(sel)) if any(r[f][i] != ref[f][i] for f in fields)]
+        report[name] = {"kernel": kname, "status_bad": int(np.count_nonzero(r["status"] & ~np.uint32(N.MCTS_EUNCERT))),
+                        "differs_from_launch": [int(sel[i]) for i in diff][:64], "n_differs": len(diff)}
+    np.savez_compressed(base + ".npz", **arrs)
+    with open(base + ".json", "w") as f:
+        json.dump(report, f, indent=1)
+    return base
+
+
 def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping[str, str]], gseeds: List[int],
                       agents_dev, *, run_id: str, device: int, progress=None) -> List[Dict[str, Any]]:
     """run_games_batched with every position, frontier table and agent stream resident in
@@ -551,10 +618,8 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     # (fast_on_device), so the next step places their move.  BK_ARENA_PIPELINE=0: one
     # search at a time on the main stream, waited for at once, FastMCTS host-staged.
     pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
-    # at most 16: 24 search streams with 32 HIP queues returned searches with
-    # BK_MCTS_ELOG statuses in one measurement (profiles/r04/sweeps/r04n, not understood
-    # yet); 8..16 are validated and no slower
-    n_slots = min(16, max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8")))) if pipeline else 1
+    # at most 32: torch hands out streams round-robin from a pool of 32 per priority
+    n_slots = min(32, max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8")))) if pipeline else 1
     job_games = max(1, int(os.environ.get("BK_ARENA_JOB_GAMES", "1000000"))) if pipeline else 1 << 30
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
     jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
@@ -569,6 +634,9 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         jstreams = [torch.cuda.ExternalStream(e.handle.stream_create(mask), device=dev) for e in engines]
     free_slots = list(range(n_slots))
     jobs: List[Dict[str, Any]] = []
+    # BK_ARENA_CAPTURE=<dir> (diagnostics): keep every search launch's inputs; a launch
+    # that returns a failed search is saved there and replayed alone (_capture_failed_job)
+    capture_dir = os.environ.get("BK_ARENA_CAPTURE", "")
     fast_eng = BlokusGPU(device) if pipeline else gpu
     inflight = np.zeros(n, bool)
 
@@ -594,6 +662,12 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             nodes = torch.empty((len(games), mcts_node_cap(iters) * N.MCTS_NODE_DTYPE.itemsize),
                                 dtype=torch.uint8, device=dev)
             o_d = torch.zeros((len(games), N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            cap_in = None
+            if capture_dir:  # the launch's inputs as the kernel sees them (it advances mt / tt in place)
+                cap_in = {"roots": roots_d.clone(), "sets": sets_g.clone(), "players": players.clone(),
+                          "zidx": zi_d.clone(), "mt": mt_g.clone()}
+                if use_tt:
+                    cap_in.update(ttk=tt[0].clone(), ttv=tt[1].clone(), ttc=tt[2].clone())
             eng.mcts_device(roots_d, sets_g, players, rh_d, zob_d, zi_d, mt_g, log_tables[iters], nodes, o_d,
                             iterations=iters, tt_keys=tt[0], tt_vals=tt[1], tt_count=tt[2],
                             max_rollout_moves=roll, exploration=c, rollout_policy=policy, asynchronous=pipeline)
@@ -607,8 +681,11 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         for t in (ga_d, roots_d, sets_g, players, zi_d, mt_g) + (tt if use_tt else ()):
             t.record_stream(js)
         inflight[games] = True
+        # nodes stays referenced until the job is finished: the launch is asynchronous
         jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done,
-                     "t0": time.perf_counter()})
+                     "t0": time.perf_counter(), "nodes": nodes, "cap": cap_in, "seq": tl["mcts_jobs_launched"],
+                     "key": (iters, roll, c, use_tt, policy), "inflight_at_launch": len(jobs)})
+        tl["mcts_jobs_launched"] += 1
         if not pipeline:
             mcts_finish(jobs.pop(0))
 
@@ -623,8 +700,12 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         o = job["o_d"].cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(len(games))
         bad = o["status"] & ~np.uint32(N.MCTS_EUNCERT)
         if bad.any():
+            where = ""
+            if capture_dir:
+                where = " (inputs and replays in " + _capture_failed_job(capture_dir, job, o, bad, zob_d,
+                                                                      log_tables) + ")"
             raise RuntimeError(f"bk_mcts: {int(np.count_nonzero(bad))} searches stopped early, status bits "
-                               f"{int(np.bitwise_or.reduce(bad))}")
+                               f"{int(np.bitwise_or.reduce(bad))}{where}")
         prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
         its = o["iterations_run"].astype(np.int64)
         kms, kplies = eng.last_kernel_ms(), int(o["rollout_plies"].astype(np.int64).sum())
@@ -705,7 +786,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
 
     stops_q = np.zeros(n, np.int64)  # the FastMCTS seats' quick_index (stop info)
     # host-side timeline: jobs' launch -> completion seen, games inside a search per step
-    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "search_games_per_step": 0}
+    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "search_games_per_step": 0, "mcts_jobs_launched": 0}
     try:
         while active.any():
             prof["rounds"] += 1

@@ -84,22 +84,11 @@
 // one memory latency instead of two.  Within noise for the 3-block k_rollout_fr
 // (profiles/r04/sweeps/r04p); +1.0 % for the 4-block one, 31.73 -> 32.03 M playouts/s
 // over three pairs of runs (profiles/r04/sweeps/r04v).  A/B: -DBK_STAGE_EAGER=0
-// fs_run_ops loads the next op's cell hash while the current op probes (A/B: -DBK_OPS_PREFETCH=1
-// measured 0.4 % slower for frontier-order config 3, 1.8 % for config 5; profiles/r04/sweeps/r04z)
-#ifndef BK_OPS_PREFETCH
-#define BK_OPS_PREFETCH 0
-#endif
 #ifndef BK_STAGE_EAGER
 #define BK_STAGE_EAGER 1
 #endif
 #ifndef BK_STAGE_EAGER_MAX
 #define BK_STAGE_EAGER_MAX 64
-#endif
-// 1: the stencil skips anchor rows no lane of the wave can use (live_anchor_rows) --
-// measured no faster: the per-row branches cost the kernel spills;
-// 0: the round-3 stencil (every anchor row), a build for the A/B measurement
-#ifndef BK_ROWSKIP_BUILD
-#define BK_ROWSKIP_BUILD 0
 #endif
 
 // Section timers (diagnostic build only, -DBK_SECTION_PROF): per-wave shader-clock
@@ -311,12 +300,9 @@ struct StencilClass {
             return BITOP3(c, b, b, LUT_ANDN);
         }
     }
-    // LANE_W1: w1 differs per lane (the lane-pair split of count_class_pair).  live: bit r
-    // set iff anchor row r can hold a legal placement in some lane of the wave (a C row
-    // in r .. r + H - 1, wave-uniform, see live_anchor_rows); the other rows are skipped
-    // with a uniform branch (their ok is 0 in every lane, f is not called)
+    // LANE_W1: w1 differs per lane (the lane-pair split of count_class_pair)
     template <bool LANE_W1 = false, typename F>
-    __device__ __forceinline__ static void scan(const Planes& P, uint32_t w1, F&& f, uint32_t live = ~0u) {
+    __device__ __forceinline__ static void scan(const Planes& P, uint32_t w1, F&& f) {
         // Shift amounts go to VGPRs: a VALU op reading an SGPR is never dual-issued on
         // gfx950 (tools/valu_probe2.hip).  NOTE: the v_bcnt below keeps
         // the whole stream at the single-issue rate anyway, so today this is neutral.
@@ -332,43 +318,12 @@ struct StencilClass {
         // and the live set no longer fits 3 waves per SIMD (other waves hide latency)
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-            // test the row's bit here (an opaque copy per row: hoisted out of the entry
-            // loop, the 20 row conditions would take 40 SGPRs and spill)
-#if BK_ROWSKIP_BUILD
-            uint32_t lv = live;
-            asm volatile("" : "+s"(lv));
-            if (!((lv >> r) & 1u)) continue;
-#endif
             const uint64_t t0 = tv<0>(P, r, sh);
             f(r, fold<1>(P, r, sh, lo(t0), hi(t0)));
             __builtin_amdgcn_sched_barrier(0);
         }
     }
 };
-
-// Anchor rows that can hold a legal placement of a piece of height H in some lane of the
-// wave: a legal placement covers a C (corner) cell, so rows r whose span r .. r + H - 1
-// holds no C row in ANY lane count 0 everywhere.  Bit r of lh[H - 1]; wave-uniform (one
-// ballot per board row).  The lanes of a rollout wave play the same root, so their
-// movers' corners lie in the same bands of rows (~10 % of the stencil's anchor rows
-// are skipped over random playouts from 20-ply roots).
-struct LiveRows {
-    uint32_t lh[5];
-};
-__device__ __forceinline__ LiveRows live_anchor_rows(const Planes& P) {
-    uint32_t live = 0;
-#pragma unroll
-    for (int R = 0; R < 20; ++R) live |= (__builtin_amdgcn_ballot_w64(P.c(R) != 0u) != 0ull) ? (1u << R) : 0u;
-    live = __builtin_amdgcn_readfirstlane(live);
-    LiveRows L;
-    uint32_t acc = live;
-#pragma unroll
-    for (int h = 0; h < 5; ++h) {
-        L.lh[h] = acc;  // rows r with a C row in r .. r + h
-        acc |= live >> (h + 1);
-    }
-    return L;
-}
 
 // Per-orientation counts in LDS, 10 bits each, three per dword: orientation g lives in
 // dword g / 3 at bit 10 * (g % 3), laid out [dword][lane] (31 dwords per lane).  The
@@ -425,8 +380,7 @@ __device__ __forceinline__ LiveRows live_anchor_rows(const Planes& P) {
 // Orientations whose piece no lane of the wave may still play are skipped with a
 // uniform branch.
 template <bool STORE, int H, int... T>
-__device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl,
-                                                const LiveRows& L) {
+__device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl) {
     uint32_t total = 0;
     uint32_t w0 = kClass[i0][0], w1 = kClass[i0][1];
 #pragma unroll 1
@@ -438,7 +392,7 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
         const bool av = (avail >> (piece - 1u)) & 1u;
         if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
             uint32_t c = 0;
-            StencilClass<H, T...>::scan(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); }, L.lh[H - 1]);
+            StencilClass<H, T...>::scan(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); });
             c = av ? c : 0u;
             if constexpr (STORE) atomicAdd(cl + (g / 3) * WAVE, c << (10 * (g % 3)));
             total += c;
@@ -456,7 +410,7 @@ __device__ __forceinline__ uint32_t count_class(int i0, int i1, const Planes& P,
 // field stays 0, so the two columns add up to the full count vector (pick_orient<true>).
 template <bool STORE, int H, int... T>
 __device__ __forceinline__ uint32_t count_class_pair(int i0, int i1, const Planes& P, uint32_t avail, uint32_t* cl,
-                                                     bool odd, const LiveRows& L) {
+                                                     bool odd) {
     uint32_t total = 0;
 #pragma unroll 1
     for (int ia = i0; ia < i1; ia += 2) {
@@ -469,8 +423,7 @@ __device__ __forceinline__ uint32_t count_class_pair(int i0, int i1, const Plane
         const bool av = ((avail >> (piece - 1u)) & 1u) && (has_b || !odd);
         if (__builtin_amdgcn_ballot_w64(av) != 0ull) {
             uint32_t c = 0;
-            StencilClass<H, T...>::template scan<true>(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); },
-                                                       L.lh[H - 1]);
+            StencilClass<H, T...>::template scan<true>(P, w1, [&](int, uint32_t ok) { c = bcnt_acc(ok, c); });
             c = av ? c : 0u;
             if constexpr (STORE) atomicAdd(cl + (g / 3) * WAVE, c << (10 * (g % 3)));
             total += c;
@@ -479,67 +432,10 @@ __device__ __forceinline__ uint32_t count_class_pair(int i0, int i1, const Plane
     return total;
 }
 
-// Tuning variant (BK_STENCIL_LITERAL): every stencil-table entry as its own
-// straight-line code with literal column shifts (code = t | shift << 8), piece and
-// orientation as constants -- no scalar table loads, no shift amounts moved from SGPRs.
-template <int H, int... CODES>
-struct StencilEntry {
-    static constexpr int NT = sizeof...(CODES);
-    static constexpr int NR = 21 - H;
-    static constexpr int cs[NT] = {CODES...};
-    template <int K>
-    __device__ __forceinline__ static uint64_t tv(const Planes& P, int r) {
-        constexpr int d = (cs[K] & 0xFF) >> 2, kind = cs[K] & 3, sh = cs[K] >> 8;
-        const uint64_t v = kind == 1 ? P.BCP[r + d] : kind == 2 ? P.BCV[r + d] : P.BC[r + d];
-        return sh == 0 ? v : v >> sh;
-    }
-    template <int K>
-    __device__ __forceinline__ static uint32_t fold(const Planes& P, int r, uint32_t b, uint32_t c) {
-        if constexpr (K + 2 <= NT - 1) {
-            const uint64_t t0 = tv<K>(P, r), t1 = tv<K + 1>(P, r);
-            b = BITOP3(b, (uint32_t)t0, (uint32_t)t1, LUT_OR3);
-            c = BITOP3(c, (uint32_t)(t0 >> 32), (uint32_t)(t1 >> 32), LUT_OR3);
-            return fold<K + 2>(P, r, b, c);
-        } else if constexpr (K + 2 == NT) {
-            const uint64_t t0 = tv<K>(P, r), t1 = tv<K + 1>(P, r);
-            b = BITOP3(b, (uint32_t)t0, (uint32_t)t1, LUT_OR3);
-            c = c | (uint32_t)(t0 >> 32);
-            return BITOP3(c, (uint32_t)(t1 >> 32), b, LUT_OR2_ANDN);
-        } else if constexpr (K + 1 == NT) {
-            const uint64_t t0 = tv<K>(P, r);
-            b = b | (uint32_t)t0;
-            return BITOP3(c, (uint32_t)(t0 >> 32), b, LUT_OR2_ANDN);
-        } else {
-            return BITOP3(c, b, b, LUT_ANDN);
-        }
-    }
-    __device__ __forceinline__ static uint32_t count(const Planes& P) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const uint64_t t0 = tv<0>(P, r);
-            acc = bcnt_acc(fold<1>(P, r, (uint32_t)t0, (uint32_t)(t0 >> 32)), acc);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        return acc;
-    }
-};
-
-template <bool STORE, int PIECE, int G, int H, int... CODES>
-__device__ __forceinline__ uint32_t count_entry(const Planes& P, uint32_t avail, uint32_t* cl) {
-    const bool av = (avail >> (PIECE - 1)) & 1u;
-    if (__builtin_amdgcn_ballot_w64(av) == 0ull) return 0u;
-    uint32_t c = StencilEntry<H, CODES...>::count(P);
-    c = av ? c : 0u;
-    if constexpr (STORE) atomicAdd(cl + (G / 3) * WAVE, c << (10 * (G % 3)));
-    return c;
-}
-
 // PAIR: lanes 2j and 2j + 1 hold the same board-player and split the entries
 // (count_class_pair); each returns its share of the total.
 template <bool STORE, bool PAIR = false>
-__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane,
-                                                   bool rowskip = true) {
+__device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t avail, uint32_t* cnt, int lane) {
     uint32_t t = 0;
     uint32_t* cl = cnt + lane;  // this lane's dwords; the orientation part is uniform
     if constexpr (STORE) {
@@ -553,36 +449,21 @@ __device__ __forceinline__ uint32_t movegen_counts(const Planes& P, uint32_t ava
     int tb0 = 0;
     asm volatile("" : "+s"(tb0));
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
-#if BK_ROWSKIP_BUILD
-    LiveRows L = live_anchor_rows(P);
-    if (!rowskip)  // uniform (tuning A/B: BK_ROWSKIP=0)
-        for (int h = 0; h < 5; ++h) L.lh[h] = ~0u;
-#else
-    (void)rowskip;
-    const LiveRows L{{~0u, ~0u, ~0u, ~0u, ~0u}};
-#endif
-#ifdef BK_STENCIL_LITERAL
-    (void)tb0;
-#define BK_COUNT_ENTRY(PIECE, G, H, ...) t += count_entry<STORE, PIECE, G, H, __VA_ARGS__>(P, avail, cl);
-    BK_ENTRY_LIST(BK_COUNT_ENTRY)
-#undef BK_COUNT_ENTRY
-#else
     // the running total is pinned after every class (the empty asm): left to itself the
     // compiler keeps the 49 class totals live to the end of the stencil and sums them
     // there, ~40 VGPRs that spilled in the frontier-order kernel
     if constexpr (PAIR) {
         const bool odd = (lane & 1) != 0;
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd, L); \
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class_pair<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, odd); \
         asm volatile("" : "+v"(t));
         BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     } else {
-#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl, L); \
+#define BK_COUNT_CLASS(i0, i1, H, ...) t += count_class<STORE, H, __VA_ARGS__>(i0 + tb0, i1 + tb0, P, avail, cl); \
         asm volatile("" : "+v"(t));
         BK_CLASS_LIST(BK_COUNT_CLASS)
 #undef BK_COUNT_CLASS
     }
-#endif
     return t;
 }
 
@@ -1721,22 +1602,13 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
         const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
         return cell + (int)((KD >> (6 * op)) & 63ull) - 21;
     };
-#if BK_OPS_PREFETCH
-    // the next op's cell hash is loaded while this op probes the table
-    uint64_t hn = real ? t.hash[key_of((int)__builtin_ctzll(real))] : 0ull;
-#endif
 #pragma unroll 1
     while (real) {
         const int s = (int)__builtin_ctzll(real);
         real &= real - 1ull;
         const int op = s - 9 * ((s * 57) >> 9);
         const int key = key_of(s);
-#if BK_OPS_PREFETCH
-        const uint64_t h = hn;
-        if (real) hn = t.hash[key_of((int)__builtin_ctzll(real))];
-#else
         const uint64_t h = t.hash[key];
-#endif
         if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h)) return false;
     }
     return true;
@@ -2297,7 +2169,6 @@ struct RolloutArgs {
                                // s, s + nslots, ...; 2: slot s plays s, then only slots
                                // < long_slots pull the rest from the counter (whole waves)
     uint32_t long_slots;
-    int32_t rowskip;           // 1: skip anchor rows no lane of the wave can use (live_anchor_rows)
     const uint8_t* quick_masks;  // bk_arena_step: per game, bits 0-3 FastMCTS stop seats (stop_out)
     const int32_t* forced;       // bk_arena_step: per game, the stop seat's chosen move (or -1)
     bk_stop_info* stop_out;      // bk_arena_step: per game, the FastMCTS root inputs at a stop
@@ -2653,7 +2524,7 @@ __device__ __forceinline__ void stop_info(const RolloutArgs& a, const Game& g, c
     si.quick_index = 0;
     si.quick_reward = 0.0;
     if (a.quick_masks && ((a.quick_masks[g.pid] >> p) & 1u)) {
-        (void)movegen_counts<true>(P, avail, my, lane, a.rowskip != 0);
+        (void)movegen_counts<true>(P, avail, my, lane);
         // list positions of the first 3 moves by piece descending: orientations are
         // piece-major, so piece P's moves are one run [s, s + c) of the list
         uint32_t k3[3] = {0u, 0u, 0u}, suf = 0u, cp = 0u;
@@ -2805,7 +2676,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             total = 0;
             // uniform-random movers: counts, draw, orientation (before the area is reused)
             if (__builtin_amdgcn_ballot_w64(!idle && !heur)) {
-                const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane, a.rowskip != 0);
+                const uint32_t t = movegen_counts<true>(P, heur ? 0u : avail, my, lane);
                 if (!idle && !heur) {
                     total = t;
                     // (a stop seat draws nothing: bk_arena_advance hands its turn back; a
@@ -2837,7 +2708,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 }
             }
         } else {
-            total = movegen_counts<true>(P, avail, my, lane, a.rowskip != 0);
+            total = movegen_counts<true>(P, avail, my, lane);
         }
         SECT(2);
         if (idle) continue;
@@ -4616,7 +4487,22 @@ struct bk_handle_s {
     int fr_blocks_per_cu = 0;    // k_rollout_fr
     int mcts_blocks_per_cu = 0;  // k_mcts
     const char* last_kernel = "";  // name of the kernel the last timed call launched
+    // tuning / test overrides (bk_set_tuning; read from the environment once, in bk_create)
+    int64_t tune[BK_TUNE_COUNT];
+    // an asynchronous bk_mcts search is running on `busy_stream` with this handle's scratch
+    bool busy = false;
+    hipStream_t busy_stream = nullptr;
 };
+
+static const char* const kTuneNames[BK_TUNE_COUNT] = {
+    "BK_MG_GROUPS", "BK_MG_STAGE", "BK_MG_PARTS", "BK_MG_PART_WAVES", "BK_DEBUG_MAX_ITERS", "BK_HANDOUT",
+    "BK_MCTS_COOP", "BK_COOP_BLOCKS_PER_CU", "BK_MCTS_SPREAD", "BK_TREE_BATCH", "BK_COOP_WALK", "BK_COOP_BAL",
+    "BK_MCTS_PAIR"};
+
+// the tuning value for key, or dflt when automatic (-1)
+static inline int64_t tune_or(const bk_handle_s* h, int key, int64_t dflt) {
+    return h->tune[key] < 0 ? dflt : h->tune[key];
+}
 
 #ifdef BK_SECTION_PROF
 static std::vector<int (*)(unsigned long long*, int)>& sect_readers() {
@@ -4635,6 +4521,15 @@ static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
     do {                                                                                \
         hipError_t _e = (call);                                                         \
         if (_e != hipSuccess) return set_err((h), BK_EHIP, #call ": %s", hipGetErrorString(_e)); \
+    } while (0)
+
+// every launching entry point: the handle's scratch may be in use by an asynchronous
+// bk_mcts search (BK_MCTS_ASYNC) until bk_synchronize
+#define BK_IDLE(h, name)                                                                \
+    do {                                                                                \
+        if ((h)->busy)                                                                  \
+            return set_err((h), BK_EINVAL, name ": an asynchronous bk_mcts search is still running on " \
+                                           "this handle (bk_synchronize first)%s", "");  \
     } while (0)
 
 static int grow(bk_handle h, void** p, size_t* cap, size_t need) {
@@ -4685,6 +4580,10 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
         return BK_EHIP;
     }
     h->num_cu = prop.multiProcessorCount;
+    for (int k = 0; k < BK_TUNE_COUNT; ++k) {  // the only place the environment is read
+        const char* env = getenv(kTuneNames[k]);
+        h->tune[k] = env && *env ? (int64_t)strtoll(env, nullptr, 10) : -1;
+    }
     int bpc = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_rollout, BLOCK, 0) != hipSuccess || bpc < 1) bpc = 1;
     h->rollout_blocks_per_cu = bpc;
@@ -4712,6 +4611,7 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
 int bk_destroy(bk_handle h) {
     if (!h) return BK_EINVAL;
     (void)hipSetDevice(h->device);
+    if (h->busy) (void)hipStreamSynchronize(h->busy_stream);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
                     h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh};
@@ -4748,6 +4648,11 @@ int bk_set_stream(bk_handle h, void* stream) {
 int bk_synchronize(bk_handle h) {
     if (!h) return BK_EINVAL;
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->busy) {  // the asynchronous search's stream (bk_set_stream may have moved h->cur)
+        HIPCHK(h, hipStreamSynchronize(h->busy_stream));
+        h->busy = false;
+        h->busy_stream = nullptr;
+    }
     HIPCHK(h, hipStreamSynchronize(h->cur));
     uint32_t sticky = 0;
     HIPCHK(h, hipMemcpy(&sticky, h->d_counter + 2, sizeof sticky, hipMemcpyDeviceToHost));
@@ -4763,6 +4668,19 @@ int bk_synchronize(bk_handle h) {
 int bk_last_error(bk_handle h, char* buf, size_t len) {
     if (!h || !buf || len == 0) return BK_EINVAL;
     snprintf(buf, len, "%s", h->err);
+    return BK_OK;
+}
+
+int bk_set_tuning(bk_handle h, int32_t key, int64_t value) {
+    if (!h || key < 0 || key >= BK_TUNE_COUNT || value < -1)
+        return set_err(h, BK_EINVAL, "bk_set_tuning: unknown key or value < -1%s", "");
+    h->tune[key] = value;
+    return BK_OK;
+}
+
+int bk_get_tuning(bk_handle h, int32_t key, int64_t* value) {
+    if (!h || !value || key < 0 || key >= BK_TUNE_COUNT) return set_err(h, BK_EINVAL, "bk_get_tuning: bad key%s", "");
+    *value = h->tune[key];
     return BK_OK;
 }
 
@@ -4808,6 +4726,7 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
         return set_err(h, BK_EINVAL, "bk_movegen: invalid arguments%s", "");
     if (n == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_movegen");
     void *d_states, *d_players;
     int rc = stage_in(h, states, sizeof(bk_state) * (size_t)n, mem, &d_states, &h->d_in, &h->d_in_cap);
     if (rc) return rc;
@@ -4835,7 +4754,7 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     const int waves = (n + WAVE - 1) / WAVE;
     int groups = (4 * h->num_cu + waves - 1) / waves;
     groups = groups < 8 ? 8 : (groups > MG_GROUPS_DEFAULT_MAX ? MG_GROUPS_DEFAULT_MAX : groups);
-    if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
+    groups = (int)tune_or(h, BK_TUNE_MG_GROUPS, groups);
     if (groups < 1) groups = 1;
     if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
     MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups, nullptr};
@@ -4863,6 +4782,7 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     if (mem == BK_MEM_DEVICE && out_mask && ((uintptr_t)out_mask & 7))
         return set_err(h, BK_EINVAL, "bk_movegen_mask: out_mask must be 8-byte aligned%s", "");
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_movegen_mask");
     void *d_states, *d_players;
     int rc = stage_in(h, states, sizeof(bk_state) * (size_t)n, mem, &d_states, &h->d_in, &h->d_in_cap);
     if (rc) return rc;
@@ -4882,7 +4802,7 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     const int waves = (n + WAVE - 1) / WAVE;
     int groups = (4 * h->num_cu + waves - 1) / waves;
     groups = groups < 8 ? 8 : (groups > MG_GROUPS_DEFAULT_MAX ? MG_GROUPS_DEFAULT_MAX : groups);
-    if (const char* env = getenv("BK_MG_GROUPS")) groups = atoi(env);  // tuning override
+    groups = (int)tune_or(h, BK_TUNE_MG_GROUPS, groups);
     if (groups < 1) groups = 1;
     if (groups > MG_GROUPS_MAX) groups = MG_GROUPS_MAX;
     const int sets = ((waves + MG_XCDS - 1) / MG_XCDS) * MG_XCDS;
@@ -4892,13 +4812,11 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     // LDS-staged whole-line writes (k_movegen_ml): the groups' waves split over MG_PARTS
     // orientation ranges of one set each; BK_MG_STAGE=0 keeps the per-lane stores
     bool staged = out_mask != nullptr;
-    if (const char* env = getenv("BK_MG_STAGE")) staged = staged && atoi(env) != 0;  // A/B override
+    staged = staged && tune_or(h, BK_TUNE_MG_STAGE, 1) != 0;
     if (staged) {
-        int parts = 4;
-        if (const char* env = getenv("BK_MG_PARTS")) parts = atoi(env);  // tuning: 4, 5, 7 or 13
+        int parts = (int)tune_or(h, BK_TUNE_MG_PARTS, 4);  // 4, 5, 7 or 13
         if (parts != 5 && parts != 7 && parts != 13) parts = 4;
-        int wp = groups / parts;
-        if (const char* env = getenv("BK_MG_PART_WAVES")) wp = atoi(env);  // tuning override
+        int wp = (int)tune_or(h, BK_TUNE_MG_PART_WAVES, groups / parts);
         wp = wp < 1 ? 1 : (wp > MG_PART_WAVES_MAX ? MG_PART_WAVES_MAX : wp);
         const dim3 grid(sets * parts), blk(wp * WAVE);
         static const uint32_t kClassHost[BK_NUM_ORIENTS][2] = BK_CLASS_TABLE_INIT;
@@ -4942,6 +4860,7 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
         return set_err(h, BK_EINVAL, "bk_has_moves: invalid arguments%s", "");
     if (n == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_has_moves");
     void* d_states;
     int rc = stage_in(h, states, sizeof(bk_state) * (size_t)n, mem, &d_states, &h->d_in, &h->d_in_cap);
     if (rc) return rc;
@@ -4994,6 +4913,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         return set_err(h, BK_EINVAL, "bk_rollout: heuristic_seats (4 bits) needs BK_ORDER_FRONTIER%s", "");
     if (n_playouts == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_rollout");
     void *d_roots, *d_idx = nullptr, *d_seeds = nullptr;
     int rc = stage_in(h, roots, sizeof(bk_state) * (size_t)n_roots, mem, &d_roots, &h->d_in, &h->d_in_cap);
     if (rc) return rc;
@@ -5080,13 +5000,12 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     const uint64_t per_lane = ((uint64_t)n_playouts + nslots - 1) / nslots + 1;
     const uint64_t per_game = (cfg->semantics == BK_SEM_ROLLOUT ? (uint64_t)cfg->max_plies + 2u : 100u);
     uint64_t iters = 2 * per_lane * per_game + 64u;  // 2x: uneven hand-outs (handout 2)
-    if (const char* dbg = getenv("BK_DEBUG_MAX_ITERS")) iters = strtoull(dbg, nullptr, 10);  // tests: force the guard
+    iters = (uint64_t)tune_or(h, BK_TUNE_DEBUG_MAX_ITERS, (int64_t)iters);  // tests: force the guard
     RolloutArgs a{(const bk_state*)d_roots, n_roots, (const int32_t*)d_idx, n_playouts, *cfg,
                   (const uint32_t*)d_seeds, d_out, (uint32_t*)h->d_slab, nslots, h->d_counter,
                   (uint32_t)(iters > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : iters), d_states,
                   (const bk_fset*)d_rsets, d_osets, fr ? (FsLane*)h->d_fslab : nullptr,
-                  (const uint8_t*)d_masks, (uint32_t*)d_rng, fr ? 0 : 2, 0u, 1};
-    if (const char* env = getenv("BK_ROWSKIP")) a.rowskip = atoi(env);  // tuning A/B
+                  (const uint8_t*)d_masks, (uint32_t*)d_rng, fr ? 0 : 2, 0u};
     a.quick_masks = (const uint8_t*)d_quick;
     a.forced = (const int32_t*)d_forced;
     a.stop_out = d_stop;
@@ -5098,7 +5017,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
     // 60.2 M playouts/s (profiles/r03/sweeps/handout.jsonl).  The frontier-order kernels
     // keep 0 (22.4 vs 21.5 M: their playout lengths vary more).  Results depend only on the
     // playout id, not on the slot (tests/test_gpu_parity.py slot independence).
-    if (const char* env = getenv("BK_HANDOUT")) a.handout = atoi(env);  // tuning override
+    a.handout = (int)tune_or(h, BK_TUNE_HANDOUT, a.handout);
     if (a.handout < 0 || a.handout > 2) a.handout = 0;
     {
         const int64_t rest = (int64_t)n_playouts - (int64_t)nslots;
@@ -5353,6 +5272,7 @@ int bk_debug_fastmcts_select(bk_handle h, int32_t n, const uint32_t* visits, con
     for (int32_t j = 0; j < n; ++j)
         if (visits[j] == 0) return set_err(h, BK_EINVAL, "bk_debug_fastmcts_select: visits must be > 0%s", "");
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_debug_fastmcts_select");
     const size_t bv = sizeof(uint32_t) * n, bt = sizeof(double) * n, bo = sizeof(int32_t) * (size_t)(pow_fix_rows + 1),
                  be = sizeof(int32_t) * (size_t)(pow_fix_len + 1);
     int rc = grow(h, &h->d_aux, &h->d_aux_cap, bt + bv + bo + be + 64);
@@ -5388,6 +5308,7 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
         return set_err(h, BK_EINVAL, "bk_fastmcts: pow_fix_entries missing%s", "");
     if (n_games == 0) return BK_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_fastmcts");
     const size_t b_off = sizeof(int32_t) * (size_t)(n_games + 1), b_it = sizeof(int32_t) * (size_t)n_games,
                  b_base = sizeof(double) * (size_t)n_games, b_mt = sizeof(uint32_t) * 625 * (size_t)n_games,
                  b_log = sizeof(double) * (size_t)log_len, b_out = sizeof(bk_fastmcts_out) * (size_t)n_games,
@@ -5489,6 +5410,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         }
     }
     HIPCHK(h, hipSetDevice(h->device));
+    BK_IDLE(h, "bk_mcts");
     const size_t n = (size_t)n_games, ttc = cfg->use_tt ? (size_t)cfg->tt_cap : 0;
     const size_t it = (size_t)cfg->iterations;
     struct Sec { const void* host; size_t bytes; int dir; void* dev; };  // dir: 1 in, 2 out, 3 in+out
@@ -5547,20 +5469,20 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     // (k_mcts_h 1.88 s flat vs k_mcts_coop_h 1.33 s at 64 per CU, 2.61 s at 128) --
     // config 4 with 8,192 games on one GPU searches 8,192 at once: 164 -> 242 games/s
     bool coop = (int64_t)n_games <= (heur ? 80 : 40) * (int64_t)h->num_cu;
-    if (const char* env = getenv("BK_MCTS_COOP")) coop = atoi(env) != 0;  // tuning / test override
+    coop = tune_or(h, BK_TUNE_MCTS_COOP, coop ? 1 : 0) != 0;
     const int blk = coop ? COOP_WAVES * WAVE : heur ? HBLOCK : BLOCK;
     // k_mcts_coop(_h) blocks (of COOP_WAVES searches) per CU: all the waves the registers
     // allow (k_mcts_coop 225 VGPRs: 2 per SIMD, twice the throughput of 1 --
     // profiles/r03/coopblocks; k_mcts_coop_h 404: 1)
     int coop_bpc = heur ? 2 : 4;
-    if (const char* env = getenv("BK_COOP_BLOCKS_PER_CU")) coop_bpc = atoi(env) > 0 ? atoi(env) : coop_bpc;  // tuning
+    if (tune_or(h, BK_TUNE_COOP_BLOCKS_PER_CU, 0) > 0) coop_bpc = (int)h->tune[BK_TUNE_COOP_BLOCKS_PER_CU];
     int blocks = h->num_cu * (coop ? coop_bpc : heur ? 3 : h->mcts_blocks_per_cu);
     // k_mcts is latency-bound at one wave per SIMD (config 5: 65,536 searches fill one
     // 256-lane block per CU): when the resident slots allow, every other lane takes a
     // search, so twice the waves hide each other's latency (11.14 vs 10.84 M sims/s,
     // profiles/r03/sweeps/mcts_spread.jsonl; 4 measured slower)
     int spread = (!heur && !coop && (int64_t)n_games * 2 <= (int64_t)blocks * blk) ? 2 : 1;
-    if (const char* env = getenv("BK_MCTS_SPREAD")) spread = atoi(env);  // tuning override
+    spread = (int)tune_or(h, BK_TUNE_MCTS_SPREAD, spread);
     if (spread < 1 || spread > WAVE || (spread & (spread - 1)) || coop) spread = 1;
     const int per_block = coop ? COOP_WAVES : blk;  // searches a block holds at once
     const int need = (int)(((int64_t)n_games * spread + per_block - 1) / per_block);
@@ -5579,7 +5501,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     // a waiting lane waits at most one simulation of the others (2x)
     const uint64_t steps = 2 * per_lane * ((uint64_t)cfg->iterations + 1) * ((uint64_t)cfg->max_rollout_moves + 2) + 64;
     int32_t tree_batch = MC_TREE_BATCH;
-    if (const char* env = getenv("BK_TREE_BATCH")) tree_batch = atoi(env);  // tuning override
+    tree_batch = (int32_t)tune_or(h, BK_TUNE_TREE_BATCH, tree_batch);
     if (tree_batch < 1) tree_batch = 1;
     MctsArgs a{(const bk_state*)sec[0].dev, (const bk_fset*)sec[1].dev, (const uint8_t*)sec[2].dev,
                (const uint64_t*)sec[3].dev, n_games, *cfg, (const uint64_t*)sec[4].dev,
@@ -5588,11 +5510,10 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1, 1};
-    if (const char* env = getenv("BK_COOP_WALK")) a.coop_walk = atoi(env);  // tuning / test override
-    if (const char* env = getenv("BK_COOP_BAL")) a.coop_balanced = atoi(env);  // tuning / test override
+    a.coop_walk = (int)tune_or(h, BK_TUNE_COOP_WALK, a.coop_walk);
+    a.coop_balanced = (int)tune_or(h, BK_TUNE_COOP_BAL, a.coop_balanced);
     // spread 2: the idle odd lane of each pair splits the even lane's stencil (k_mcts_pair)
-    bool pair = true;
-    if (const char* env = getenv("BK_MCTS_PAIR")) pair = atoi(env) != 0;  // tuning / test override
+    const bool pair = tune_or(h, BK_TUNE_MCTS_PAIR, 1) != 0;
     HIPCHK(h, hipEventRecord(h->ev0, h->cur));
     if (coop && heur) {
         h->last_kernel = "k_mcts_coop_h";
@@ -5613,7 +5534,11 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev1, h->cur));
     h->timed = true;
-    if (mem == BK_MEM_DEVICE && (cfg->flags & BK_MCTS_ASYNC)) return BK_OK;  // errors: bk_synchronize
+    if (mem == BK_MEM_DEVICE && (cfg->flags & BK_MCTS_ASYNC)) {  // errors: bk_synchronize
+        h->busy = true;  // the running search owns the scratch until then
+        h->busy_stream = h->cur;
+        return BK_OK;
+    }
     uint32_t ctr[4];
     if (mem == BK_MEM_HOST) {
         for (int i = 0; i < NSEC; ++i)

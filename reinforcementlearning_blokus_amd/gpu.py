@@ -64,6 +64,13 @@ class BlokusGPU:
         iteration guard or read a bad root_index (bk_synchronize)."""
         self.handle.synchronize()
 
+    def tune(self, **overrides):
+        """Set tuning / test overrides of this handle by their environment-variable names
+        without the BK_ prefix (tune(MCTS_COOP=1, COOP_BAL=None); None = automatic).  The
+        library reads the environment once per handle, at creation (bk_set_tuning)."""
+        for k, v in overrides.items():
+            self.handle.set_tuning("BK_" + k, v)
+
     def _check_playout_tensors(self, roots, n_playouts, root_index, compat_seeds, out, rng):
         import torch
         _check_device_tensor(roots, "roots", torch.uint8, (roots.shape[0], 256), self.device)

@@ -164,12 +164,14 @@ def test_device_iteration_guard_is_reported(gpu, monkeypatch):
     import torch
     roots = pack_many([replay(POS[8])])
     droots = torch.from_numpy(roots.view(np.uint8).reshape(-1, 256).copy()).cuda()
-    monkeypatch.setenv("BK_DEBUG_MAX_ITERS", "3")
-    gpu.rollout(droots, 512, seed=2)
-    with pytest.raises(RuntimeError, match="guard"):
-        gpu.synchronize()
-    with pytest.raises(RuntimeError, match="guard"):  # the host path reports it at once
-        gpu.rollout(roots, 512, seed=2)
-    monkeypatch.delenv("BK_DEBUG_MAX_ITERS")
+    gpu.tune(DEBUG_MAX_ITERS=3)
+    try:
+        gpu.rollout(droots, 512, seed=2)
+        with pytest.raises(RuntimeError, match="guard"):
+            gpu.synchronize()
+        with pytest.raises(RuntimeError, match="guard"):  # the host path reports it at once
+            gpu.rollout(roots, 512, seed=2)
+    finally:
+        gpu.tune(DEBUG_MAX_ITERS=None)
     gpu.rollout(droots, 512, seed=2)
     gpu.synchronize()

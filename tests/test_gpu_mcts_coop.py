@@ -26,9 +26,10 @@ def _run(gpu, roots, sets, iters, policy, max_roll, coop, monkeypatch, seed0=100
     from reinforcementlearning_blokus_amd.gpu import MctsTT
     from reinforcementlearning_blokus_amd.mcts.zobrist import ZobristHash, flat_keys, hash_states
     from reinforcementlearning_blokus_amd.workloads import numpy_mt_states
-    monkeypatch.setenv("BK_MCTS_COOP", "1" if coop else "0")
-    for k, v in (env or {}).items():
-        monkeypatch.setenv(k, v)
+    # the handle's overrides (bk_set_tuning; the library reads the environment only when
+    # a handle is created)
+    gpu.tune(MCTS_COOP=1 if coop else 0, MCTS_SPREAD=None, MCTS_PAIR=None, COOP_BAL=None, COOP_WALK=None)
+    gpu.tune(**{k[3:]: int(v) for k, v in (env or {}).items()})
     n = len(roots)
     zob = np.stack([flat_keys(ZobristHash(seed=t)) for t in range(3)])
     zi = (np.arange(n) % 3).astype(np.int32)

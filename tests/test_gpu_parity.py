@@ -64,8 +64,11 @@ def test_movegen_orientation_groups_equal(gpu, groups, monkeypatch):
     st = pack_many(boards)
     players = np.array([b.cur for b in boards], dtype=np.uint8)
     cnt0, rows0 = gpu.movegen(st, players)
-    monkeypatch.setenv("BK_MG_GROUPS", str(groups))
-    cnt, rows = gpu.movegen(st, players)
+    gpu.tune(MG_GROUPS=groups)
+    try:
+        cnt, rows = gpu.movegen(st, players)
+    finally:
+        gpu.tune(MG_GROUPS=None)
     assert np.array_equal(cnt, cnt0) and np.array_equal(rows, rows0)
     for i in range(0, 300, 29):
         assert int(cnt[i]) == len(O.legal_moves(boards[i], boards[i].cur, O.ORDER_NAIVE))
@@ -198,19 +201,21 @@ def test_movegen_mask_staged_equals_per_lane_stores(gpu, monkeypatch, groups, pa
     groups / parts waves each, at least 1 and at most 8) writes the same masks and counts as
     k_movegen_m's per-lane stores (BK_MG_STAGE=0), for ragged sizes; the launch names the
     staged kernel."""
-    monkeypatch.setenv("BK_MG_GROUPS", groups)
-    monkeypatch.setenv("BK_MG_PARTS", parts)
-    for n in (1, 70, 600):
-        boards = oracle_states(n, seed0=7100 + n)
-        st = pack_many(boards)
-        players = np.array([b.cur for b in boards], dtype=np.uint8)
-        monkeypatch.setenv("BK_MG_STAGE", "1")
-        c1, m1 = gpu.movegen_mask(st, players)
-        assert gpu.last_kernel() == "k_movegen_ml" + parts
-        monkeypatch.setenv("BK_MG_STAGE", "0")
-        c0, m0 = gpu.movegen_mask(st, players)
-        assert gpu.last_kernel() == "k_movegen_m"
-        assert np.array_equal(c1, c0) and np.array_equal(m1, m0), n
+    gpu.tune(MG_GROUPS=int(groups), MG_PARTS=int(parts))
+    try:
+        for n in (1, 70, 600):
+            boards = oracle_states(n, seed0=7100 + n)
+            st = pack_many(boards)
+            players = np.array([b.cur for b in boards], dtype=np.uint8)
+            gpu.tune(MG_STAGE=1)
+            c1, m1 = gpu.movegen_mask(st, players)
+            assert gpu.last_kernel() == "k_movegen_ml" + parts
+            gpu.tune(MG_STAGE=0)
+            c0, m0 = gpu.movegen_mask(st, players)
+            assert gpu.last_kernel() == "k_movegen_m"
+            assert np.array_equal(c1, c0) and np.array_equal(m1, m0), n
+    finally:
+        gpu.tune(MG_GROUPS=None, MG_PARTS=None, MG_STAGE=None)
 
 
 @pytest.mark.parametrize("stage", ["1", "0"])
@@ -220,7 +225,15 @@ def test_movegen_mask_staged_odd_word_output(gpu, monkeypatch, stage):
     16-byte stores shift to that parity, the masks equal the aligned call's and the words
     either side stay untouched."""
     import torch
-    monkeypatch.setenv("BK_MG_STAGE", stage)
+    gpu.tune(MG_STAGE=int(stage))
+    try:
+        _odd_word_output(gpu, stage)
+    finally:
+        gpu.tune(MG_STAGE=None)
+
+
+def _odd_word_output(gpu, stage):
+    import torch
     from reinforcementlearning_blokus_amd import _native as N
     n = 130
     boards = oracle_states(n, seed0=7300)

@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bk_abi_version() == N.ABI_VERSION == 4
+    assert lib.bk_abi_version() == N.ABI_VERSION == 5
     assert lib.bk_tables_version() >= 1
 
 
@@ -46,6 +46,26 @@ def test_invalid_arguments_rejected_without_gpu():
     lib = N.load()
     assert lib.bk_destroy(None) == N.EINVAL
     assert lib.bk_orient_info(91, None, None, None, None) == N.EINVAL
+    assert lib.bk_set_tuning(None, 0, 1) == N.EINVAL
+    assert lib.bk_get_tuning(None, 0, None) == N.EINVAL
+
+
+def test_environment_read_only_at_handle_creation():
+    """the library reads its BK_* tuning variables once, in bk_create
+    (into the handle; bk_set_tuning changes them), never inside an entry point -- a stray
+    variable cannot change a running caller's kernel choice.  Checked on the source: the
+    only getenv calls sit in bk_create."""
+    src = open(os.path.join(ROOT, "reinforcementlearning_blokus_amd", "csrc", "blokus_kernels.hip")).read()
+    create = src.index("int bk_create(")
+    create_end = src.index("\nint bk_destroy(", create)
+    calls = [m.start() for m in re.finditer(r"\bgetenv\s*\(", src)]
+    assert calls and all(create < c < create_end for c in calls), calls
+    # the header's tuning keys and the binding's names agree, in order
+    hdr = open(os.path.join(ROOT, "include", "blokus_hip.h")).read()
+    keys = re.findall(r"^\s*BK_TUNE_(\w+)\s*(?:=\s*0)?,", hdr, flags=re.M)
+    assert ["BK_" + k for k in keys] == list(N.TUNE_KEYS), keys
+    names = re.findall(r'"(BK_\w+)"', src[src.index("kTuneNames"):src.index("};", src.index("kTuneNames"))])
+    assert names == list(N.TUNE_KEYS)
 
 
 def test_gpu_free_container_fails_loudly():

@@ -107,14 +107,6 @@ def render_classes(table):
         rows += classes[k]
         i += n
     lines.append("")
-    # the same entries with everything literal (tuning variant BK_STENCIL_LITERAL):
-    # X(piece, g, height, code0, code1, ...) with code = t | column shift << 8
-    lines.append("#define BK_ENTRY_LIST(X) \\")
-    for k in order:
-        for w0, w1 in classes[k]:
-            codes = [t | ((((w1 >> (3 * (j - 1))) & 7) if j > 0 else 0) << 8) for j, t in enumerate(k[1])]
-            lines.append(f"    X({w0 & 0xFF}, {w0 >> 8}, {k[0]}, {', '.join(str(c) for c in codes)}) \\")
-    lines.append("")
     lines.append("#define BK_CLASS_TABLE_INIT { \\")
     for w0, w1 in rows:
         lines.append(f"    {{{hex(w0)}, {hex(w1)}}}, \\")
