@@ -79,6 +79,8 @@ def parse(argv=None):
                          "(MCTSAgent's default rollout agent)")
     ap.add_argument("--boards", type=int, default=4096, help="config2 boards")
     ap.add_argument("--all-players", action="store_true", help="config2: all 4 players of every board")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="config2: launch every step from the host instead of replaying a captured hipGraph")
     ap.add_argument("--root-plies", type=int, default=20)
     ap.add_argument("--seed", type=int, default=20260301)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
@@ -802,16 +804,41 @@ def run_config2(args, world, rank, local, dist):
     n = len(st)
     states = torch.from_numpy(st.view(np.uint8).reshape(n, 256).copy()).to(dev)
     players = torch.from_numpy(pl.copy()).to(dev)
+    from reinforcementlearning_blokus_amd import _native as N
     stream = torch.cuda.Stream(dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    masks = torch.empty((n, N.N_ORIENTS, 7), dtype=torch.int64, device=dev)
+
+    def step():  # one bk_movegen_mask launch into the preallocated outputs
+        gpu._stream_from_torch()
+        gpu.handle.movegen_mask(states.data_ptr(), players.data_ptr(), n, masks.data_ptr(), cnt.data_ptr(),
+                                N.MEM_DEVICE)
+
+    # A step is a ~16 us kernel; launched one by one from Python (ctypes, memset, launch:
+    # ~25 us of host time per step) the GPU waits on the host.  The steps are captured
+    # into a hipGraph of `per` launches instead (every step still runs the whole batch),
+    # and the timed region replays it (--no-graph: one launch per step from the host).
+    per = 1 if args.no_graph else max(d for d in range(1, min(10, args.steps) + 1) if args.steps % d == 0)
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):
-            cnt, masks = gpu.movegen_mask(states, players)
+            step()
+        graph = None
+        if not args.no_graph:
+            stream.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                for _ in range(per):
+                    step()
+            graph.replay()  # one untimed replay
         barrier_sync(dist)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record(stream)
-        for _ in range(args.steps):
-            cnt, masks = gpu.movegen_mask(states, players)
+        for _ in range(args.steps // per):
+            if graph is not None:
+                graph.replay()
+            else:
+                step()
         e1.record(stream)
         barrier_sync(dist)
         elapsed = time.perf_counter() - t0
@@ -834,6 +861,7 @@ def run_config2(args, world, rank, local, dist):
                                "masks, 91 x 7 u64 per board-player, + counts (bk_movegen_mask)",
                    "boards": nb, "board_players": n,
                    "legal_moves_per_board_player": moves / n, "us_per_batch": kernel_ms * 1e3,
+                   "launch": "host launch per step" if graph is None else f"hipGraph replays of {per} launches",
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,

@@ -423,6 +423,10 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
     seat_kind = np.zeros((len(idx), 4), np.int8)  # 0 random/heuristic, 1 mcts, 2 fast
     for i, gi in enumerate(idx):
         st = seats_of[i]
+        # RunConfig holds exactly 4 distinct agents (arena_runner.py:125-200), so an agent
+        # plays one seat of a game and searches at most once per piece: the device TT
+        # capacity below relies on it
+        assert len({st[str(p + 1)] for p in range(4)}) == 4, st
         done: Dict[str, Tuple[int, int]] = {}
         for p in range(4):
             name = st[str(p + 1)]
@@ -475,7 +479,7 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
     import torch
 
     from .. import _native as N
-    from ..gpu import BlokusGPU
+    from ..gpu import BlokusGPU, mcts_node_cap
     os.makedirs(capture_dir, exist_ok=True)
     base = os.path.join(capture_dir, f"mcts_fail_job{job['seq']}")
     cap = job["cap"]
@@ -485,7 +489,9 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
     n = cap["roots"].shape[0]
     bad_idx = np.flatnonzero(bad)
     arrs = {k: v.cpu().numpy() for k, v in cap.items()}
-    arrs.update(out=job["o_d"].cpu().numpy(), nodes_bad=job["nodes"][bad_idx].cpu().numpy(), bad_idx=bad_idx,
+    if job["nodes"] is not None:
+        arrs["nodes_bad"] = job["nodes"][bad_idx].cpu().numpy()
+    arrs.update(out=job["o_d"].cpu().numpy(), bad_idx=bad_idx,
                 games=np.asarray(job["games"]), aid=np.asarray(job["aid"]),
                 zob=zob_d.index_select(0, cap["zidx"].long()).cpu().numpy(),
                 key=np.array([iters, roll, use_tt, policy], np.int64), c=np.array([c]))
@@ -498,8 +504,8 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
         st.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(st):
             pick = lambda t: t.index_select(0, s).contiguous()  # noqa: E731
-            nodes = pick(job["nodes"]) if dirty else torch.zeros((k, job["nodes"].shape[1]), dtype=torch.uint8,
-                                                                 device=dev)
+            width = mcts_node_cap(iters) * N.MCTS_NODE_DTYPE.itemsize
+            nodes = pick(job["nodes"]) if dirty else torch.zeros((k, width), dtype=torch.uint8, device=dev)
             out = torch.zeros((k, N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
             tt = (pick(cap["ttk"]), pick(cap["ttv"]), pick(cap["ttc"])) if use_tt else (None, None, None)
             g.mcts_device(pick(cap["roots"]), pick(cap["sets"]), pick(cap["players"]), None, zob_d,
@@ -515,8 +521,10 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
     report = {"seq": job["seq"], "n": int(n), "bad_idx": bad_idx.tolist(), "slot": job["slot"],
               "inflight_at_launch": job["inflight_at_launch"], "key": [iters, roll, c, use_tt, policy],
               "orig_status": orig["status"][bad_idx].tolist()}
-    for name, sel, dirty in (("whole", np.arange(n), False), ("bad_alone", bad_idx, False),
-                             ("whole_dirty_pool", np.arange(n), True)):
+    runs = [("whole", np.arange(n), False), ("bad_alone", bad_idx, False)]
+    if job["nodes"] is not None:
+        runs.append(("whole_dirty_pool", np.arange(n), True))
+    for name, sel, dirty in runs:
         r, kname = replay(sel, dirty)
         arrs["replay_" + name] = r.view(np.uint8)
         ref = orig[sel]
@@ -637,6 +645,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     # BK_ARENA_CAPTURE=<dir> (diagnostics): keep every search launch's inputs; a launch
     # that returns a failed search is saved there and replayed alone (_capture_failed_job)
     capture_dir = os.environ.get("BK_ARENA_CAPTURE", "")
+    drop_nodes = os.environ.get("BK_ARENA_DROP_NODES", "0") != "0"  # A/B of the round-4 lifetime (diagnostics)
     fast_eng = BlokusGPU(device) if pipeline else gpu
     inflight = np.zeros(n, bool)
 
@@ -683,7 +692,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         inflight[games] = True
         # nodes stays referenced until the job is finished: the launch is asynchronous
         jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done,
-                     "t0": time.perf_counter(), "nodes": nodes, "cap": cap_in, "seq": tl["mcts_jobs_launched"],
+                     "t0": time.perf_counter(), "nodes": None if drop_nodes else nodes, "cap": cap_in, "seq": tl["mcts_jobs_launched"],
                      "key": (iters, roll, c, use_tt, policy), "inflight_at_launch": len(jobs)})
         tl["mcts_jobs_launched"] += 1
         if not pipeline:
@@ -737,6 +746,10 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         move on the device (FastMCTSAgent: quick move below 5 iterations, else the best
         child, else index 0), so the next step places it with no host round trip."""
         k = len(games)
+        if int(np.max(nl)) > N.FASTMCTS_MAX_CHILDREN:  # k_fastmcts would leave the output unset
+            g = int(games[int(np.argmax(nl))])
+            raise RuntimeError(f"game {idx[g]}: a FastMCTS root with {int(np.max(nl))} legal moves, more than "
+                               f"bk_fastmcts supports ({N.FASTMCTS_MAX_CHILDREN})")
         need = max(counts) + 1
         if need not in fast_tabs:
             lt = _log_table(need)
@@ -753,7 +766,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         base = st[:, 8:16].contiguous().view(torch.float64).reshape(k)
         quick_i = st[:, 4:8].contiguous().view(torch.int32).reshape(k)
         mt_g = mtf_d.index_select(0, a_d).contiguous()
-        o = torch.empty((k, N.FASTMCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        o = torch.zeros((k, N.FASTMCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
         fast_eng.fastmcts_device(off_d, it_d, base, mt_g, lt_d, fo_d, fe_d, ce, o)
         mtf_d.index_copy_(0, a_d, mt_g)
         w = o[:, :12].contiguous().view(torch.int32)  # best_index, iterations, n_children

@@ -2146,6 +2146,7 @@ __device__ __forceinline__ void heur_walk_frontier(int gs, const uint32_t (&ok)[
 // BK_STATUS_STOP (32, include/blokus_hip.h): bk_arena_advance stopped at a stop seat
 #define BK_STICKY_GUARD 1u  // a persistent kernel's iteration guard tripped: results incomplete
 #define BK_STICKY_ROOT 2u   // a root_index entry outside [0, n_roots)
+#define BK_STICKY_FASTMCTS 4u  // k_fastmcts: a root with too many children or a short log table
 
 struct RolloutArgs {
     const bk_state* roots;
@@ -2724,7 +2725,12 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         if constexpr (HEUR) {
             if (forced) {
                 fmove = !(g.forced & BK_FORCE_INDEX);
-                const bool bad = total == 0u || (fmove ? (g.forced / 400 >= BK_NUM_ORIENTS) : gs < 0);
+                // a move int must name an orientation of a piece the mover still holds (the
+                // anchor's legality is checked against the orientation's legal set below)
+                const int fg = g.forced / 400;
+                const bool bad = total == 0u ||
+                                 (fmove ? (fg >= BK_NUM_ORIENTS || !((avail >> ((kInfo[fg] & 0xFFu) - 1u)) & 1u))
+                                        : gs < 0);
                 if (bad) {
                     g.status |= BK_STATUS_BADFORCE;
                     finish_game<FR>(a, g, slab, slot);
@@ -2986,7 +2992,7 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
     for (int k = lane; k < n && k < BK_FASTMCTS_MAX_CHILDREN; k += WAVE) { visits[k] = 0; total[k] = 0.0; }
     __syncthreads();
     if (n > BK_FASTMCTS_MAX_CHILDREN || iters >= a.log_len) {
-        if (lane == 0) atomicOr(a.err, 1u);
+        if (lane == 0) { atomicOr(a.err, 1u); atomicOr(a.err + 1, BK_STICKY_FASTMCTS); }
         return;
     }
     int nch = 0;
@@ -4492,6 +4498,7 @@ struct bk_handle_s {
     // an asynchronous bk_mcts search is running on `busy_stream` with this handle's scratch
     bool busy = false;
     hipStream_t busy_stream = nullptr;
+    bool capturing = false;  // the current launch goes into a graph being captured (untimed)
 };
 
 static const char* const kTuneNames[BK_TUNE_COUNT] = {
@@ -4660,6 +4667,9 @@ int bk_synchronize(bk_handle h) {
         HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof sticky));
         if (sticky & BK_STICKY_GUARD)
             return set_err(h, BK_EOVERFLOW, "device-path launch: iteration guard tripped, results incomplete%s", "");
+        if (sticky & BK_STICKY_FASTMCTS)
+            return set_err(h, BK_EINVAL, "device-path bk_fastmcts: a root with more than BK_FASTMCTS_MAX_CHILDREN "
+                                         "children or iterations past the log table (its output is not set)%s", "");
         return set_err(h, BK_EINVAL, "device-path launch: root_index entry outside [0, n_roots)%s", "");
     }
     return BK_OK;
@@ -4711,6 +4721,23 @@ int bk_last_kernel_ms(bk_handle h, float* ms) {
     return BK_OK;
 }
 
+// HIP events around a launch (bk_last_kernel_ms).  Not while the stream is being captured
+// into a graph (hipStreamBeginCapture: the caller times the graph's replays itself): the
+// launches then go into the graph untimed, and bk_last_kernel_ms reports the last timed one.
+static hipError_t mark_start(bk_handle h) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(h->cur, &st);
+    if (e != hipSuccess) return e;
+    h->capturing = st != hipStreamCaptureStatusNone;
+    return h->capturing ? hipSuccess : hipEventRecord(h->ev0, h->cur);
+}
+static hipError_t mark_end(bk_handle h) {
+    if (h->capturing) return hipSuccess;
+    const hipError_t e = hipEventRecord(h->ev1, h->cur);
+    if (e == hipSuccess) h->timed = true;
+    return e;
+}
+
 static int stage_in(bk_handle h, const void* src, size_t bytes, int mem, void** dev, void** buf, size_t* cap) {
     if (mem == BK_MEM_DEVICE) { *dev = const_cast<void*>(src); return BK_OK; }
     int rc = grow(h, buf, cap, bytes);
@@ -4760,12 +4787,11 @@ int bk_movegen(bk_handle h, const bk_state* states, const uint8_t* players, int3
     MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, d_rows, d_count, nullptr, groups, nullptr};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
     const int grid = waves * groups;
-    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    HIPCHK(h, mark_start(h));
     h->last_kernel = "k_movegen_g";
     hipLaunchKernelGGL(k_movegen_g, dim3(grid), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
-    h->timed = true;
+    HIPCHK(h, mark_end(h));
     if (mem == BK_MEM_HOST) {
         if (out_count) HIPCHK(h, hipMemcpyAsync(out_count, d_count, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, h->cur));
         if (out_rows) HIPCHK(h, hipMemcpyAsync(out_rows, d_rows, rows_bytes, hipMemcpyDeviceToHost, h->cur));
@@ -4808,7 +4834,7 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
     const int sets = ((waves + MG_XCDS - 1) / MG_XCDS) * MG_XCDS;
     MovegenArgs a{(const bk_state*)d_states, (const uint8_t*)d_players, n, nullptr, d_count, nullptr, groups, d_mask};
     if (d_count) HIPCHK(h, hipMemsetAsync(d_count, 0, sizeof(uint32_t) * (size_t)n, h->cur));  // atomics add in
-    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    HIPCHK(h, mark_start(h));
     // LDS-staged whole-line writes (k_movegen_ml): the groups' waves split over MG_PARTS
     // orientation ranges of one set each; BK_MG_STAGE=0 keeps the per-lane stores
     bool staged = out_mask != nullptr;
@@ -4845,8 +4871,7 @@ int bk_movegen_mask(bk_handle h, const bk_state* states, const uint8_t* players,
         hipLaunchKernelGGL(k_movegen_m, dim3(sets * groups), dim3(WAVE), 0, h->cur, a);
     }
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
-    h->timed = true;
+    HIPCHK(h, mark_end(h));
     if (mem == BK_MEM_HOST) {
         if (out_count) HIPCHK(h, hipMemcpyAsync(out_count, d_count, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, h->cur));
         if (out_mask) HIPCHK(h, hipMemcpyAsync(out_mask, d_mask, mask_bytes, hipMemcpyDeviceToHost, h->cur));
@@ -4871,12 +4896,11 @@ int bk_has_moves(bk_handle h, const bk_state* states, int32_t n, uint8_t* out_ma
         d_mask = (uint8_t*)h->d_out;
     }
     MovegenArgs a{(const bk_state*)d_states, nullptr, n, nullptr, nullptr, d_mask, 0, nullptr};
-    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    HIPCHK(h, mark_start(h));
     h->last_kernel = "k_has_moves";
     hipLaunchKernelGGL(k_has_moves, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
-    h->timed = true;
+    HIPCHK(h, mark_end(h));
     if (mem == BK_MEM_HOST) {
         HIPCHK(h, hipMemcpyAsync(out_mask4, d_mask, (size_t)n, hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipStreamSynchronize(h->cur));
@@ -5024,7 +5048,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         int64_t ls = rest <= 0 ? 0 : rest >= (int64_t)nslots ? (int64_t)nslots : ((rest + WAVE - 1) / WAVE) * WAVE;
         a.long_slots = (uint32_t)ls;
     }
-    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    HIPCHK(h, mark_start(h));
     if (heur) {
         h->last_kernel = "k_rollout_fr_h";
         hipLaunchKernelGGL(k_rollout_fr_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
@@ -5039,8 +5063,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         hipLaunchKernelGGL(k_rollout, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     }
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
-    h->timed = true;
+    HIPCHK(h, mark_end(h));
     if (mem == BK_MEM_HOST) {
         if (out)
             HIPCHK(h, hipMemcpyAsync(out, d_out, sizeof(bk_result) * (size_t)n_playouts, hipMemcpyDeviceToHost, h->cur));
@@ -5359,12 +5382,11 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
     FastMctsArgs a{n_games, d_off, d_it, d_base, d_mt, d_log, log_len, PowFix{d_fo, d_fe, pow_fix_rows}, exploration,
                    d_out, d_vis,
                    h->d_counter + 1};
-    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    HIPCHK(h, mark_start(h));
     h->last_kernel = "k_fastmcts";
     hipLaunchKernelGGL(k_fastmcts, dim3(n_games), dim3(WAVE), 0, h->cur, a);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
-    h->timed = true;
+    HIPCHK(h, mark_end(h));
     if (mem == BK_MEM_HOST) {
         uint32_t ctr[4];
         HIPCHK(h, hipMemcpyAsync(out, d_out, b_out, hipMemcpyDeviceToHost, h->cur));
@@ -5374,6 +5396,7 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
                                      hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipStreamSynchronize(h->cur));
+        if (ctr[2]) HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof(uint32_t)));  // reported here
         if (ctr[1]) return set_err(h, BK_EINVAL, "bk_fastmcts: too many children or log table too short%s", "");
     }
     return BK_OK;
@@ -5514,7 +5537,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     a.coop_balanced = (int)tune_or(h, BK_TUNE_COOP_BAL, a.coop_balanced);
     // spread 2: the idle odd lane of each pair splits the even lane's stencil (k_mcts_pair)
     const bool pair = tune_or(h, BK_TUNE_MCTS_PAIR, 1) != 0;
-    HIPCHK(h, hipEventRecord(h->ev0, h->cur));
+    HIPCHK(h, mark_start(h));
     if (coop && heur) {
         h->last_kernel = "k_mcts_coop_h";
         hipLaunchKernelGGL(k_mcts_coop_h, dim3(blocks), dim3(blk), 0, h->cur, a);
@@ -5532,8 +5555,7 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         hipLaunchKernelGGL(k_mcts, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     }
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->ev1, h->cur));
-    h->timed = true;
+    HIPCHK(h, mark_end(h));
     if (mem == BK_MEM_DEVICE && (cfg->flags & BK_MCTS_ASYNC)) {  // errors: bk_synchronize
         h->busy = true;  // the running search owns the scratch until then
         h->busy_stream = h->cur;

@@ -180,7 +180,8 @@ def test_device_driver_equals_host_staged_batches(monkeypatch, seed, policy, str
     agent streams stay in HBM; search moves go back as forced moves, FastMCTS inputs come
     from the kernel's stop info) against the host-staged rounds (BK_ARENA_DEVICE=0): every
     record field and the search agents' simulation counts equal, game by game, on mixed
-    seats that include an agent playing two seats.  streams: the MCTS searches in flight
+    seats (RunConfig takes exactly 4 distinct agents, so each plays one seat of a game;
+    _device_agents asserts it).  streams: the MCTS searches in flight
     on that many streams while the other games play on (BK_ARENA_MCTS_STREAMS), or "0",
     one search at a time waited for at once (BK_ARENA_PIPELINE=0)."""
     from reinforcementlearning_blokus_amd.arena.runner import run_games_batched

@@ -254,3 +254,42 @@ def _odd_word_output(gpu, stage):
     assert b[0] == -7 and b[-1] == -7
     assert np.array_equal(b[1:-1].view(np.uint64).reshape(n, N.N_ORIENTS, 7), ref)
     assert np.array_equal(cd.cpu().numpy().astype(np.uint32), cnt)
+
+
+def test_movegen_mask_graph_replay_equals_eager(gpu):
+    """bench.py config 2 captures its bk_movegen_mask launches into a hipGraph (the
+    library skips its timing events on a capturing stream) and replays it: the replayed
+    masks and counts equal an eager call's, and a replay after the inputs change
+    recomputes from the new inputs (the graph holds the launch, not its results)."""
+    import torch
+    from reinforcementlearning_blokus_amd import _native as N
+    n = 333
+    boards = oracle_states(2 * n, seed0=7700)
+    st = pack_many(boards)
+    players = np.array([b.cur for b in boards], dtype=np.uint8)
+    c_ref, m_ref = gpu.movegen_mask(st, players)
+    dev = torch.device("cuda", 0)
+    sd = torch.from_numpy(st[:n].view(np.uint8).reshape(n, 256).copy()).to(dev)
+    pd = torch.from_numpy(players[:n].copy()).to(dev)
+    cnt = torch.empty(n, dtype=torch.int32, device=dev)
+    masks = torch.zeros((n, N.N_ORIENTS, 7), dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(dev)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(stream):
+        gpu._stream_from_torch()
+        gpu.handle.movegen_mask(sd.data_ptr(), pd.data_ptr(), n, masks.data_ptr(), cnt.data_ptr(), N.MEM_DEVICE)
+        stream.synchronize()
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(2):
+                gpu._stream_from_torch()
+                gpu.handle.movegen_mask(sd.data_ptr(), pd.data_ptr(), n, masks.data_ptr(), cnt.data_ptr(),
+                                        N.MEM_DEVICE)
+    for half in (0, 1):
+        sd.copy_(torch.from_numpy(st[half * n:(half + 1) * n].view(np.uint8).reshape(n, 256).copy()))
+        pd.copy_(torch.from_numpy(players[half * n:(half + 1) * n].copy()))
+        masks.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(cnt.cpu().numpy().astype(np.uint32), c_ref[half * n:(half + 1) * n])
+        assert np.array_equal(masks.cpu().numpy().view(np.uint64), m_ref[half * n:(half + 1) * n])
+    gpu.handle.set_stream(None)
