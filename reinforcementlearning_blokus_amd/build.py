@@ -46,10 +46,21 @@ UNITS = {"host": 1, "movegen": 2, "rollout": 3, "rollout_fr": 4, "rollout_frh": 
          "mcts": 7, "mcts_pair": 8, "mcts_h": 9, "coop": 10, "coop_h": 11}
 
 
-def compile_library(out: str, defines=(), verbose: bool = True, jobs: int = 0) -> str:
+# per-unit code-generation flags (measured per kernel).  Machine LICM hoists
+# loop-invariant address and constant computations out of the persistent loops into
+# registers held for the whole kernel; without it k_rollout_fr spills 35 instead of 62
+# VGPRs (+2 % frontier-order playouts/s) and k_mcts_coop_h needs 294 instead of 355
+# registers (profiles/r05/sweeps/r05b, r05a)
+_NO_MLICM = ("-mllvm", "-disable-machine-licm")
+UNIT_FLAGS = {"rollout_fr": _NO_MLICM, "coop": _NO_MLICM, "coop_h": _NO_MLICM}
+
+
+def compile_library(out: str, defines=(), verbose: bool = True, jobs: int = 0, unit_flags=None) -> str:
     """Compile every unit of csrc/blokus_kernels.hip with hipcc (gfx950) in parallel and
     link them into `out` (one fat binary per kernel unit; kernels are launched from the
-    host unit through their host stubs)."""
+    host unit through their host stubs).  unit_flags: extra hipcc flags per unit name
+    (default UNIT_FLAGS)."""
+    unit_flags = UNIT_FLAGS if unit_flags is None else unit_flags
     from concurrent.futures import ThreadPoolExecutor
     objdir = out + ".objs"
     os.makedirs(objdir, exist_ok=True)
@@ -59,7 +70,7 @@ def compile_library(out: str, defines=(), verbose: bool = True, jobs: int = 0) -
     def unit(item):
         name, u = item
         obj = os.path.join(objdir, name + ".o")
-        cmd = base + [f"-DBK_TU={u}"]
+        cmd = base + list(unit_flags.get(name, ())) + [f"-DBK_TU={u}"]
         cmd += ["-c", "-o", obj, SRC]
         if verbose:
             print("[build] " + " ".join(cmd), flush=True)

@@ -181,7 +181,14 @@ __device__ __forceinline__ uint32_t plane_row(const uint64_t* w, int R) {
 // adds one per-lane term), rows move as dwordx4; the record stays L1/L2-resident.
 #define SLAB_FIELDS 5
 #define SLAB_RNG_BASE (SLAB_FIELDS * 20)
-#define SLAB_WORDS (SLAB_RNG_BASE + 16)
+// BK_SLAB_PAD: each lane's record starts on a 128-byte line (512-byte stride instead of
+// 464): with FsLane's padding below, frontier-order config 3 31.9 -> 33.5 M playouts/s
+// (profiles/r05/sweeps/r05b); the per-lane records of 262,144 resident lanes far exceed
+// the L2 and the Infinity Cache, so every line a ply touches is a memory round trip
+#ifndef BK_SLAB_PAD
+#define BK_SLAB_PAD 1
+#endif
+#define SLAB_WORDS (BK_SLAB_PAD ? 128 : SLAB_RNG_BASE + 16)
 struct Slab {
     uint32_t* base;  // = slab + slot * SLAB_WORDS (16-byte aligned)
     __device__ __forceinline__ uint32_t& at(int f, int R) const { return base[f * 20 + R]; }
@@ -1614,10 +1621,18 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
     return true;
 }
 
-// per-lane frontier record in the rollout kernel: the tables plus resize scratch
+// per-lane frontier record in the rollout kernel: the tables plus resize scratch.
+// BK_FSLANE_PAD: padded to whole 128-byte lines, so each player's table starts on a line
+// and a table of <= 64 slots is ONE line (2,592 -> 2,688 bytes; see BK_SLAB_PAD)
+#ifndef BK_FSLANE_PAD
+#define BK_FSLANE_PAD 1
+#endif
 struct FsLane {
     bk_fset s;
     int16_t tmp[BK_FSET_SLOTS];
+#if BK_FSLANE_PAD
+    int16_t pad[48];  // 2592 -> 2688 bytes
+#endif
 };
 
 // update_frontier_after_move (engine/board.py:315-367) of player p's table in fl for a
@@ -1719,9 +1734,14 @@ __device__ __forceinline__ bool fs_recopy_global(FsLane* fl, int q, const uint64
 // copies of copies, mcts_agent.py:113-145): from the LDS stage, the keys are re-inserted
 // straight into the global table (slots from a register bitmap), so the copy costs no
 // second record and no reads of global memory.
-template <int STAGE, bool RECOPY = false>
+struct NoMark {
+    __device__ __forceinline__ void operator()(int) const {}
+};
+
+// mark(i): section boundaries for the diagnostic build (-DBK_SECTION_PROF)
+template <int STAGE, bool RECOPY = false, typename Mark = NoMark>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
-                                               const int32_t (&cells)[5], uint64_t real) {
+                                               const int32_t (&cells)[5], uint64_t real, Mark mark = Mark()) {
     bk_fset* gfs = &fl->s;
     // BK_STAGE_EAGER: stages of <= 64 slots load all STAGE slots at once, alongside the
     // mask (the storage holds BK_FSET_SLOTS >= STAGE): one memory latency instead of the
@@ -1750,7 +1770,10 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
         uint16_t m = m0, f = f0, u = u0;
         uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab, 1, &dirty};
-        if (fs_run_ops(t, fl->tmp, cells, real)) {
+        mark(8);
+        const bool ran = fs_run_ops(t, fl->tmp, cells, real);
+        mark(9);
+        if (ran) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
             const uint32_t newsize = fs_copy_size(u);
             if (!RECOPY || (newsize - 1 == m && f == u)) {  // (a copy of a clean table is the table)
@@ -2823,9 +2846,16 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             }
             // before the table staging reuses the area
             const uint64_t real = frontier_ops(rows_lds, slab, p, (g.first >> p) & 1u, gs, ar, ac, m);
+            SECT(7);
             int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + 2 * lane;
             // (HEUR: the area holds 84 dwords per lane, a 128-slot stage fits)
-            if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real)) g.status |= 2u;
+#ifdef BK_SECTION_PROF
+            auto mark = [&](int i) { SECT(i); };
+#else
+            NoMark mark;
+#endif
+            if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real, mark))
+                g.status |= 2u;
         }
         SECT(6);
         g.cells.set(p, g.cells.get(p) + (uint32_t)n);
@@ -4098,13 +4128,10 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
     if (L < 0) { R = 0.0; gs = -1; return true; }
     gs = L + WAVE * h;
     R = cumS[gs];
-    if (h) {  // the chosen orientation's rows, from the lane that listed them
-#pragma unroll
-        for (int r = 0; r < 20; ++r) gok[r] = __shfl(ok1[r], L);
-    } else {
-#pragma unroll
-        for (int r = 0; r < 20; ++r) gok[r] = __shfl(ok0[r], L);
-    }
+    // the chosen orientation's legal rows, recomputed by every lane from the {B, C} rows
+    // (column 0: every lane's column holds the same rows): ok0 / ok1 then die once the
+    // moves are listed instead of staying live through the e pass (registers)
+    lane_ok_rows(gs, rows, gok);
     return true;
 }
 
@@ -4231,10 +4258,10 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // orientations are evaluated: locate / walk read it and the set operations run on it
     __shared__ __attribute__((aligned(16))) int16_t coop_stage[COOP_WAVES][16 * DMA_RUNS];
     const bool coop_walk_on = a.coop_walk != 0;
-    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
+    // the wave index is uniform (readfirstlane): the wave's LDS area, slab and McLane
+    // addresses live in scalar registers
+    const int lane0 = threadIdx.x & (WAVE - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     uint32_t* my = lds + wv * COOP_AREA;
-    uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
-    int16_t* lk = reinterpret_cast<int16_t*>(my) + 2 * lane;
     uint64_t* htab = reinterpret_cast<uint64_t*>(lds + COOP_AREA * COOP_WAVES);
     HeurShared* hs = reinterpret_cast<HeurShared*>(lds + COOP_AREA * COOP_WAVES + 2 * BK_CELLS);
     for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab[i] = kCellHash[i];
@@ -4250,6 +4277,14 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // scan, 3 draw + pick, 4 locate / heuristic walk, 5 frontier ops + place + expansion
     SECT_DECL
     for (uint64_t step = 0;; ++step) {
+        // An opaque per-step copy of the lane index: every lane-dependent address (LDS
+        // columns, table entries of this lane's orientations) is recomputed inside the
+        // loop, not hoisted out of it into registers held for the whole kernel (~60 such
+        // addresses kept k_mcts_coop_h at one wave per SIMD)
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        uint2* rows_lds = reinterpret_cast<uint2*>(my) + lane;
+        int16_t* lk = reinterpret_cast<int16_t*>(my) + 2 * lane;
         SECT(5);
         // ---- tree work until the search needs a movegen (uniform over the wave)
         bool done = false;

@@ -22,6 +22,11 @@ NAMES = {0: "loop tail", 1: "game start/finish", 2: "derive+movegen counts", 3: 
          12: "mcts: expand place/copies/TT", 13: "mcts: loop tail", 14: "mcts: rollout place"}
 
 
+# k_rollout_fr's frontier place, split (the place_frontier marks)
+FR_NAMES = {7: "frontier ops windows", 8: "place: stage load + LDS write", 9: "place: set ops",
+            6: "place: write-back"}
+
+
 def build():
     sys.path.insert(0, ROOT)
     from reinforcementlearning_blokus_amd import build as B
@@ -43,11 +48,12 @@ def run():
     L = N.load()
     buf = (C.c_uint64 * 16)()
 
-    def read(tag, extra):
+    def read(tag, extra, names=None):
         rc = L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
         assert rc == 0, rc
         tot = sum(buf)
-        rows = {NAMES.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
+        nm = {**NAMES, **(names or {})}
+        rows = {nm.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
         print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows}), flush=True)
 
     L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
@@ -60,7 +66,7 @@ def run():
                                          rng=N.RNG_PHILOX, seed=5, max_plies=20,
                                          root_index=np.zeros(G, dtype=np.int32))
     gpu.rollout_frontier(froots, fsets, G * R, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=1, root_index=idx)
-    read("k_rollout_fr", {"kernel_ms": gpu.last_kernel_ms()})
+    read("k_rollout_fr", {"kernel_ms": gpu.last_kernel_ms()}, FR_NAMES)
     for games in (4096, 65536):
         froots, fsets = gpu.rollout_frontier(empty_state(), N.fset_new(1), games, semantics=N.SEM_ADVANCE,
                                              rng=N.RNG_PHILOX, seed=5, max_plies=20,
@@ -89,11 +95,12 @@ def run_mcts():
     L = N.load()
     buf = (C.c_uint64 * 16)()
 
-    def read(tag, extra):
+    def read(tag, extra, names=None):
         rc = L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
         assert rc == 0, rc
         tot = sum(buf)
-        rows = {NAMES.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
+        nm = {**NAMES, **(names or {})}
+        rows = {nm.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
         print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows}), flush=True)
 
     for games, iters, policy in ((65536, 512, N.MCTS_ROLLOUT_RANDOM), (4096, 96, N.MCTS_ROLLOUT_HEURISTIC)):
