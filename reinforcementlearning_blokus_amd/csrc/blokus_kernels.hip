@@ -188,7 +188,12 @@ __device__ __forceinline__ uint32_t plane_row(const uint64_t* w, int R) {
 #ifndef BK_SLAB_PAD
 #define BK_SLAB_PAD 1
 #endif
-#define SLAB_WORDS (BK_SLAB_PAD ? 128 : SLAB_RNG_BASE + 16)
+// frontier-order rollouts: the four players' table headers (mask, fill, used as uint16)
+// live in the slab, in the line the occupancy plane ends in (read every ply anyway),
+// instead of in the FsLane record's own header line
+#define SLAB_HDR_BASE (SLAB_RNG_BASE + 16)
+#define SLAB_WORDS (BK_SLAB_PAD ? 128 : SLAB_HDR_BASE + 8)
+static_assert(SLAB_HDR_BASE + 6 <= SLAB_WORDS, "the table headers fit the slab");
 struct Slab {
     uint32_t* base;  // = slab + slot * SLAB_WORDS (16-byte aligned)
     __device__ __forceinline__ uint32_t& at(int f, int R) const { return base[f * 20 + R]; }
@@ -1739,10 +1744,16 @@ struct NoMark {
 };
 
 // mark(i): section boundaries for the diagnostic build (-DBK_SECTION_PROF)
+// hdr: player p's (mask, fill, used) when kept outside the record (the rollout slab);
+// nullptr: the record's own header
 template <int STAGE, bool RECOPY = false, typename Mark = NoMark>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
-                                               const int32_t (&cells)[5], uint64_t real, Mark mark = Mark()) {
+                                               const int32_t (&cells)[5], uint64_t real, Mark mark = Mark(),
+                                               uint16_t* hdr = nullptr) {
     bk_fset* gfs = &fl->s;
+    uint16_t* const hm = hdr ? hdr : &gfs->mask[p];
+    uint16_t* const hf = hdr ? hdr + 1 : &gfs->fill[p];
+    uint16_t* const hu = hdr ? hdr + 2 : &gfs->used[p];
     // BK_STAGE_EAGER: stages of <= 64 slots load all STAGE slots at once, alongside the
     // mask (the storage holds BK_FSET_SLOTS >= STAGE): one memory latency instead of the
     // mask's, then the table's
@@ -1753,7 +1764,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 #pragma unroll
         for (int i = 0; i < STAGE / 8; ++i) pre[i] = src4[i];
     }
-    const uint32_t gmask = gfs->mask[p];
+    const uint32_t gmask = *hm;
     bk_u32_alias* lw = reinterpret_cast<bk_u32_alias*>(lk);
     if (STAGE > 0 && gmask < (uint32_t)STAGE) {
 #pragma unroll
@@ -1766,7 +1777,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
                 lw[(4 * i + 3) * WAVE] = v.w;
             }
         }
-        const uint16_t m0 = (uint16_t)gmask, f0 = gfs->fill[p], u0 = gfs->used[p];
+        const uint16_t m0 = (uint16_t)gmask, f0 = *hf, u0 = *hu;
         uint16_t m = m0, f = f0, u = u0;
         uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab, 1, &dirty};
@@ -1783,16 +1794,16 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
                         dst4[i] = make_uint4(lw[(4 * i + 0) * WAVE], lw[(4 * i + 1) * WAVE],
                                              lw[(4 * i + 2) * WAVE], lw[(4 * i + 3) * WAVE]);
                 }
-                if (m != m0) gfs->mask[p] = m;
-                if (f != f0) gfs->fill[p] = f;
-                if (u != u0) gfs->used[p] = u;
+                if (m != m0) *hm = m;
+                if (f != f0) *hf = f;
+                if (u != u0) *hu = u;
                 return true;
             }
             // the copy: newsize <= 2 * STAGE <= BK_FSET_SLOTS (u < STAGE * 3 / 5)
             const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
 #pragma unroll 1
             for (uint32_t i = 0; i < newsize / 8; ++i) dst4[i] = unused;
-            gfs->mask[p] = (uint16_t)(newsize - 1); gfs->fill[p] = u; gfs->used[p] = u;
+            *hm = (uint16_t)(newsize - 1); *hf = u; *hu = u;
             SlotBits o;
             int16_t* dk = gfs->key[p];
 #pragma unroll 1
@@ -1805,8 +1816,10 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
             return true;
         }
     }
-    if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real)) return false;
-    return RECOPY ? fs_recopy_global(fl, p, htab) : true;
+    const FsetRef gt{gfs->key[p], 2, hm, hf, hu, BK_FSET_SLOTS, htab};
+    if (!fs_run_ops(gt, fl->tmp, cells, real)) return false;
+    if constexpr (RECOPY) return fs_recopy_global(fl, p, htab);  // (MCTS records: hdr is nullptr)
+    return true;
 }
 
 // k_mcts_pair's LDS-DMA stage of the mover's table: the lane pair (2q, 2q + 1) loads run
@@ -2266,6 +2279,11 @@ __device__ __forceinline__ void store_state(const RolloutArgs& a, const Game& g,
     o->reserved[1] = a.seat_masks ? g.passes0 + (uint32_t)g.passes : 0u;
 }
 
+// player p's table header in the rollout slab (frontier order, SLAB_HDR_BASE)
+__device__ __forceinline__ uint16_t* slab_hdr(const Slab& slab, int p) {
+    return reinterpret_cast<uint16_t*>(&slab.word(SLAB_HDR_BASE)) + 3 * p;
+}
+
 // a plain copy of the four tables: slots 0..mask of each (the rest is never read) and
 // the counters, as uint4
 __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
@@ -2281,6 +2299,52 @@ __device__ __forceinline__ void copy_fset(bk_fset* dst, const bk_fset* src) {
         const bk_u4_alias* s4 = reinterpret_cast<const bk_u4_alias*>(src->key[q]);
         bk_u4_alias* d4 = reinterpret_cast<bk_u4_alias*>(dst->key[q]);
         const int nv = (int)(masks[q] + 1u) / 8;  // 8 slots per uint4
+#pragma unroll 2
+        for (int i = 0; i < nv; ++i) d4[i] = s4[i];
+    }
+}
+
+// copy_fset with the headers (mask, fill, used) to / from the rollout slab instead of the
+// record's header line (the record's own header is not kept up to date)
+__device__ __forceinline__ void copy_fset_in(bk_fset* dst, const Slab& slab, const bk_fset* src) {
+    const bk_u4_alias* tail_s = reinterpret_cast<const bk_u4_alias*>(&src->mask[0]);
+    const uint4 t0 = tail_s[0], t1 = tail_s[1];  // mask[4] fill[4] used[4] reserved[4]
+    const uint32_t masks[4] = {t0.x & 0xFFFFu, t0.x >> 16, t0.y & 0xFFFFu, t0.y >> 16};
+    const uint32_t fills[4] = {t0.z & 0xFFFFu, t0.z >> 16, t0.w & 0xFFFFu, t0.w >> 16};
+    const uint32_t useds[4] = {t1.x & 0xFFFFu, t1.x >> 16, t1.y & 0xFFFFu, t1.y >> 16};
+    // (mask, fill, used) x 4 as 6 dwords
+    slab.word(SLAB_HDR_BASE + 0) = masks[0] | (fills[0] << 16);
+    slab.word(SLAB_HDR_BASE + 1) = useds[0] | (masks[1] << 16);
+    slab.word(SLAB_HDR_BASE + 2) = fills[1] | (useds[1] << 16);
+    slab.word(SLAB_HDR_BASE + 3) = masks[2] | (fills[2] << 16);
+    slab.word(SLAB_HDR_BASE + 4) = useds[2] | (masks[3] << 16);
+    slab.word(SLAB_HDR_BASE + 5) = fills[3] | (useds[3] << 16);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bk_u4_alias* s4 = reinterpret_cast<const bk_u4_alias*>(src->key[q]);
+        bk_u4_alias* d4 = reinterpret_cast<bk_u4_alias*>(dst->key[q]);
+        const int nv = (int)(masks[q] + 1u) / 8;  // 8 slots per uint4
+#pragma unroll 2
+        for (int i = 0; i < nv; ++i) d4[i] = s4[i];
+    }
+}
+
+__device__ __forceinline__ void copy_fset_out(bk_fset* dst, const bk_fset* src, const Slab& slab) {
+    uint32_t h[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) h[i] = slab.word(SLAB_HDR_BASE + i);
+    const uint32_t masks[4] = {h[0] & 0xFFFFu, h[1] >> 16, h[3] & 0xFFFFu, h[4] >> 16};
+    const uint32_t fills[4] = {h[0] >> 16, h[2] & 0xFFFFu, h[3] >> 16, h[5] & 0xFFFFu};
+    const uint32_t useds[4] = {h[1] & 0xFFFFu, h[2] >> 16, h[4] & 0xFFFFu, h[5] >> 16};
+    bk_u4_alias* tail_d = reinterpret_cast<bk_u4_alias*>(&dst->mask[0]);
+    tail_d[0] = make_uint4(masks[0] | (masks[1] << 16), masks[2] | (masks[3] << 16), fills[0] | (fills[1] << 16),
+                           fills[2] | (fills[3] << 16));
+    tail_d[1] = make_uint4(useds[0] | (useds[1] << 16), useds[2] | (useds[3] << 16), 0u, 0u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const bk_u4_alias* s4 = reinterpret_cast<const bk_u4_alias*>(src->key[q]);
+        bk_u4_alias* d4 = reinterpret_cast<bk_u4_alias*>(dst->key[q]);
+        const int nv = (int)(masks[q] + 1u) / 8;
 #pragma unroll 2
         for (int i = 0; i < nv; ++i) d4[i] = s4[i];
     }
@@ -2337,7 +2401,7 @@ __device__ __forceinline__ void finish_game(const RolloutArgs& a, Game& g, const
     }
     if (a.out_states != nullptr) {  // BK_SEM_ADVANCE, or an arena run that wants final states
         store_state(a, g, slab);
-        if constexpr (FR) copy_fset(a.out_sets + g.pid, &a.fslab[slot].s);
+        if constexpr (FR) copy_fset_out(a.out_sets + g.pid, &a.fslab[slot].s, slab);
         if (a.out == nullptr) { g.pid = -1; return; }
     }
     bk_result r;
@@ -2450,10 +2514,15 @@ __device__ __forceinline__ void start_game(const RolloutArgs& a, Game& g, const 
             bk_fset* d = &a.fslab[slot].s;
             const bk_fset* src = a.root_sets + ri;
 #pragma unroll 1
-            for (int q = 0; q < 4; ++q)
+            for (int q = 0; q < 4; ++q) {
                 if (!fs_copy_dev(d, q, src, htab)) g.status |= 2u;
+                uint16_t* hq = slab_hdr(slab, q);  // the header lives in the slab from here on
+                hq[0] = d->mask[q];
+                hq[1] = d->fill[q];
+                hq[2] = d->used[q];
+            }
         } else {
-            copy_fset(&a.fslab[slot].s, a.root_sets + ri);
+            copy_fset_in(&a.fslab[slot].s, slab, a.root_sets + ri);
         }
     }
     g.hmask = a.seat_masks ? (a.seat_masks[pid] & 0xFu) : (uint32_t)a.cfg.heuristic_seats;
@@ -2542,7 +2611,8 @@ __device__ __forceinline__ double draw_double(const RolloutArgs& a, Game& g, con
 // are recomputed (the LDS area held other data since); locate overwrites the rows' C
 // half, so the rows are rewritten before each of the (at most 3) locates.
 __device__ __forceinline__ void stop_info(const RolloutArgs& a, const Game& g, const Planes& P, uint32_t* my, int lane,
-                                       uint2* rows_lds, const bk_fset* fs, int p, uint32_t avail, uint32_t total) {
+                                       uint2* rows_lds, const bk_fset* fs, int fmask, int p, uint32_t avail,
+                                       uint32_t total) {
     bk_stop_info si;
     si.n_legal = (int32_t)total;
     si.quick_index = 0;
@@ -2577,7 +2647,7 @@ __device__ __forceinline__ void stop_info(const RolloutArgs& a, const Game& g, c
 #pragma unroll
             for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
             int ar, ac;
-            locate_move_frontier(g3[i], kk3[i], rows_lds, fs->key[p], fs->mask[p], ar, ac);
+            locate_move_frontier(g3[i], kk3[i], rows_lds, fs->key[p], fmask, ar, ac);
             const double d = __dadd_rn(fabs((double)ar - 9.5), fabs((double)ac - 9.5));
             if (q < 0 || d < best) { best = d; q = i; }  // min(): the first nearest
         }
@@ -2738,7 +2808,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         if (idle) continue;
         if (FR && total > 0u && ((g.smask >> p) & 1u) && !forced) {  // a search seat is to move: hand the game back
             if constexpr (HEUR) {
-                if (a.stop_out) stop_info(a, g, P, my, lane, rows_lds, &a.fslab[slot].s, p, avail, total);
+                if (a.stop_out)
+                    stop_info(a, g, P, my, lane, rows_lds, &a.fslab[slot].s, (int)*slab_hdr(slab, p), p, avail, total);
             }
             g.status |= BK_STATUS_STOP;
             finish_game<FR>(a, g, slab, slot);
@@ -2782,6 +2853,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         int ar, ac;
         if constexpr (FR) {
             const bk_fset* fs = &a.fslab[slot].s;
+            const int fmask = (int)*slab_hdr(slab, p);
             if (fmove) {  // the search's move: legal iff its anchor is in the orientation's legal set
                 gs = g.forced / 400;
                 ar = (g.forced % 400) / 20;
@@ -2793,11 +2865,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 ac = 0;
             } else if (heur) {
                 const int edge_w = (g.move_count0 + g.plies) < 30 ? 6 : 3;
-                heur_walk_frontier(gs, h_ok, rows_lds, fs->key[p], fs->mask[p], hs, edge_w, h_target, h_R, h_total,
+                heur_walk_frontier(gs, h_ok, rows_lds, fs->key[p], fmask, hs, edge_w, h_target, h_R, h_total,
                                    ar, ac, h_unc);
                 if (h_unc) g.status |= BK_STATUS_UNCERT;
             } else {
-                locate_move_frontier(gs, kk, rows_lds, fs->key[p], fs->mask[p], ar, ac);
+                locate_move_frontier(gs, kk, rows_lds, fs->key[p], fmask, ar, ac);
             }
         } else {
             locate_move_lds(gs, kk, rows_lds, ar, ac);
@@ -2854,7 +2926,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
 #else
             NoMark mark;
 #endif
-            if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real, mark))
+            if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real, mark,
+                                                              slab_hdr(slab, p)))
                 g.status |= 2u;
         }
         SECT(6);
