@@ -256,6 +256,10 @@ int bk_fset_place(bk_fset* s, const bk_state* after, int32_t player, const int32
 int bk_fset_copy(bk_fset* dst, const bk_fset* src);
 /* iteration order of player's set into out (cap entries); returns the count or < 0 */
 int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap);
+/* Diagnostics (tests): one set operation on player's set, set.add((r, c)) (add = 1) or
+   set.discard((r, c)) (add = 0), key = r*20+c: the probe / insert / resize code every
+   frontier-order kernel runs.  BK_EOVERFLOW: the table outgrew its 256 slots. */
+int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add);
 
 /*
  * bk_rollout / bk_advance in the reference's FRONTIER order (cfg->order ==

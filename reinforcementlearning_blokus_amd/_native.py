@@ -34,7 +34,7 @@ EXPORTS = (
     "bk_rollout", "bk_advance", "bk_fastmcts", "bk_last_kernel_ms", "bk_last_kernel",
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
-    "bk_arena_step", "bk_mt_cursor_init", "bk_set_tuning", "bk_get_tuning",
+    "bk_arena_step", "bk_mt_cursor_init", "bk_set_tuning", "bk_get_tuning", "bk_debug_fset_op",
 )
 # bk_set_tuning keys (include/blokus_hip.h BK_TUNE_*), by the environment variable name
 # bk_create reads each from once
@@ -186,6 +186,7 @@ def load():
                                   vp, vp, C.c_int32, vp, vp, vp, vp, C.c_int]),
             "bk_debug_sections": (C.c_int, [vp, vp, C.c_int32, C.c_int32]),
             "bk_set_tuning": (C.c_int, [vp, C.c_int32, C.c_int64]),
+            "bk_debug_fset_op": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int32]),
             "bk_get_tuning": (C.c_int, [vp, C.c_int32, P(C.c_int64)]),
         }
         for name, (res, args) in sigs.items():

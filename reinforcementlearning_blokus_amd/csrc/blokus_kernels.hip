@@ -1468,17 +1468,58 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 //   chain, else the unused slot that ended the search (then maybe resize);
 // * discard: the key's slot becomes a dummy (absent key: no-op).
 // false: the table outgrew its storage (add only).
-__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h) {
-    const uint32_t mask = *t.mask;
-    // One flat loop over the probe sequence (a divergent nested loop costs the wave far
-    // more exec-mask bookkeeping than its VALU work): from i = hash & mask the 10 slots
-    // i .. i + 9 when they fit below mask (LINEAR_PROBES 9), else slot i alone, then
-    // i = (5 i + 1 + perturb) & mask with perturb >>= 5.  Slot indices stay 32-bit: only
-    // the low bits of 5 i + 1 + perturb survive the mask.
+// The probe sequence of key k (hash h) in table t: the slot e where the search stops (k
+// found, or the first unused slot) with its value kk, and the last dummy seen before it
+// (freeslot, -1 if none).  From i = hash & mask the 10 slots i .. i + 9 when they fit
+// below mask (LINEAR_PROBES 9), else slot i alone, then i = (5 i + 1 + perturb) & mask
+// with perturb >>= 5.  Slot indices stay 32-bit: only the low bits of 5 i + 1 + perturb
+// survive the mask.
+// * Tables stored as slot pairs (sh == 1: one dword holds slots 2j, 2j + 1) are probed
+//   FOUR slots per step: the two dwords of pairs e / 2 and e / 2 + 1 are read together
+//   and the slots of the linear run among them are checked in order in registers, so a
+//   run of n slots costs ~n / 4 dependent reads instead of n (the wave iterates the
+//   longest chain of its lanes).
+// * Other layouts: one slot per step, as one flat loop (a divergent nested loop costs the
+//   wave far more exec-mask bookkeeping than its VALU work).
+__host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint32_t mask, uint32_t& e_out,
+                                         int16_t& kk_out, int32_t& freeslot) {
     uint64_t perturb = h;
     uint32_t i = (uint32_t)h & mask, e = i;
     uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
-    int32_t freeslot = -1;
+    freeslot = -1;
+    if (t.sh == 1) {
+        const bk_u32_alias* w = reinterpret_cast<const bk_u32_alias*>(t.key);
+        const uint32_t ds = (uint32_t)t.stride >> 1;  // dwords between consecutive pairs
+        for (;;) {
+            const uint32_t q = e >> 1, last = e + left;  // the run is e .. last
+            const uint32_t w0 = w[q * ds];
+            const uint32_t w1 = 2u * q + 2u <= last ? w[(q + 1u) * ds] : 0u;  // (never past the run)
+            bool stop = false;
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt) {
+                const uint32_t sl = 2u * q + (uint32_t)tt;
+                const int16_t v = (int16_t)(((tt < 2 ? w0 : w1) >> (16 * (tt & 1))) & 0xFFFFu);
+                const bool valid = !stop && sl >= e && sl <= last;
+                if (valid && (v == FS_UNUSED || v == k)) {
+                    stop = true;
+                    e_out = sl;
+                    kk_out = v;
+                } else if (valid && v == FS_DUMMY) {
+                    freeslot = (int32_t)sl;
+                }
+            }
+            if (stop) return;
+            if (2u * q + 3u < last) {  // the run goes on past these four slots
+                e = 2u * q + 4u;
+                left = last - e;
+            } else {
+                perturb >>= FS_SHIFT;
+                i = (i * 5u + 1u + (uint32_t)perturb) & mask;
+                e = i;
+                left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
+            }
+        }
+    }
     int16_t kk;
     for (;;) {
         kk = t.at(e);
@@ -1494,6 +1535,16 @@ __host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool
             left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
         }
     }
+    e_out = e;
+    kk_out = kk;
+}
+
+__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h) {
+    const uint32_t mask = *t.mask;
+    uint32_t e;
+    int16_t kk;
+    int32_t freeslot;
+    fs_probe(t, k, h, mask, e, kk, freeslot);
     if (kk == k) {  // present: discard leaves a dummy, add is a no-op
         if (!add) {
             t.at(e) = FS_DUMMY;
@@ -5309,6 +5360,13 @@ int bk_fset_copy(bk_fset* dst, const bk_fset* src) {
             return BK_EINVAL;
     }
     return BK_OK;
+}
+
+int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add) {
+    if (!s || player < 0 || player > 3 || key < 0 || key >= BK_CELLS || s->mask[player] + 1u > BK_FSET_SLOTS)
+        return BK_EINVAL;
+    int16_t tmp[BK_FSET_SLOTS];
+    return fs_op(fs_ref(s, player, kCellHashHost), tmp, (int16_t)key, add != 0) ? BK_OK : BK_EOVERFLOW;
 }
 
 int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {

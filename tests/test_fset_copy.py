@@ -151,3 +151,43 @@ def test_set_copy_matches_cpython():
         assert O.pyset_copy_list(slots, e.mask, e.fill, e.used) == ref
     assert trials > 2000
     assert runs > 0  # the linear-run case is exercised
+
+
+def test_set_operations_slot_for_slot():
+    """add / discard one at a time through the library's host restatement (bk_debug_fset_op:
+    the probe, insert and resize code every frontier-order kernel runs, including the
+    four-slots-per-step probe of pair-stored tables) against the pinned Python
+    restatement, slot for slot after every operation, and against CPython's own iteration
+    order: heavy churn, so probe chains run through many dummies, across linear runs and
+    perturbation steps, and tables resize up to 256 slots."""
+    import ctypes as C
+    L = N.load()
+    rnd = random.Random(77)
+    cells = [(r, c) for r in range(20) for c in range(20)]
+    ops = long_chains = 0
+    for trial in range(300):
+        s, e = {(0, 0)}, PySet()
+        e.add((0, 0))
+        fs = N.fset_new(1)  # player 0's set = {(0, 0)} (the start corner)
+        # a hot subset of keys per trial: chains through many dummies
+        hot = rnd.sample(cells, rnd.choice([12, 40, 90, 160]))
+        for _ in range(rnd.randint(50, 600)):
+            k = rnd.choice(hot)
+            add = rnd.random() < 0.55
+            if add:
+                s.add(k), e.add(k)
+            else:
+                s.discard(k), e.discard(k)
+            if e.mask + 1 > N.FSET_SLOTS:  # beyond the library's storage: the trial ends here
+                break
+            rc = L.bk_debug_fset_op(fs.ctypes.data, 0, k[0] * 20 + k[1], int(add))
+            assert rc == N.OK, rc
+            ops += 1
+            m = int(fs["mask"][0, 0])
+            assert m == e.mask and int(fs["fill"][0, 0]) == e.fill and int(fs["used"][0, 0]) == e.used
+            assert fs["key"][0, 0, : m + 1].tolist() == e.slots(), (trial, k, add)
+        else:
+            assert e.order() == list(s)
+            assert N.fset_list(fs, 0) == [r * 20 + c for r, c in s]
+        long_chains += e.mask >= 63 and e.fill - e.used > e.used // 2
+    assert ops > 50000 and long_chains > 10
