@@ -1474,26 +1474,28 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 // below mask (LINEAR_PROBES 9), else slot i alone, then i = (5 i + 1 + perturb) & mask
 // with perturb >>= 5.  Slot indices stay 32-bit: only the low bits of 5 i + 1 + perturb
 // survive the mask.
-// * Tables stored as slot pairs (sh == 1: one dword holds slots 2j, 2j + 1) are probed
-//   FOUR slots per step: the two dwords of pairs e / 2 and e / 2 + 1 are read together
+// * Tables stored in runs of >= 2 slots (sh >= 1: one dword holds slots 2j, 2j + 1) are
+//   probed FOUR slots per step: the two dwords of pairs e / 2 and e / 2 + 1 are read together
 //   and the slots of the linear run among them are checked in order in registers, so a
 //   run of n slots costs ~n / 4 dependent reads instead of n (the wave iterates the
 //   longest chain of its lanes).
-// * Other layouts: one slot per step, as one flat loop (a divergent nested loop costs the
-//   wave far more exec-mask bookkeeping than its VALU work).
+// * Runs of one slot (sh == 0): one slot per step, as one flat loop (a divergent nested
+//   loop costs the wave far more exec-mask bookkeeping than its VALU work).
 __host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint32_t mask, uint32_t& e_out,
                                          int16_t& kk_out, int32_t& freeslot) {
     uint64_t perturb = h;
     uint32_t i = (uint32_t)h & mask, e = i;
     uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
     freeslot = -1;
-    if (t.sh == 1) {
+    if (t.sh >= 1) {
         const bk_u32_alias* w = reinterpret_cast<const bk_u32_alias*>(t.key);
-        const uint32_t ds = (uint32_t)t.stride >> 1;  // dwords between consecutive pairs
+        const uint32_t rmask = (1u << t.sh) - 1u;
+        // dword of slot pair q: slots 2q, 2q + 1 sit in one run (runs hold 2^sh >= 2 slots)
+        auto pair_dw = [&](uint32_t q) { return (((2u * q) >> t.sh) * (uint32_t)t.stride + ((2u * q) & rmask)) >> 1; };
         for (;;) {
             const uint32_t q = e >> 1, last = e + left;  // the run is e .. last
-            const uint32_t w0 = w[q * ds];
-            const uint32_t w1 = 2u * q + 2u <= last ? w[(q + 1u) * ds] : 0u;  // (never past the run)
+            const uint32_t w0 = w[pair_dw(q)];
+            const uint32_t w1 = 2u * q + 2u <= last ? w[pair_dw(q + 1u)] : 0u;  // (never past the run)
             bool stop = false;
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt) {
