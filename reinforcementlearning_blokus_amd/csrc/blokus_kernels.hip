@@ -87,6 +87,12 @@
 #ifndef BK_STAGE_EAGER
 #define BK_STAGE_EAGER 1
 #endif
+// fs_run_ops keeps the cell hashes of the next BK_OPS_HQUEUE set operations in flight (0:
+// each op loads its own)
+#ifndef BK_OPS_HQUEUE
+#define BK_OPS_HQUEUE 0
+#endif
+
 #ifndef BK_STAGE_EAGER_MAX
 #define BK_STAGE_EAGER_MAX 64
 #endif
@@ -1473,55 +1479,17 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 // (freeslot, -1 if none).  From i = hash & mask the 10 slots i .. i + 9 when they fit
 // below mask (LINEAR_PROBES 9), else slot i alone, then i = (5 i + 1 + perturb) & mask
 // with perturb >>= 5.  Slot indices stay 32-bit: only the low bits of 5 i + 1 + perturb
-// survive the mask.
-// * Tables stored in runs of >= 2 slots (sh >= 1: one dword holds slots 2j, 2j + 1) are
-//   probed FOUR slots per step: the two dwords of pairs e / 2 and e / 2 + 1 are read together
-//   and the slots of the linear run among them are checked in order in registers, so a
-//   run of n slots costs ~n / 4 dependent reads instead of n (the wave iterates the
-//   longest chain of its lanes).
-// * Runs of one slot (sh == 0): one slot per step, as one flat loop (a divergent nested
-//   loop costs the wave far more exec-mask bookkeeping than its VALU work).
+// survive the mask.  One slot per step, as one flat loop (a divergent nested loop costs
+// the wave far more exec-mask bookkeeping than its VALU work).  Reading two or four slots
+// per step from the pair-stored tables measured slower (frontier-order config 3 34.1 ->
+// 33.2 / 33.0 M playouts/s, config 5 17.6 -> 17.1 / 17.0 M; profiles/r05/sweeps/r05f):
+// most chains end at their first or second slot.
 __host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint32_t mask, uint32_t& e_out,
                                          int16_t& kk_out, int32_t& freeslot) {
     uint64_t perturb = h;
     uint32_t i = (uint32_t)h & mask, e = i;
     uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
     freeslot = -1;
-    if (t.sh >= 1) {
-        const bk_u32_alias* w = reinterpret_cast<const bk_u32_alias*>(t.key);
-        const uint32_t rmask = (1u << t.sh) - 1u;
-        // dword of slot pair q: slots 2q, 2q + 1 sit in one run (runs hold 2^sh >= 2 slots)
-        auto pair_dw = [&](uint32_t q) { return (((2u * q) >> t.sh) * (uint32_t)t.stride + ((2u * q) & rmask)) >> 1; };
-        for (;;) {
-            const uint32_t q = e >> 1, last = e + left;  // the run is e .. last
-            const uint32_t w0 = w[pair_dw(q)];
-            const uint32_t w1 = 2u * q + 2u <= last ? w[pair_dw(q + 1u)] : 0u;  // (never past the run)
-            bool stop = false;
-#pragma unroll
-            for (int tt = 0; tt < 4; ++tt) {
-                const uint32_t sl = 2u * q + (uint32_t)tt;
-                const int16_t v = (int16_t)(((tt < 2 ? w0 : w1) >> (16 * (tt & 1))) & 0xFFFFu);
-                const bool valid = !stop && sl >= e && sl <= last;
-                if (valid && (v == FS_UNUSED || v == k)) {
-                    stop = true;
-                    e_out = sl;
-                    kk_out = v;
-                } else if (valid && v == FS_DUMMY) {
-                    freeslot = (int32_t)sl;
-                }
-            }
-            if (stop) return;
-            if (2u * q + 3u < last) {  // the run goes on past these four slots
-                e = 2u * q + 4u;
-                left = last - e;
-            } else {
-                perturb >>= FS_SHIFT;
-                i = (i * 5u + 1u + (uint32_t)perturb) & mask;
-                e = i;
-                left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
-            }
-        }
-    }
     int16_t kk;
     for (;;) {
         kk = t.at(e);
@@ -1667,13 +1635,39 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
         const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
         return cell + (int)((KD >> (6 * op)) & 63ull) - 21;
     };
+#if BK_OPS_HQUEUE
+    // the cell hashes of the next BK_OPS_HQUEUE ops are loaded before they are needed: the
+    // first ones together, then each op issues the load of the op that many places ahead
+    constexpr int QN = BK_OPS_HQUEUE;
+    uint64_t hq[QN];
+    uint64_t ahead = real;
+#pragma unroll
+    for (int j = 0; j < QN; ++j) {
+        hq[j] = 0ull;
+        if (ahead) {
+            hq[j] = t.hash[key_of((int)__builtin_ctzll(ahead))];
+            ahead &= ahead - 1ull;
+        }
+    }
+#endif
 #pragma unroll 1
     while (real) {
         const int s = (int)__builtin_ctzll(real);
         real &= real - 1ull;
         const int op = s - 9 * ((s * 57) >> 9);
         const int key = key_of(s);
+#if BK_OPS_HQUEUE
+        const uint64_t h = hq[0];
+#pragma unroll
+        for (int j = 0; j + 1 < QN; ++j) hq[j] = hq[j + 1];
+        hq[QN - 1] = 0ull;
+        if (ahead) {
+            hq[QN - 1] = t.hash[key_of((int)__builtin_ctzll(ahead))];
+            ahead &= ahead - 1ull;
+        }
+#else
         const uint64_t h = t.hash[key];
+#endif
         if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h)) return false;
     }
     return true;
