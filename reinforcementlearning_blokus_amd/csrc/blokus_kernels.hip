@@ -87,11 +87,6 @@
 #ifndef BK_STAGE_EAGER
 #define BK_STAGE_EAGER 1
 #endif
-// fs_run_ops keeps the cell hashes of the next BK_OPS_HQUEUE set operations in flight (0:
-// each op loads its own)
-#ifndef BK_OPS_HQUEUE
-#define BK_OPS_HQUEUE 0
-#endif
 
 #ifndef BK_STAGE_EAGER_MAX
 #define BK_STAGE_EAGER_MAX 64
@@ -1635,39 +1630,15 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
         const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
         return cell + (int)((KD >> (6 * op)) & 63ull) - 21;
     };
-#if BK_OPS_HQUEUE
-    // the cell hashes of the next BK_OPS_HQUEUE ops are loaded before they are needed: the
-    // first ones together, then each op issues the load of the op that many places ahead
-    constexpr int QN = BK_OPS_HQUEUE;
-    uint64_t hq[QN];
-    uint64_t ahead = real;
-#pragma unroll
-    for (int j = 0; j < QN; ++j) {
-        hq[j] = 0ull;
-        if (ahead) {
-            hq[j] = t.hash[key_of((int)__builtin_ctzll(ahead))];
-            ahead &= ahead - 1ull;
-        }
-    }
-#endif
 #pragma unroll 1
     while (real) {
         const int s = (int)__builtin_ctzll(real);
         real &= real - 1ull;
         const int op = s - 9 * ((s * 57) >> 9);
         const int key = key_of(s);
-#if BK_OPS_HQUEUE
-        const uint64_t h = hq[0];
-#pragma unroll
-        for (int j = 0; j + 1 < QN; ++j) hq[j] = hq[j + 1];
-        hq[QN - 1] = 0ull;
-        if (ahead) {
-            hq[QN - 1] = t.hash[key_of((int)__builtin_ctzll(ahead))];
-            ahead &= ahead - 1ull;
-        }
-#else
+        // (loading the next ops' hashes ahead, 3 or 6 in flight, measured slower:
+        // 34.2 -> 33.6 M frontier-order playouts/s, profiles/r05/sweeps/r05g)
         const uint64_t h = t.hash[key];
-#endif
         if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h)) return false;
     }
     return true;
@@ -2973,6 +2944,9 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
 #else
             NoMark mark;
 #endif
+            // (staging every table of <= 128 slots in packed per-lane segments of the area,
+            // so no lane probes its table in global memory, measured slower: 34.2 -> 31.7 M
+            // playouts/s, profiles/r05/sweeps/r05i: the kernel is issue-bound, not waiting)
             if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real, mark,
                                                               slab_hdr(slab, p)))
                 g.status |= 2u;
