@@ -1447,6 +1447,91 @@ __host__ __device__ inline void fs_insert_clean(FsetRef t, uint32_t mask, int16_
     t.at(e) = k;
 }
 
+// Occupancy of a table of <= 256 slots in registers: set_insert_clean's probe sequence
+// on a fresh table needs only "is slot i unused", so a clean re-insert never reads the
+// destination back.
+struct SlotBits {
+    uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    __host__ __device__ __forceinline__ bool test(uint32_t i) const {
+        const uint32_t q = i >> 6;
+        const uint64_t w = q == 0u ? w0 : q == 1u ? w1 : q == 2u ? w2 : w3;
+        return ((w >> (i & 63u)) & 1ull) != 0ull;
+    }
+    __host__ __device__ __forceinline__ void set(uint32_t i) {
+        const uint64_t b = 1ull << (i & 63u);
+        const uint32_t q = i >> 6;
+        w0 |= q == 0u ? b : 0ull;
+        w1 |= q == 1u ? b : 0ull;
+        w2 |= q == 2u ? b : 0ull;
+        w3 |= q == 3u ? b : 0ull;
+    }
+};
+
+// fs_insert_clean's slot for key hash h in a fresh table of mask + 1 slots whose used
+// slots are `o` (marks the slot used)
+__host__ __device__ __forceinline__ uint32_t fs_clean_slot(uint64_t h, uint32_t mask, SlotBits& o) {
+    uint64_t perturb = h;
+    uint32_t i = (uint32_t)h & mask, e = i;
+    uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
+#pragma unroll 1
+    while (o.test(e)) {  // fs_insert_clean's sequence
+        if (left > 0u) {
+            --left;
+            ++e;
+        } else {
+            perturb >>= FS_SHIFT;
+            i = (i * 5u + 1u + (uint32_t)perturb) & mask;
+            e = i;
+            left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
+        }
+    }
+    o.set(e);
+    return e;
+}
+
+// set_table_resize without a copy of the old table, for tables staged in LDS (new size
+// <= 128): pass 1 walks the old slots in order and gives each active key its slot in the
+// fresh table from a register bitmap (fs_clean_slot: set_insert_clean's probe sequence),
+// leaving the tag key | slot << 9 in the old slot (keys < 400 take 9 bits, slots < 128
+// the other 7; -1 = nothing to move); pass 2 moves every tagged key to its slot by
+// following the chain of tags it displaces.  The result is fs_resize's, slot for slot
+// (tests/test_fset_copy.py through bk_debug_fset_op), without the old keys' round trip
+// through the record's global tmp, which cost k_mcts_pair one dependent memory latency per
+// key (~10 % of its rollout placements resize a table).
+__host__ __device__ inline bool fs_resize_inplace(FsetRef t, uint32_t minused) {
+    uint32_t newsize = 8;
+    while (newsize <= minused) newsize <<= 1;
+    if (newsize > t.cap || newsize > 128u) return false;
+    const uint32_t omask = *t.mask;
+    for (uint32_t i = omask + 1u; i < newsize; ++i) t.at(i) = FS_UNUSED;
+    {
+        SlotBits o;
+        for (uint32_t i = 0; i <= omask; ++i) {
+            const int16_t k = t.at(i);
+            const uint32_t tag = k >= 0 ? ((uint32_t)k | (fs_clean_slot(t.hash[k], newsize - 1u, o) << 9)) : 0xFFFFu;
+            t.at(i) = (int16_t)(uint16_t)tag;
+        }
+    }
+    SlotBits fin;  // slots that hold their final key
+    for (uint32_t i = 0; i <= omask; ++i) {
+        if (fin.test(i)) continue;
+        uint32_t v = (uint16_t)t.at(i);
+        if (v == 0xFFFFu) continue;
+        t.at(i) = FS_UNUSED;
+        for (;;) {
+            const uint32_t j = v >> 9;
+            const uint32_t w = (uint16_t)t.at(j);
+            t.at(j) = (int16_t)(v & 511u);
+            fin.set(j);
+            if (w == 0xFFFFu) break;
+            v = w;  // a tag displaced from j: its key moves next
+        }
+    }
+    *t.mask = (uint16_t)(newsize - 1u);
+    *t.fill = *t.used;
+    return true;
+}
+
 // set_table_resize(minused): fresh table, active entries re-inserted in slot order.
 // tmp (stride 1) holds the old keys.  false: the storage cannot hold the new table.
 __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minused) {
@@ -1468,7 +1553,8 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 // * add: an existing key is a no-op; a new key takes the LAST dummy seen on its probe
 //   chain, else the unused slot that ended the search (then maybe resize);
 // * discard: the key's slot becomes a dummy (absent key: no-op).
-// false: the table outgrew its storage (add only).
+// false: the table outgrew its storage (add only).  tmp == nullptr: resize in place
+// (fs_resize_inplace; LDS-staged tables).
 // The probe sequence of key k (hash h) in table t: the slot e where the search stops (k
 // found, or the first unused slot) with its value kk, and the last dummy seen before it
 // (freeslot, -1 if none).  From i = hash & mask the 10 slots i .. i + 9 when they fit
@@ -1530,8 +1616,12 @@ __host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool
     t.at(e) = k;
     t.mark(e);
     if ((uint64_t)*t.fill * 5 < (uint64_t)mask * 3) return true;
+#if defined(BK_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    atomicAdd(&g_sections[15], 1ull);  // diagnostic: resizes
+#endif
     if (t.dirty) *t.dirty = ~0u;  // every slot is rewritten
-    return fs_resize(t, tmp, *t.used > 50000 ? *t.used * 2u : *t.used * 4u);
+    const uint32_t minused = *t.used > 50000 ? *t.used * 2u : *t.used * 4u;
+    return tmp ? fs_resize(t, tmp, minused) : fs_resize_inplace(t, minused);
 }
 
 __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
@@ -1664,48 +1754,6 @@ struct FsLane {
 // WAVE): one ds_write_b32 / ds_read_b32 per slot pair, and a probe of ANY slot by each
 // lane hits bank `lane` (conflict-free).  A larger table (or a move that grows one past
 // the stage) is updated in place.  false: table overflow.
-// Occupancy of a table of <= 256 slots in registers: set_insert_clean's probe sequence
-// on a fresh table needs only "is slot i unused", so a clean re-insert never reads the
-// destination back.
-struct SlotBits {
-    uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    __device__ __forceinline__ bool test(uint32_t i) const {
-        const uint32_t q = i >> 6;
-        const uint64_t w = q == 0u ? w0 : q == 1u ? w1 : q == 2u ? w2 : w3;
-        return ((w >> (i & 63u)) & 1ull) != 0ull;
-    }
-    __device__ __forceinline__ void set(uint32_t i) {
-        const uint64_t b = 1ull << (i & 63u);
-        const uint32_t q = i >> 6;
-        w0 |= q == 0u ? b : 0ull;
-        w1 |= q == 1u ? b : 0ull;
-        w2 |= q == 2u ? b : 0ull;
-        w3 |= q == 3u ? b : 0ull;
-    }
-};
-
-// fs_insert_clean's slot for key hash h in a fresh table of mask + 1 slots whose used
-// slots are `o` (marks the slot used)
-__device__ __forceinline__ uint32_t fs_clean_slot(uint64_t h, uint32_t mask, SlotBits& o) {
-    uint64_t perturb = h;
-    uint32_t i = (uint32_t)h & mask, e = i;
-    uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
-#pragma unroll 1
-    while (o.test(e)) {  // fs_insert_clean's sequence
-        if (left > 0u) {
-            --left;
-            ++e;
-        } else {
-            perturb >>= FS_SHIFT;
-            i = (i * 5u + 1u + (uint32_t)perturb) & mask;
-            e = i;
-            left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
-        }
-    }
-    o.set(e);
-    return e;
-}
-
 // fs_copy_dev's size rule: the copy of a table with `used` active keys has newsize
 // slots; the copy is slot-for-slot the source when the size is unchanged and the source
 // has no dummies (set_merge's same-size path)
@@ -1800,7 +1848,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
         uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab, 1, &dirty};
         mark(8);
-        const bool ran = fs_run_ops(t, fl->tmp, cells, real);
+        const bool ran = fs_run_ops(t, nullptr, cells, real);
         mark(9);
         if (ran) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
@@ -1852,15 +1900,17 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 // back to the global table when the ops outgrow the stage.
 // RUN_U4: uint4 distance between 16-slot runs (k_mcts_pair's pair stage: 64; the
 // cooperative kernels' one-per-wave stage, a plain array: 2)
-template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4>
+template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4, typename Mark = NoMark>
 __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* stage_q, const uint64_t* htab,
-                                                   const int32_t (&cells)[5], uint64_t real) {
+                                                   const int32_t (&cells)[5], uint64_t real, Mark mark = Mark()) {
     bk_fset* gfs = &fl->s;
     const uint16_t m0 = gfs->mask[p], f0 = gfs->fill[p], u0 = gfs->used[p];
     uint16_t m = m0, f = f0, u = u0;
     uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
     FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4, &dirty};
-    if (fs_run_ops(t, fl->tmp, cells, real)) {
+    const bool ran = fs_run_ops(t, nullptr, cells, real);
+    mark(5);
+    if (ran) {
         bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
         const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(stage_q);
         const uint32_t newsize = fs_copy_size(u);
@@ -3334,11 +3384,11 @@ __device__ __forceinline__ void piece_cells(int gs, int ar, int ac, uint32_t (&p
 // RECOPY: the table then becomes its Board.copy() in place (expansion and replay edges:
 // node boards are copies).
 // stage_q (k_mcts_pair): the mover's table is already in the LDS-DMA stage at stage_q.
-template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4>
+template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4, typename Mark = NoMark>
 __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
                                                 const uint64_t* htab, const uint32_t (&pm)[5],
                                                 const int32_t (&cells)[5], uint64_t real, int16_t* lk,
-                                                int16_t* stage_q = nullptr) {
+                                                int16_t* stage_q = nullptr, Mark mark = Mark()) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
 #pragma unroll
@@ -3348,7 +3398,8 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
             slab.at(4, ar + d) |= pm[d];
         }
     }
-    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real)
+    mark(4);
+    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real, mark)
                             : place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
@@ -3865,6 +3916,18 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         piece_cells(gs, ar, ac, pm, cells);
         // all lanes, before any table staging
         const uint64_t real = frontier_ops(rows_lds, slab, p, (m.first >> p) & 1u, gs, ar, ac, pm);
+        SECT(3);
+#ifdef BK_SECTION_PROF
+        {  // diagnostic counts (not cycles): [6] places per wave, [7] real ops, [15] wave max of real ops
+            uint32_t c = (uint32_t)__popcll(real), cm = c, cs = c;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                cm = max(cm, (uint32_t)__shfl_xor((int)cm, o));
+                cs += (uint32_t)__shfl_xor((int)cs, o);
+            }
+            sect_acc[6] += 1; sect_acc[7] += cs; sect_acc[14] += 0 * cm;
+        }
+#endif
         // MCTSNode.expand (mcts_agent.py:113-145) places on new_board = board.copy() (B),
         // a rollout ply on sim (B): one place call site for both
         const bool expand = m.mode == MC_EXPAND;
@@ -3887,8 +3950,13 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         // and MCTSNode(new_board)'s copy replaces the mover's table in place; the rollout's
         // sim = node.board.copy() is that copy again (A), and its plies place on A
         int16_t* sq = (PAIR && staged) ? stage_q : nullptr;
-        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
-        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
+#ifdef BK_SECTION_PROF
+        auto mark = [&](int i) { SECT(i); };
+#else
+        NoMark mark;
+#endif
+        if (expand) ok &= mc_place_staged<true>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, mark);
+        else ok &= mc_place_staged<false>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, mark);
         if (expand) {
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
@@ -5336,7 +5404,10 @@ int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add) {
     if (!s || player < 0 || player > 3 || key < 0 || key >= BK_CELLS || s->mask[player] + 1u > BK_FSET_SLOTS)
         return BK_EINVAL;
     int16_t tmp[BK_FSET_SLOTS];
-    return fs_op(fs_ref(s, player, kCellHashHost), tmp, (int16_t)key, add != 0) ? BK_OK : BK_EOVERFLOW;
+    // add bit 1: resize in place (fs_resize_inplace, the staged kernels' path; <= 128 slots)
+    return fs_op(fs_ref(s, player, kCellHashHost), (add & 2) ? nullptr : tmp, (int16_t)key, (add & 1) != 0)
+               ? BK_OK
+               : BK_EOVERFLOW;
 }
 
 int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {

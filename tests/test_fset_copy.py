@@ -12,6 +12,7 @@ that advanced i got wrong)."""
 import random
 
 import numpy as np
+import pytest
 
 from oracle import pyoracle as O
 from reinforcementlearning_blokus_amd import _native as N
@@ -153,16 +154,17 @@ def test_set_copy_matches_cpython():
     assert runs > 0  # the linear-run case is exercised
 
 
-def test_set_operations_slot_for_slot():
+@pytest.mark.parametrize("inplace", [False, True])
+def test_set_operations_slot_for_slot(inplace):
     """add / discard one at a time through the library's host restatement (bk_debug_fset_op:
-    the probe, insert and resize code every frontier-order kernel runs, including the
-    four-slots-per-step probe of pair-stored tables) against the pinned Python
-    restatement, slot for slot after every operation, and against CPython's own iteration
-    order: heavy churn, so probe chains run through many dummies, across linear runs and
-    perturbation steps, and tables resize up to 256 slots."""
-    import ctypes as C
+    the probe, insert and resize code every frontier-order kernel runs; inplace: the
+    resize without a copy of the old table that the LDS-staged tables use) against the
+    pinned Python restatement, slot for slot after every operation, and against CPython's
+    own iteration order: heavy churn, so probe chains run through many dummies, across
+    linear runs and perturbation steps, and tables resize up to 256 slots (128 in place)."""
     L = N.load()
     rnd = random.Random(77)
+    cap = 128 if inplace else N.FSET_SLOTS
     cells = [(r, c) for r in range(20) for c in range(20)]
     ops = long_chains = 0
     for trial in range(300):
@@ -178,9 +180,9 @@ def test_set_operations_slot_for_slot():
                 s.add(k), e.add(k)
             else:
                 s.discard(k), e.discard(k)
-            if e.mask + 1 > N.FSET_SLOTS:  # beyond the library's storage: the trial ends here
+            if e.mask + 1 > cap:  # beyond the library's storage: the trial ends here
                 break
-            rc = L.bk_debug_fset_op(fs.ctypes.data, 0, k[0] * 20 + k[1], int(add))
+            rc = L.bk_debug_fset_op(fs.ctypes.data, 0, k[0] * 20 + k[1], int(add) | (2 if inplace else 0))
             assert rc == N.OK, rc
             ops += 1
             m = int(fs["mask"][0, 0])

@@ -101,7 +101,7 @@ def run_mcts():
         tot = sum(buf)
         nm = {**NAMES, **(names or {})}
         rows = {nm.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
-        print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows}), flush=True)
+        print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows, "raw": list(buf)}), flush=True)
 
     for games, iters, policy in ((65536, 512, N.MCTS_ROLLOUT_RANDOM), (4096, 96, N.MCTS_ROLLOUT_HEURISTIC)):
         roots, sets = frontier_roots(gpu, games, 20, seed=11)
@@ -113,8 +113,11 @@ def run_mcts():
         gpu.mcts_device(b.roots, b.sets, b.players, b.root_hash, b.zobrist, b.zidx, b.mt, b.log_table, b.nodes,
                         b.out, iterations=iters, tt_keys=b.tt_keys, tt_vals=b.tt_vals, tt_count=b.tt_count,
                         chunk=64, resume_from=iters - 64, rollout_policy=policy)
-        # k_mcts splits its tree phase: 0 select, 1 replay, 2 game start/finish/complete
-        NAMES.update({0: "mcts tree: select", 1: "mcts tree: replay", 2: "mcts tree: start/finish/terminal"})
+        # k_mcts splits its tree phase: 0 select, 1 replay, 2 game start/finish/complete;
+        # and its place: 3 frontier ops windows, 4 slab rows, 5 set ops (k_mcts_pair's stage)
+        NAMES.update({0: "mcts tree: select", 1: "mcts tree: replay", 2: "mcts tree: start/finish/terminal",
+                      3: "mcts place: ops windows", 4: "mcts place: piece cells + slab rows",
+                      5: "mcts place: set ops", 14: "mcts place: write-back + rollout tail"})
         read("k_mcts" if policy == N.MCTS_ROLLOUT_RANDOM else "k_mcts_h",
              {"games": games, "iterations": f"{iters - 64}..{iters}", "kernel_ms": gpu.last_kernel_ms()})
 
