@@ -258,9 +258,9 @@ int bk_fset_copy(bk_fset* dst, const bk_fset* src);
 int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap);
 /* Diagnostics (tests): one set operation on player's set, set.add((r, c)) (add = 1) or
    set.discard((r, c)) (add = 0), key = r*20+c: the probe / insert / resize code every
-   frontier-order kernel runs; add | 2: resize in place, as the kernels' LDS-staged tables
-   do (tables of <= 128 slots).  BK_EOVERFLOW: the table outgrew its 256 slots (128 with
-   add | 2). */
+   frontier-order kernel runs; add | 2: resize through a small scratch, as the kernels'
+   LDS-staged tables do (tables of <= 128 slots).  BK_EOVERFLOW: the table outgrew its 256
+   slots (128 with add | 2). */
 int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add);
 
 /*

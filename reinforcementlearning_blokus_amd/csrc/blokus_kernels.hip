@@ -384,6 +384,11 @@ struct StencilClass {
 #ifndef FR_BLOCKS_PER_CU
 #define FR_BLOCKS_PER_CU 4
 #endif
+// LDS-staged frontier tables resize through an LDS scratch (fs_resize_lds) where the
+// caller has one; 0: always through the record's global tmp (fs_resize)
+#ifndef BK_RESIZE_LDS
+#define BK_RESIZE_LDS 1
+#endif
 #ifndef MCTS_BLOCKS_PER_CU
 #define MCTS_BLOCKS_PER_CU 2
 #endif
@@ -1402,14 +1407,14 @@ static const uint64_t kCellHashHost[BK_CELLS] = BK_CELL_HASH_INIT;
 #define FS_DUMMY ((int16_t)-2)
 
 struct FsetRef {  // one player's table: runs of 2^sh slots, run j at key[j * stride]
-    int16_t* key;
-    int stride;       // 2: a plain array; 2 * WAVE: slot pairs of one lane interleaved in LDS;
+    int16_t* key = nullptr;
+    int stride = 2;   // 2: a plain array; 2 * WAVE: slot pairs of one lane interleaved in LDS;
                       // 512 (sh 4): 16-slot runs of a lane pair's LDS-DMA stage (k_mcts_pair)
-    uint16_t* mask;
-    uint16_t* fill;
-    uint16_t* used;
-    uint32_t cap;     // largest table this storage holds (power of 2)
-    const uint64_t* hash;  // hash((r, c)) by cell
+    uint16_t* mask = nullptr;
+    uint16_t* fill = nullptr;
+    uint16_t* used = nullptr;
+    uint32_t cap = 0; // largest table this storage holds (power of 2)
+    const uint64_t* hash = nullptr;  // hash((r, c)) by cell
     int sh = 1;       // log2 of the run length
     uint32_t* dirty = nullptr;  // if set: bit j marks 8-slot chunk j written (all: a resize)
     __host__ __device__ __forceinline__ int16_t& at(uint32_t i) const {
@@ -1489,46 +1494,50 @@ __host__ __device__ __forceinline__ uint32_t fs_clean_slot(uint64_t h, uint32_t 
     return e;
 }
 
-// set_table_resize without a copy of the old table, for tables staged in LDS (new size
-// <= 128): pass 1 walks the old slots in order and gives each active key its slot in the
-// fresh table from a register bitmap (fs_clean_slot: set_insert_clean's probe sequence),
-// leaving the tag key | slot << 9 in the old slot (keys < 400 take 9 bits, slots < 128
-// the other 7; -1 = nothing to move); pass 2 moves every tagged key to its slot by
-// following the chain of tags it displaces.  The result is fs_resize's, slot for slot
-// (tests/test_fset_copy.py through bk_debug_fset_op), without the old keys' round trip
-// through the record's global tmp, which cost k_mcts_pair one dependent memory latency per
-// key (~10 % of its rollout placements resize a table).
-__host__ __device__ inline bool fs_resize_inplace(FsetRef t, uint32_t minused) {
+// set_table_resize for a table staged in LDS, with a small LDS scratch `tmp` (FsetRef
+// layout, at least cap / 4 keys): the active keys, read 16 slots at a time (the reads
+// issued together), go to tmp in slot order; the table is cleared and they are
+// re-inserted with their slots from a register occupancy bitmap (fs_clean_slot:
+// set_insert_clean's probe sequence), 8 keys and their cell hashes loaded at a time.  A
+// resize that stays within the storage has used * 4 < newsize <= cap, so tmp never holds
+// more than cap / 4 keys.  Equal to fs_resize slot for slot (tests/test_fset_copy.py
+// through bk_debug_fset_op).  fs_resize instead copies every slot to the record's tmp in
+// global memory and re-inserts one dependent memory latency at a time: resizes were ~86 %
+// of k_rollout_fr's set-operation time and ~90 % of k_mcts_pair's
+// (profiles/r05/sweeps/r05n, -DBK_SECTION_PROF).
+__host__ __device__ inline bool fs_resize_lds(FsetRef t, FsetRef tmp, uint32_t minused) {
     uint32_t newsize = 8;
     while (newsize <= minused) newsize <<= 1;
-    if (newsize > t.cap || newsize > 128u) return false;
+    if (newsize > t.cap) return false;
     const uint32_t omask = *t.mask;
-    for (uint32_t i = omask + 1u; i < newsize; ++i) t.at(i) = FS_UNUSED;
-    {
-        SlotBits o;
-        for (uint32_t i = 0; i <= omask; ++i) {
-            const int16_t k = t.at(i);
-            const uint32_t tag = k >= 0 ? ((uint32_t)k | (fs_clean_slot(t.hash[k], newsize - 1u, o) << 9)) : 0xFFFFu;
-            t.at(i) = (int16_t)(uint16_t)tag;
+    uint32_t n = 0;
+    for (uint32_t b = 0; b <= omask; b += 16) {
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            w[j] = b + 2u * (uint32_t)j <= omask ? *reinterpret_cast<const bk_u32_alias*>(&t.at(b + 2u * (uint32_t)j))
+                                                 : 0xFFFFFFFFu;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int16_t k = (int16_t)(w[q >> 1] >> (16 * (q & 1)));
+            if (k >= 0) tmp.at(n++) = k;
         }
     }
-    SlotBits fin;  // slots that hold their final key
-    for (uint32_t i = 0; i <= omask; ++i) {
-        if (fin.test(i)) continue;
-        uint32_t v = (uint16_t)t.at(i);
-        if (v == 0xFFFFu) continue;
-        t.at(i) = FS_UNUSED;
-        for (;;) {
-            const uint32_t j = v >> 9;
-            const uint32_t w = (uint16_t)t.at(j);
-            t.at(j) = (int16_t)(v & 511u);
-            fin.set(j);
-            if (w == 0xFFFFu) break;
-            v = w;  // a tag displaced from j: its key moves next
-        }
-    }
+    for (uint32_t j = 0; j < newsize; j += 2) *reinterpret_cast<bk_u32_alias*>(&t.at(j)) = 0xFFFFFFFFu;
     *t.mask = (uint16_t)(newsize - 1u);
     *t.fill = *t.used;
+    SlotBits o;
+    for (uint32_t b = 0; b < n; b += 8) {
+        int16_t k[8];
+        uint64_t h[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) k[q] = b + (uint32_t)q < n ? tmp.at(b + (uint32_t)q) : (int16_t)-1;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) h[q] = k[q] >= 0 ? t.hash[k[q]] : 0ull;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (k[q] >= 0) t.at(fs_clean_slot(h[q], newsize - 1u, o)) = k[q];
+    }
     return true;
 }
 
@@ -1553,8 +1562,8 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 // * add: an existing key is a no-op; a new key takes the LAST dummy seen on its probe
 //   chain, else the unused slot that ended the search (then maybe resize);
 // * discard: the key's slot becomes a dummy (absent key: no-op).
-// false: the table outgrew its storage (add only).  tmp == nullptr: resize in place
-// (fs_resize_inplace; LDS-staged tables).
+// false: the table outgrew its storage (add only).  ltmp.key set: an LDS-staged table,
+// resized through the LDS scratch ltmp (fs_resize_lds); else through tmp (fs_resize).
 // The probe sequence of key k (hash h) in table t: the slot e where the search stops (k
 // found, or the first unused slot) with its value kk, and the last dummy seen before it
 // (freeslot, -1 if none).  From i = hash & mask the 10 slots i .. i + 9 when they fit
@@ -1590,7 +1599,8 @@ __host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint3
     kk_out = kk;
 }
 
-__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h) {
+__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h,
+                                       FsetRef ltmp = FsetRef{}) {
     const uint32_t mask = *t.mask;
     uint32_t e;
     int16_t kk;
@@ -1616,12 +1626,19 @@ __host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool
     t.at(e) = k;
     t.mark(e);
     if ((uint64_t)*t.fill * 5 < (uint64_t)mask * 3) return true;
-#if defined(BK_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
-    atomicAdd(&g_sections[15], 1ull);  // diagnostic: resizes
-#endif
     if (t.dirty) *t.dirty = ~0u;  // every slot is rewritten
     const uint32_t minused = *t.used > 50000 ? *t.used * 2u : *t.used * 4u;
-    return tmp ? fs_resize(t, tmp, minused) : fs_resize_inplace(t, minused);
+#if defined(BK_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    // diagnostic (section slot 15): wave cycles in resizes, counted by the first lane of
+    // each resize branch
+    const uint64_t rt0 = clock64();
+    const bool rok = ltmp.key ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
+    const uint64_t rex = __builtin_amdgcn_read_exec();
+    if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(rex)) atomicAdd(&g_sections[15], clock64() - rt0);
+    return rok;
+#else
+    return ltmp.key ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
+#endif
 }
 
 __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
@@ -1710,7 +1727,8 @@ __host__ __device__ inline bool fs_copy(FsetRef d, const int16_t* skey, uint32_t
 // Run the ops marked in `real` (frontier_ops) on table t, in order: one probe routine in
 // a per-lane loop, so a wave runs as many probe chains as its busiest lane has real ops
 // (typically ~10) instead of all 45.  false: table overflow.
-__device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_t (&cells)[5], uint64_t real) {
+__device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_t (&cells)[5], uint64_t real,
+                                           FsetRef ltmp = FsetRef{}) {
     // key offset + 21 of op o, 6 bits each: 0, -21, -19, 19, 21, -20, 20, -1, 1
     constexpr uint64_t KD = (21ull << 0) | (0ull << 6) | (2ull << 12) | (40ull << 18) | (42ull << 24) |
                             (1ull << 30) | (41ull << 36) | (20ull << 42) | (22ull << 48);
@@ -1729,9 +1747,20 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
         // (loading the next ops' hashes ahead, 3 or 6 in flight, measured slower:
         // 34.2 -> 33.6 M frontier-order playouts/s, profiles/r05/sweeps/r05g)
         const uint64_t h = t.hash[key];
-        if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h)) return false;
+        if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h, ltmp)) return false;
     }
     return true;
+}
+
+// the LDS scratch of fs_resize_lds: this lane's [slot pair][lane] column from ltk (none:
+// nullptr)
+__device__ __forceinline__ FsetRef lds_tmp(int16_t* ltk) {
+    FsetRef r{};
+    if (BK_RESIZE_LDS && ltk) {
+        r.key = ltk;
+        r.stride = 2 * WAVE;
+    }
+    return r;
 }
 
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch.
@@ -1812,10 +1841,12 @@ struct NoMark {
 // mark(i): section boundaries for the diagnostic build (-DBK_SECTION_PROF)
 // hdr: player p's (mask, fill, used) when kept outside the record (the rollout slab);
 // nullptr: the record's own header
+// ltk: an LDS column for fs_resize_lds's scratch (STAGE / 4 keys, [slot pair][lane]), or
+// nullptr (resizes go through the record's global tmp)
 template <int STAGE, bool RECOPY = false, typename Mark = NoMark>
 __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, const uint64_t* htab,
                                                const int32_t (&cells)[5], uint64_t real, Mark mark = Mark(),
-                                               uint16_t* hdr = nullptr) {
+                                               uint16_t* hdr = nullptr, int16_t* ltk = nullptr) {
     bk_fset* gfs = &fl->s;
     uint16_t* const hm = hdr ? hdr : &gfs->mask[p];
     uint16_t* const hf = hdr ? hdr + 1 : &gfs->fill[p];
@@ -1848,7 +1879,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
         uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab, 1, &dirty};
         mark(8);
-        const bool ran = fs_run_ops(t, nullptr, cells, real);
+        const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk));
         mark(9);
         if (ran) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
@@ -1902,13 +1933,14 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 // cooperative kernels' one-per-wave stage, a plain array: 2)
 template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4, typename Mark = NoMark>
 __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* stage_q, const uint64_t* htab,
-                                                   const int32_t (&cells)[5], uint64_t real, Mark mark = Mark()) {
+                                                   const int32_t (&cells)[5], uint64_t real, Mark mark = Mark(),
+                                                   int16_t* ltk = nullptr) {
     bk_fset* gfs = &fl->s;
     const uint16_t m0 = gfs->mask[p], f0 = gfs->fill[p], u0 = gfs->used[p];
     uint16_t m = m0, f = f0, u = u0;
     uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
     FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4, &dirty};
-    const bool ran = fs_run_ops(t, nullptr, cells, real);
+    const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk));
     mark(5);
     if (ran) {
         bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
@@ -2997,8 +3029,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             // (staging every table of <= 128 slots in packed per-lane segments of the area,
             // so no lane probes its table in global memory, measured slower: 34.2 -> 31.7 M
             // playouts/s, profiles/r05/sweeps/r05i: the kernel is issue-bound, not waiting)
-            if (!place_frontier<HEUR ? 128 : BK_FS_STAGE_FR>(&a.fslab[slot], p, lk, htab, cells, real, mark,
-                                                              slab_hdr(slab, p)))
+            // resize scratch: the area's dwords after the stage (FR: 32..39, HEUR: 64..83)
+            constexpr int STG = HEUR ? 128 : BK_FS_STAGE_FR;
+            static_assert(STG / 2 + STG / 8 <= AREA / WAVE, "the resize scratch fits the area");
+            if (!place_frontier<STG>(&a.fslab[slot], p, lk, htab, cells, real, mark, slab_hdr(slab, p),
+                                     lk + 2 * WAVE * (STG / 2)))
                 g.status |= 2u;
         }
         SECT(6);
@@ -3399,7 +3434,9 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
         }
     }
     mark(4);
-    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real, mark)
+    // (the DMA stage leaves this lane's LDS column free for the resize scratch; the
+    // 128-slot stage in the column itself does not)
+    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real, mark, lk)
                             : place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
@@ -3918,14 +3955,12 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         const uint64_t real = frontier_ops(rows_lds, slab, p, (m.first >> p) & 1u, gs, ar, ac, pm);
         SECT(3);
 #ifdef BK_SECTION_PROF
-        {  // diagnostic counts (not cycles): [6] places per wave, [7] real ops, [15] wave max of real ops
-            uint32_t c = (uint32_t)__popcll(real), cm = c, cs = c;
+        {  // diagnostic counts (not cycles): [6] placements (wave steps), [7] their real ops
+            uint32_t cs = (uint32_t)__popcll(real);
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                cm = max(cm, (uint32_t)__shfl_xor((int)cm, o));
-                cs += (uint32_t)__shfl_xor((int)cs, o);
-            }
-            sect_acc[6] += 1; sect_acc[7] += cs; sect_acc[14] += 0 * cm;
+            for (int o = 32; o >= 1; o >>= 1) cs += (uint32_t)__shfl_xor((int)cs, o);
+            sect_acc[6] += 1;
+            sect_acc[7] += cs;
         }
 #endif
         // MCTSNode.expand (mcts_agent.py:113-145) places on new_board = board.copy() (B),
@@ -5404,10 +5439,13 @@ int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add) {
     if (!s || player < 0 || player > 3 || key < 0 || key >= BK_CELLS || s->mask[player] + 1u > BK_FSET_SLOTS)
         return BK_EINVAL;
     int16_t tmp[BK_FSET_SLOTS];
-    // add bit 1: resize in place (fs_resize_inplace, the staged kernels' path; <= 128 slots)
-    return fs_op(fs_ref(s, player, kCellHashHost), (add & 2) ? nullptr : tmp, (int16_t)key, (add & 1) != 0)
-               ? BK_OK
-               : BK_EOVERFLOW;
+    // add bit 1: the staged kernels' resize (fs_resize_lds, tables of <= 128 slots)
+    FsetRef t = fs_ref(s, player, kCellHashHost), lt{};
+    if (add & 2) {
+        t.cap = 128;
+        lt.key = tmp;
+    }
+    return fs_op_h(t, tmp, (int16_t)key, (add & 1) != 0, kCellHashHost[key], lt) ? BK_OK : BK_EOVERFLOW;
 }
 
 int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {

@@ -14,12 +14,13 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "tools", "_prof", "libblokus_hip_sections.so")
+LIB = os.environ.get("BK_SECTIONS_LIB") or os.path.join(ROOT, "tools", "_prof", "libblokus_hip_sections.so")
 
 NAMES = {0: "loop tail", 1: "game start/finish", 2: "derive+movegen counts", 3: "draw+pick+rows->LDS",
          4: "locate", 5: "apply", 6: "frontier place", 8: "mcts: tree select/replay/backprop/start",
          9: "mcts: derive+movegen", 10: "mcts: expand bookkeeping/draw+pick", 11: "mcts: locate_frontier",
-         12: "mcts: expand place/copies/TT", 13: "mcts: loop tail", 14: "mcts: rollout place"}
+         12: "mcts: expand place/copies/TT", 13: "mcts: loop tail", 14: "mcts: rollout place",
+         15: "(resizes, inside the set ops: not a section)"}
 
 
 # k_rollout_fr's frontier place, split (the place_frontier marks)
@@ -54,7 +55,7 @@ def run():
         tot = sum(buf)
         nm = {**NAMES, **(names or {})}
         rows = {nm.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
-        print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows}), flush=True)
+        print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows, "raw": list(buf)}), flush=True)
 
     L.bk_debug_sections(gpu.handle._h, buf, 16, 1)
     G, R = 256, 1024
