@@ -1599,8 +1599,9 @@ __host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint3
     kk_out = kk;
 }
 
-__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h,
-                                       FsetRef ltmp = FsetRef{}) {
+// the set operation without its resize: true when the add filled the table to the resize
+// threshold (the caller then runs fs_resize_any before the next operation)
+__host__ __device__ inline bool fs_op_nr(FsetRef t, int16_t k, bool add, uint64_t h) {
     const uint32_t mask = *t.mask;
     uint32_t e;
     int16_t kk;
@@ -1612,20 +1613,24 @@ __host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool
             t.mark(e);
             *t.used -= 1;
         }
-        return true;
+        return false;
     }
-    if (!add) return true;
+    if (!add) return false;
     if (freeslot >= 0) {
         *t.used += 1;
         t.at((uint32_t)freeslot) = k;
         t.mark((uint32_t)freeslot);
-        return true;
+        return false;
     }
     *t.fill += 1;
     *t.used += 1;
     t.at(e) = k;
     t.mark(e);
-    if ((uint64_t)*t.fill * 5 < (uint64_t)mask * 3) return true;
+    return (uint64_t)*t.fill * 5 >= (uint64_t)mask * 3;
+}
+
+// set_table_resize after an add reached the threshold (set_add_entry's resize call)
+__host__ __device__ inline bool fs_resize_any(FsetRef t, int16_t* tmp, FsetRef ltmp) {
     if (t.dirty) *t.dirty = ~0u;  // every slot is rewritten
     const uint32_t minused = *t.used > 50000 ? *t.used * 2u : *t.used * 4u;
 #if defined(BK_SECTION_PROF) && defined(__HIP_DEVICE_COMPILE__)
@@ -1639,6 +1644,11 @@ __host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool
 #else
     return ltmp.key ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
 #endif
+}
+
+__host__ __device__ inline bool fs_op_h(FsetRef t, int16_t* tmp, int16_t k, bool add, uint64_t h,
+                                       FsetRef ltmp = FsetRef{}) {
+    return !fs_op_nr(t, k, add, h) || fs_resize_any(t, tmp, ltmp);
 }
 
 __host__ __device__ inline bool fs_op(FsetRef t, int16_t* tmp, int16_t k, bool add) {
@@ -1738,18 +1748,32 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
         const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
         return cell + (int)((KD >> (6 * op)) & 63ull) - 21;
     };
+    // A lane whose add reaches the resize threshold leaves the op loop; once every lane of
+    // the wave has finished or stopped there, the resizes run together (one pass of the
+    // resize code per round instead of one per op iteration that has a resizing lane:
+    // ~6 lanes of a wave resize a table per frontier-order ply), then the ops go on.
+    bool ok = true;
 #pragma unroll 1
-    while (real) {
-        const int s = (int)__builtin_ctzll(real);
-        real &= real - 1ull;
-        const int op = s - 9 * ((s * 57) >> 9);
-        const int key = key_of(s);
-        // (loading the next ops' hashes ahead, 3 or 6 in flight, measured slower:
-        // 34.2 -> 33.6 M frontier-order playouts/s, profiles/r05/sweeps/r05g)
-        const uint64_t h = t.hash[key];
-        if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, h, ltmp)) return false;
+    for (;;) {
+        bool need = false;
+#pragma unroll 1
+        while (real && !need) {
+            const int s = (int)__builtin_ctzll(real);
+            real &= real - 1ull;
+            const int op = s - 9 * ((s * 57) >> 9);
+            const int key = key_of(s);
+            // (loading the next ops' hashes ahead, 3 or 6 in flight, measured slower:
+            // 34.2 -> 33.6 M frontier-order playouts/s, profiles/r05/sweeps/r05g)
+            const uint64_t h = t.hash[key];
+            need = fs_op_nr(t, (int16_t)key, (unsigned)(op - 1) < 4u, h);
+        }
+        if (need && !fs_resize_any(t, tmp, ltmp)) {
+            ok = false;  // the table outgrew this storage: the caller starts over elsewhere
+            real = 0;
+        }
+        if (__builtin_amdgcn_ballot_w64(real != 0ull) == 0ull) break;
     }
-    return true;
+    return ok;
 }
 
 // the LDS scratch of fs_resize_lds: this lane's [slot pair][lane] column from ltk (none:
