@@ -1494,13 +1494,15 @@ __host__ __device__ __forceinline__ uint32_t fs_clean_slot(uint64_t h, uint32_t 
     return e;
 }
 
-// set_table_resize for a table staged in LDS, with a small LDS scratch `tmp` (FsetRef
-// layout, at least cap / 4 keys): the active keys, read 16 slots at a time (the reads
+// set_table_resize through a small LDS scratch `tmp` (FsetRef layout; the caller checks
+// that tmp.cap >= used keys): the active keys, read 16 slots at a time (the reads
 // issued together), go to tmp in slot order; the table is cleared and they are
 // re-inserted with their slots from a register occupancy bitmap (fs_clean_slot:
 // set_insert_clean's probe sequence), 8 keys and their cell hashes loaded at a time.  A
 // resize that stays within the storage has used * 4 < newsize <= cap, so tmp never holds
-// more than cap / 4 keys.  Equal to fs_resize slot for slot (tests/test_fset_copy.py
+// more than cap / 4 keys.  The table itself may be staged in LDS or in global memory (a
+// table too large for the stage: its slots are read 16 at a time as well).  Equal to
+// fs_resize slot for slot (tests/test_fset_copy.py
 // through bk_debug_fset_op).  fs_resize instead copies every slot to the record's tmp in
 // global memory and re-inserts one dependent memory latency at a time: resizes were ~86 %
 // of k_rollout_fr's set-operation time and ~90 % of k_mcts_pair's
@@ -1637,12 +1639,12 @@ __host__ __device__ inline bool fs_resize_any(FsetRef t, int16_t* tmp, FsetRef l
     // diagnostic (section slot 15): wave cycles in resizes, counted by the first lane of
     // each resize branch
     const uint64_t rt0 = clock64();
-    const bool rok = ltmp.key ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
+    const bool rok = ltmp.key && *t.used <= ltmp.cap ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
     const uint64_t rex = __builtin_amdgcn_read_exec();
     if ((uint32_t)__lane_id() == (uint32_t)__builtin_ctzll(rex)) atomicAdd(&g_sections[15], clock64() - rt0);
     return rok;
 #else
-    return ltmp.key ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
+    return ltmp.key && *t.used <= ltmp.cap ? fs_resize_lds(t, ltmp, minused) : fs_resize(t, tmp, minused);
 #endif
 }
 
@@ -1776,13 +1778,14 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
     return ok;
 }
 
-// the LDS scratch of fs_resize_lds: this lane's [slot pair][lane] column from ltk (none:
-// nullptr)
-__device__ __forceinline__ FsetRef lds_tmp(int16_t* ltk) {
+// the LDS scratch of fs_resize_lds: this lane's [slot pair][lane] column from ltk, room
+// for `keys` keys (none: nullptr)
+__device__ __forceinline__ FsetRef lds_tmp(int16_t* ltk, uint32_t keys) {
     FsetRef r{};
     if (BK_RESIZE_LDS && ltk) {
         r.key = ltk;
         r.stride = 2 * WAVE;
+        r.cap = keys;
     }
     return r;
 }
@@ -1903,7 +1906,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
         uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
         FsetRef t{lk, 2 * WAVE, &m, &f, &u, (uint32_t)STAGE, htab, 1, &dirty};
         mark(8);
-        const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk));
+        const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk, STAGE / 4));
         mark(9);
         if (ran) {
             bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
@@ -1937,8 +1940,10 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
             return true;
         }
     }
+    // (a table too large for the stage: its resizes use the lane's whole column of the
+    // area, STAGE keys, as their scratch -- the stage is not in use)
     const FsetRef gt{gfs->key[p], 2, hm, hf, hu, BK_FSET_SLOTS, htab};
-    if (!fs_run_ops(gt, fl->tmp, cells, real)) return false;
+    if (!fs_run_ops(gt, fl->tmp, cells, real, lds_tmp(ltk ? lk : nullptr, (uint32_t)STAGE))) return false;
     if constexpr (RECOPY) return fs_recopy_global(fl, p, htab);  // (MCTS records: hdr is nullptr)
     return true;
 }
@@ -1964,7 +1969,7 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
     uint16_t m = m0, f = f0, u = u0;
     uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
     FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4, &dirty};
-    const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk));
+    const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk, 32u));
     mark(5);
     if (ran) {
         bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
@@ -2001,7 +2006,7 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
         }
         return true;
     }
-    if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real)) return false;
+    if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real, lds_tmp(ltk, 80u))) return false;
     return RECOPY ? fs_recopy_global(fl, p, htab) : true;
 }
 
