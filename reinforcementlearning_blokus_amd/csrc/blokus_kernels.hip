@@ -1739,6 +1739,9 @@ __host__ __device__ inline bool fs_copy(FsetRef d, const int16_t* skey, uint32_t
 // Run the ops marked in `real` (frontier_ops) on table t, in order: one probe routine in
 // a per-lane loop, so a wave runs as many probe chains as its busiest lane has real ops
 // (typically ~10) instead of all 45.  false: table overflow.
+// BATCH false: every lane of the wave runs the same table (the cooperative kernels), so
+// resizes run inline
+template <bool BATCH = true>
 __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_t (&cells)[5], uint64_t real,
                                            FsetRef ltmp = FsetRef{}) {
     // key offset + 21 of op o, 6 bits each: 0, -21, -19, 19, 21, -20, 20, -1, 1
@@ -1750,6 +1753,17 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
         const int cell = q == 0 ? cells[0] : q == 1 ? cells[1] : q == 2 ? cells[2] : q == 3 ? cells[3] : cells[4];
         return cell + (int)((KD >> (6 * op)) & 63ull) - 21;
     };
+    if constexpr (!BATCH) {
+#pragma unroll 1
+        while (real) {
+            const int s = (int)__builtin_ctzll(real);
+            real &= real - 1ull;
+            const int op = s - 9 * ((s * 57) >> 9);
+            const int key = key_of(s);
+            if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, t.hash[key], ltmp)) return false;
+        }
+        return true;
+    }
     // A lane whose add reaches the resize threshold leaves the op loop; once every lane of
     // the wave has finished or stopped there, the resizes run together (one pass of the
     // resize code per round instead of one per op iteration that has a resizing lane:
@@ -1969,7 +1983,8 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
     uint16_t m = m0, f = f0, u = u0;
     uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
     FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4, &dirty};
-    const bool ran = fs_run_ops(t, fl->tmp, cells, real, lds_tmp(ltk, 32u));
+    constexpr bool BATCH = RUN_U4 != 2;  // (RUN_U4 2: the cooperative kernels' one stage per wave)
+    const bool ran = fs_run_ops<BATCH>(t, fl->tmp, cells, real, lds_tmp(ltk, 32u));
     mark(5);
     if (ran) {
         bk_u4_alias* dst4 = reinterpret_cast<bk_u4_alias*>(gfs->key[p]);
@@ -2006,7 +2021,7 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
         }
         return true;
     }
-    if (!fs_run_ops(fs_ref(gfs, p, htab), fl->tmp, cells, real, lds_tmp(ltk, 80u))) return false;
+    if (!fs_run_ops<BATCH>(fs_ref(gfs, p, htab), fl->tmp, cells, real, lds_tmp(ltk, 80u))) return false;
     return RECOPY ? fs_recopy_global(fl, p, htab) : true;
 }
 
@@ -3455,17 +3470,28 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
                                                 int16_t* stage_q = nullptr, Mark mark = Mark()) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
+    {  // every row load issued before any store (one memory latency, not one per row)
+        uint32_t ow[5], oc[5];
 #pragma unroll
-    for (int d = 0; d < 5; ++d) {
-        if (pm[d]) {
-            slab.at(p, ar + d) |= pm[d];
-            slab.at(4, ar + d) |= pm[d];
+        for (int d = 0; d < 5; ++d) {
+            ow[d] = pm[d] ? slab.at(p, ar + d) : 0u;
+            oc[d] = pm[d] ? slab.at(4, ar + d) : 0u;
+        }
+#pragma unroll
+        for (int d = 0; d < 5; ++d) {
+            if (pm[d]) {
+                slab.at(p, ar + d) = ow[d] | pm[d];
+                slab.at(4, ar + d) = oc[d] | pm[d];
+            }
         }
     }
     mark(4);
-    // (the DMA stage leaves this lane's LDS column free for the resize scratch; the
-    // 128-slot stage in the column itself does not)
-    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real, mark, lk)
+    // (k_mcts_pair's DMA stage leaves this lane's LDS column free for the resize scratch;
+    // the 128-slot stage in the column itself does not.  The cooperative kernels, RUN_U4
+    // 2, resize through the record's tmp: the scratch measured 1-2 % slower there,
+    // profiles/r05/sweeps/r05u)
+    const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real, mark,
+                                                                 RUN_U4 == 2 ? nullptr : lk)
                             : place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
