@@ -645,7 +645,6 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     # BK_ARENA_CAPTURE=<dir> (diagnostics): keep every search launch's inputs; a launch
     # that returns a failed search is saved there and replayed alone (_capture_failed_job)
     capture_dir = os.environ.get("BK_ARENA_CAPTURE", "")
-    drop_nodes = os.environ.get("BK_ARENA_DROP_NODES", "0") != "0"  # A/B of the round-4 lifetime (diagnostics)
     fast_eng = BlokusGPU(device) if pipeline else gpu
     inflight = np.zeros(n, bool)
 
@@ -692,7 +691,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         inflight[games] = True
         # nodes stays referenced until the job is finished: the launch is asynchronous
         jobs.append({"slot": slot, "games": games, "aid": aid, "o_d": o_d, "tc": tt[2], "done": done,
-                     "t0": time.perf_counter(), "nodes": None if drop_nodes else nodes, "cap": cap_in, "seq": tl["mcts_jobs_launched"],
+                     "t0": time.perf_counter(), "nodes": nodes, "cap": cap_in, "seq": tl["mcts_jobs_launched"],
                      "key": (iters, roll, c, use_tt, policy), "inflight_at_launch": len(jobs)})
         tl["mcts_jobs_launched"] += 1
         if not pipeline:
