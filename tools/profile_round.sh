@@ -5,7 +5,7 @@
 #   2. one PMC pass per counter group (FETCH_SIZE / WRITE_SIZE / SQ_*), each its own
 #      rocprofv3 run with --kernel-trace only (never with sys/runtime traces)
 # Then, in the build container: python tools/summarize_prof.py gpurun_out/$TAG/<w> \
-#   r04/<name> <kernel> --units <units per launch> --unit <unit> [--keep-first]
+#   r05/<name> <kernel> --units <units per launch> --unit <unit> [--keep-first]
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -u
 TAG=${1:-prof}
@@ -15,8 +15,8 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 step() { local rc=$1; shift; echo "$* rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 declare -A ARGS
-ARGS[config3]="--steps 5 --warmup 1 --no-cpu-baseline"
-ARGS[config3fr]="--order frontier --steps 5 --warmup 1 --no-cpu-baseline"
+ARGS[config3]="--steps 5 --warmup 1 --no-cpu-baseline --no-frontier-order"
+ARGS[config3fr]="--order frontier --steps 5 --warmup 1 --no-cpu-baseline --no-frontier-order"
 ARGS[config2]="--workload config2 --steps 50 --warmup 2 --no-cpu-baseline"
 ARGS[config5]="--workload config5 --steps 1 --warmup 0 --no-cpu-baseline"
 ARGS[config4]="--workload config4 --games 1024 --steps 1 --warmup 0 --no-cpu-baseline"
