@@ -104,7 +104,11 @@ def run_mcts():
         rows = {nm.get(i, str(i)): round(buf[i] / tot, 4) for i in range(16) if buf[i]}
         print(json.dumps({"run": tag, **extra, "cycles": tot, "share": rows, "raw": list(buf)}), flush=True)
 
-    for games, iters, policy in ((65536, 512, N.MCTS_ROLLOUT_RANDOM), (4096, 96, N.MCTS_ROLLOUT_HEURISTIC)):
+    runs = ((65536, int(os.environ.get("BK_SECT_ITERS", "512")), N.MCTS_ROLLOUT_RANDOM),
+            (4096, 96, N.MCTS_ROLLOUT_HEURISTIC))
+    if os.environ.get("BK_SECT_ITERS"):
+        runs = runs[:1]
+    for games, iters, policy in runs:
         roots, sets = frontier_roots(gpu, games, 20, seed=11)
         b = MctsBatch(gpu, roots, sets, iterations=iters, seed0=3)
         gpu.mcts_device(b.roots, b.sets, b.players, b.root_hash, b.zobrist, b.zidx, b.mt, b.log_table, b.nodes,
