@@ -4311,19 +4311,22 @@ __device__ __forceinline__ void coop_list_moves(uint16_t* ml, uint32_t idx, uint
 #define COOP_MOVE_CAP 2048
 #define COOP_ML_DWORD (40 * WAVE)                        // after the rows' 40 dwords per lane
 #define COOP_CUM_DWORD (COOP_ML_DWORD + COOP_MOVE_CAP / 2)  // cumE[91], cumS[91] (doubles)
+template <typename Mark = NoMark>
 __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* area, int lane, const HeurShared* hs,
                                                    int edge_w, const uint32_t (&ok0)[20], const uint32_t (&ok1)[20],
                                                    const uint32_t (&cnt)[2], const CoopScan& sc, const uint32_t* st,
                                                    uint32_t& pos, uint32_t pre0, uint32_t pre1, double& target,
                                                    double& R, double& total, bool& uncertain, int& gs,
-                                                   uint32_t (&gok)[20]) {
+                                                   uint32_t (&gok)[20], Mark mark = Mark()) {
     const uint32_t n_moves = sc.total;
     if (n_moves > COOP_MOVE_CAP) return false;
     uint16_t* ml = reinterpret_cast<uint16_t*>(area + COOP_ML_DWORD);
     double* cumE = reinterpret_cast<double*>(area + COOP_CUM_DWORD);
     double* cumS = cumE + BK_NUM_ORIENTS;
+    mark(3);
     coop_list_moves(ml, sc.i0 - sc.c0, (uint32_t)lane, ok0);
     coop_list_moves(ml, sc.i1 - sc.c1, (uint32_t)(lane + WAVE), ok1);
+    mark(6);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -4353,6 +4356,7 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    mark(7);
     total = carry;
     // the HeuristicAgent's draw (random_sample), as coop_heur_pick
     double u;
@@ -4638,9 +4642,14 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         bool h_unc = false;
         if (hroll) {
             uint32_t* st = a.mt + (size_t)m.game * (FM_N + 1);
+#ifdef BK_SECTION_PROF
+            auto cmark = [&](int i) { SECT(i); };
+#else
+            NoMark cmark;
+#endif
             if (!a.coop_balanced ||
                 !coop_heur_balanced(rows_lds - lane, my, lane, hs, edge_w, okA, okB, cnt, sc, st, m.mt_pos, h_pre0,
-                                    h_pre1, h_target, h_R, h_total, h_unc, gs, h_ok)) {
+                                    h_pre1, h_target, h_R, h_total, h_unc, gs, h_ok, cmark)) {
                 // more legal moves than the list holds: per-lane orientation sums
                 es[0] = cnt[0] ? lane_orient_sum(lane, okA, rows_lds, hs, edge_w) : 0.0;
                 es[1] = cnt[1] ? lane_orient_sum(lane + WAVE, okB, rows_lds, hs, edge_w) : 0.0;
