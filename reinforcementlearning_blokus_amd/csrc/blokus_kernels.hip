@@ -165,6 +165,23 @@ constexpr FopsTable make_fops_first() {
 }
 __constant__ FopsTable kFopsFirst = make_fops_first();
 
+// The picked orientation's table entries (kInfo, kCells, kFopsFirst), loaded once per ply
+// with the loads issued together right after the pick, for locate / apply / the frontier
+// update, which otherwise each reload them (a dependent memory latency apiece)
+struct OrientRow {
+    uint32_t info;
+    uint32_t cell[5];
+    uint64_t ffirst;
+};
+__device__ __forceinline__ OrientRow orient_row(int gs) {
+    OrientRow o;
+    o.info = kInfo[gs];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) o.cell[q] = kCells[gs][q];
+    o.ffirst = kFopsFirst.m[gs];
+    return o;
+}
+
 // ------------------------------------------------------------------------------------
 // state <-> rows
 // ------------------------------------------------------------------------------------
@@ -601,15 +618,16 @@ __device__ __forceinline__ void locate_move(int gs, uint32_t kk, const uint32_t 
 // selects.  Cells beyond the orientation's count repeat cell 0 (ORing a term twice is
 // harmless).  Anchor rows past 20 - height cannot hold the piece: they are evaluated
 // at the last valid row (so every read stays in rows 0..19) and then dropped.
-__device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2* rows, int& out_r, int& out_c) {
-    const uint32_t info = kInfo[gs];
+__device__ __forceinline__ void locate_move_lds(const OrientRow& orow, uint32_t kk, const uint2* rows, int& out_r,
+                                                int& out_c) {
+    const uint32_t info = orow.info;
     const int n = (int)((info >> 8) & 0xFFu);
     const int rlim = 20 - (int)((info >> 16) & 0xFFu);
     const uint2* base[5];
     uint32_t sh[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        const uint32_t cell = k < n ? orow.cell[k] : orow.cell[0];
         base[k] = rows + (cell >> 8) * WAVE;
         sh[k] = cell & 0xFFu;
     }
@@ -640,6 +658,9 @@ __device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2
     }
     out_r = found_r;
     out_c = found_c;
+}
+__device__ __forceinline__ void locate_move_lds(int gs, uint32_t kk, const uint2* rows, int& out_r, int& out_c) {
+    locate_move_lds(orient_row(gs), kk, rows, out_r, out_c);
 }
 
 // Frontier-order variant (BK_ORDER_FRONTIER): the kk-th anchor of orientation gs in the
@@ -678,9 +699,9 @@ __device__ __forceinline__ void locate_pass1(int gs, uint2* rows) {
 // RS: uint4 distance between 16-slot runs of the table (2: a plain array; 64: the lane
 // pair's LDS-DMA stage of k_mcts_pair)
 template <int RS = 2>
-__device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2* rows, const int16_t* key,
-                                                     int mask, int& out_r, int& out_c) {
-    const uint32_t info = kInfo[gs];
+__device__ __forceinline__ void locate_move_frontier(const OrientRow& orow, uint32_t kk, uint2* rows,
+                                                     const int16_t* key, int mask, int& out_r, int& out_c) {
+    const uint32_t info = orow.info;
     const int n = (int)((info >> 8) & 0xFFu);
     const int rlim = 20 - (int)((info >> 16) & 0xFFu);
     const uint2* base[5];
@@ -688,7 +709,7 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
     int cd[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        const uint32_t cell = k < n ? orow.cell[k] : orow.cell[0];
         base[k] = rows + (cell >> 8) * WAVE;
         sh[k] = cell & 0xFFu;
         cd[k] = (int)(cell >> 8);
@@ -794,6 +815,11 @@ __device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2*
     }
     out_r = found_r;
     out_c = found_c;
+}
+template <int RS = 2>
+__device__ __forceinline__ void locate_move_frontier(int gs, uint32_t kk, uint2* rows, const int16_t* key, int mask,
+                                                     int& out_r, int& out_c) {
+    locate_move_frontier<RS>(orient_row(gs), kk, rows, key, mask, out_r, out_c);
 }
 
 // locate_move_frontier for a lane PAIR holding one search (k_mcts_pair): both lanes call
@@ -949,8 +975,8 @@ __device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2*
 // FROM_SLAB: the blocked rows are derived from the slab (occupancy and own rows before
 // the move) instead of read from the LDS rows (MCTS replay, where no movegen ran).
 template <bool FROM_SLAB = false>
-__device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& slab, int p, bool first, int gs,
-                                                 int ar, int ac, const uint32_t (&m)[5]) {
+__device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& slab, int p, bool first,
+                                                 const OrientRow& orow, int ar, int ac, const uint32_t (&m)[5]) {
     uint32_t o[9];  // own rows ar - 2 .. ar + 6 before the move
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
@@ -987,7 +1013,7 @@ __device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& 
     uint64_t real = 0;
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
-        const uint32_t cell = kCells[gs][q];  // entries past the piece's cells: masked below
+        const uint32_t cell = orow.cell[q];  // entries past the piece's cells: masked below
         const int sh = ((int)(cell >> 8) + 1) * 7 + (int)(cell & 0xFFu) + 1 - 8;
         const uint32_t tm = (uint32_t)(wm >> sh), ta = (uint32_t)(wa >> sh);
         const uint32_t code = ((tm >> 8) & 1u) | ((ta << 1) & 2u) | (ta & 4u) | ((ta >> 11) & 8u) |
@@ -995,12 +1021,17 @@ __device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& 
                               ((tm >> 1) & 256u);
         real |= (uint64_t)code << (9 * q);
     }
-    real &= kFopsFirst.m[gs];
+    real &= orow.ffirst;
     // the LDS rows of this lane are overwritten by other lanes' table staging right after
     // this call: every load above must complete first (no sinking past those stores)
     uint32_t lo = (uint32_t)real, hi = (uint32_t)(real >> 32);
     asm volatile("" : "+v"(lo), "+v"(hi) : : "memory");
     return ((uint64_t)hi << 32) | lo;
+}
+template <bool FROM_SLAB = false>
+__device__ __forceinline__ uint64_t frontier_ops(const uint2* rows, const Slab& slab, int p, bool first, int gs,
+                                                 int ar, int ac, const uint32_t (&m)[5]) {
+    return frontier_ops<FROM_SLAB>(rows, slab, p, first, orient_row(gs), ar, ac, m);
 }
 
 // ------------------------------------------------------------------------------------
@@ -2990,6 +3021,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             const uint32_t k = draw_index(a, g, slab, slot, total);
             gs = pick_orient(my, lane, k, kk);
         }
+        // the picked orientation's table entries (loads issued before the rows' LDS writes)
+        OrientRow orow = orient_row(gs < 0 ? 0 : gs);
         // counts are consumed: the area now takes the mover's rows for locate
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
@@ -3002,6 +3035,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                 gs = g.forced / 400;
                 ar = (g.forced % 400) / 20;
                 ac = g.forced % 20;
+                orow = orient_row(gs);
                 locate_pass1(gs, rows_lds);
                 if (!((rows_lds[ar * WAVE].y >> ac) & 1u)) ar = -1;
             } else if (heur && gs < 0) {
@@ -3013,10 +3047,10 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
                                    ar, ac, h_unc);
                 if (h_unc) g.status |= BK_STATUS_UNCERT;
             } else {
-                locate_move_frontier(gs, kk, rows_lds, fs->key[p], fmask, ar, ac);
+                locate_move_frontier(orow, kk, rows_lds, fs->key[p], fmask, ar, ac);
             }
         } else {
-            locate_move_lds(gs, kk, rows_lds, ar, ac);
+            locate_move_lds(orow, kk, rows_lds, ar, ac);
         }
         if (HEUR && ar < 0) {  // cannot happen (counts > 0 means e sums > 0); never write off the board
             g.status |= forced ? BK_STATUS_BADFORCE : BK_STATUS_UNCERT;
@@ -3026,13 +3060,13 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
         if constexpr (HEUR) g.forced = -1;  // consumed
         SECT(4);
         // ---- apply (engine/board.py:515-555): own plane, occupancy, used, first, score
-        const uint32_t info = kInfo[gs];
+        const uint32_t info = orow.info;
         const int n = (int)((info >> 8) & 0xFFu);
         // per piece row d: one mask; all row loads issued before any store
         uint32_t m[5] = {0u, 0u, 0u, 0u, 0u};
 #pragma unroll
         for (int q = 0; q < 5; ++q) {
-            const uint32_t cell = kCells[gs][q];
+            const uint32_t cell = orow.cell[q];
             const uint32_t bit = q < n ? (1u << (ac + (int)(cell & 0xFFu))) : 0u;
 #pragma unroll
             for (int d = 0; d < 5; ++d) m[d] |= ((cell >> 8) == (uint32_t)d) ? bit : 0u;
@@ -3057,11 +3091,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
             int32_t cells[5];
 #pragma unroll
             for (int q = 0; q < 5; ++q) {
-                const uint32_t cell = kCells[gs][q < n ? q : 0];
+                const uint32_t cell = q < n ? orow.cell[q] : orow.cell[0];
                 cells[q] = (ar + (int)(cell >> 8)) * 20 + ac + (int)(cell & 0xFFu);
             }
             // before the table staging reuses the area
-            const uint64_t real = frontier_ops(rows_lds, slab, p, (g.first >> p) & 1u, gs, ar, ac, m);
+            const uint64_t real = frontier_ops(rows_lds, slab, p, (g.first >> p) & 1u, orow, ar, ac, m);
             SECT(7);
             int16_t* lk = reinterpret_cast<int16_t*>(lds + wv * AREA) + 2 * lane;
             // (HEUR: the area holds 84 dwords per lane, a 128-slot stage fits)
