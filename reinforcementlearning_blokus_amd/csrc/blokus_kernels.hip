@@ -401,6 +401,10 @@ struct StencilClass {
 #ifndef FR_BLOCKS_PER_CU
 #define FR_BLOCKS_PER_CU 4
 #endif
+// tables probed in global memory read 8-slot chunks (FsetRef::gchunk, fs_probe)
+#ifndef BK_GLOBAL_CHUNK
+#define BK_GLOBAL_CHUNK 1
+#endif
 // LDS-staged frontier tables resize through an LDS scratch (fs_resize_lds) where the
 // caller has one; 0: always through the record's global tmp (fs_resize)
 #ifndef BK_RESIZE_LDS
@@ -1448,6 +1452,7 @@ struct FsetRef {  // one player's table: runs of 2^sh slots, run j at key[j * st
     const uint64_t* hash = nullptr;  // hash((r, c)) by cell
     int sh = 1;       // log2 of the run length
     uint32_t* dirty = nullptr;  // if set: bit j marks 8-slot chunk j written (all: a resize)
+    bool gchunk = false;  // a plain array in global memory: probes read 8-slot chunks (fs_probe)
     __host__ __device__ __forceinline__ int16_t& at(uint32_t i) const {
         return key[(i >> sh) * (uint32_t)stride + (i & ((1u << sh) - 1u))];
     }
@@ -1607,6 +1612,9 @@ __host__ __device__ inline bool fs_resize(FsetRef t, int16_t* tmp, uint32_t minu
 // per step from the pair-stored tables measured slower (frontier-order config 3 34.1 ->
 // 33.2 / 33.0 M playouts/s, config 5 17.6 -> 17.1 / 17.0 M; profiles/r05/sweeps/r05f):
 // most chains end at their first or second slot.
+// t.gchunk (a table probed in global memory, k_rollout_fr's 128-slot tables): the probe
+// reads the 16-byte chunk holding slot e (8 slots, one memory latency) and walks the
+// linear run from registers, loading the next chunk only when the sequence leaves it.
 __host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint32_t mask, uint32_t& e_out,
                                          int16_t& kk_out, int32_t& freeslot) {
     uint64_t perturb = h;
@@ -1614,6 +1622,34 @@ __host__ __device__ inline void fs_probe(FsetRef t, int16_t k, uint64_t h, uint3
     uint32_t left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
     freeslot = -1;
     int16_t kk;
+    if (t.gchunk) {
+        const bk_u4_alias* k4 = reinterpret_cast<const bk_u4_alias*>(t.key);
+        uint32_t cb = e >> 3;
+        uint4 c = k4[cb];
+        for (;;) {
+            if ((e >> 3) != cb) {
+                cb = e >> 3;
+                c = k4[cb];
+            }
+            const uint32_t q = (e >> 1) & 3u;
+            const uint32_t w = q == 0u ? c.x : q == 1u ? c.y : q == 2u ? c.z : c.w;
+            kk = (int16_t)(w >> (16u * (e & 1u)));
+            if (kk == FS_UNUSED || kk == k) break;
+            if (kk == FS_DUMMY) freeslot = (int32_t)e;
+            if (left > 0u) {
+                --left;
+                ++e;
+            } else {
+                perturb >>= FS_SHIFT;
+                i = (i * 5u + 1u + (uint32_t)perturb) & mask;
+                e = i;
+                left = i + FS_PROBES <= mask ? FS_PROBES : 0u;
+            }
+        }
+        e_out = e;
+        kk_out = kk;
+        return;
+    }
     for (;;) {
         kk = t.at(e);
         if (kk == FS_UNUSED || kk == k) break;
@@ -1987,7 +2023,8 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     }
     // (a table too large for the stage: its resizes use the lane's whole column of the
     // area, STAGE keys, as their scratch -- the stage is not in use)
-    const FsetRef gt{gfs->key[p], 2, hm, hf, hu, BK_FSET_SLOTS, htab};
+    FsetRef gt{gfs->key[p], 2, hm, hf, hu, BK_FSET_SLOTS, htab};
+    gt.gchunk = BK_GLOBAL_CHUNK && ltk != nullptr;  // (the playout kernels: k_rollout_fr)
     if (!fs_run_ops(gt, fl->tmp, cells, real, lds_tmp(ltk ? lk : nullptr, (uint32_t)STAGE))) return false;
     if constexpr (RECOPY) return fs_recopy_global(fl, p, htab);  // (MCTS records: hdr is nullptr)
     return true;
