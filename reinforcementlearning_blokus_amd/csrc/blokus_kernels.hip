@@ -4212,6 +4212,9 @@ __global__ void k_mcts_h(MctsArgs a);
 // run both kernels on the same batches).
 // ------------------------------------------------------------------------------------
 #define COOP_WAVES 2                             // searches (waves) per block
+#ifndef BK_COOP_SLAB_LDS
+#define BK_COOP_SLAB_LDS 1  // the cooperative kernels keep the search's slab in LDS
+#endif
 #ifndef COOP_H_WAVES_PER_SIMD
 #define COOP_H_WAVES_PER_SIMD 1                  // k_mcts_coop_h waves per SIMD (2: <= 256 registers, spills)
 #endif
@@ -4584,6 +4587,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // the mover's table (<= 128 slots), one copy per wave, loaded by LDS-DMA while the
     // orientations are evaluated: locate / walk read it and the set operations run on it
     __shared__ __attribute__((aligned(16))) int16_t coop_stage[COOP_WAVES][16 * DMA_RUNS];
+    __shared__ __attribute__((aligned(16))) uint32_t coop_slab[COOP_WAVES][SLAB_WORDS];
     const bool coop_walk_on = a.coop_walk != 0;
     // the wave index is uniform (readfirstlane): the wave's LDS area, slab and McLane
     // addresses live in scalar registers
@@ -4595,7 +4599,9 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
     __syncthreads();
     const uint32_t slot = blockIdx.x * COOP_WAVES + wv;  // one slab / McLane per search
-    const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
+    // the search's board (the slab: planes, occupancy) lives in LDS, one per wave: it
+    // is rebuilt from the root at every iteration, so nothing outside the wave reads it
+    const Slab slab{BK_COOP_SLAB_LDS ? coop_slab[wv] : a.slab + (size_t)slot * SLAB_WORDS};
     McLane* L = a.lanes + slot;
     Mc m;
     m.game = -1;
