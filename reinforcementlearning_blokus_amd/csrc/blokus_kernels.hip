@@ -2042,15 +2042,17 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
 // back to the global table when the ops outgrow the stage.
 // RUN_U4: uint4 distance between 16-slot runs (k_mcts_pair's pair stage: 64; the
 // cooperative kernels' one-per-wave stage, a plain array: 2)
+// inplace: stage_q IS the record's table (k_mcts_coop_h's McLane in LDS): the ops run on
+// it directly with its full storage, and nothing is written back
 template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4, typename Mark = NoMark>
 __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* stage_q, const uint64_t* htab,
                                                    const int32_t (&cells)[5], uint64_t real, Mark mark = Mark(),
-                                                   int16_t* ltk = nullptr) {
+                                                   int16_t* ltk = nullptr, bool inplace = false) {
     bk_fset* gfs = &fl->s;
     const uint16_t m0 = gfs->mask[p], f0 = gfs->fill[p], u0 = gfs->used[p];
     uint16_t m = m0, f = f0, u = u0;
     uint32_t dirty = 0;  // 8-slot chunks the ops wrote: only those go back to the table
-    FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, 16u * DMA_RUNS, htab, 4, &dirty};
+    FsetRef t{stage_q, 8 * RUN_U4, &m, &f, &u, inplace ? (uint32_t)BK_FSET_SLOTS : 16u * DMA_RUNS, htab, 4, &dirty};
     constexpr bool BATCH = RUN_U4 != 2;  // (RUN_U4 2: the cooperative kernels' one stage per wave)
     const bool ran = fs_run_ops<BATCH>(t, fl->tmp, cells, real, lds_tmp(ltk, 32u));
     mark(5);
@@ -2059,11 +2061,13 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
         const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(stage_q);
         const uint32_t newsize = fs_copy_size(u);
         if (!RECOPY || (newsize - 1 == m && f == u)) {  // (a copy of a clean table is the table)
+            if (!inplace) {
 #pragma unroll
-            for (int r = 0; r < DMA_RUNS; ++r) {
-                if ((uint32_t)(16 * r) <= m) {
-                    if ((dirty >> (2 * r)) & 1u) dst4[2 * r] = src4[r * RUN_U4];
-                    if ((dirty >> (2 * r + 1)) & 1u) dst4[2 * r + 1] = src4[r * RUN_U4 + 1];
+                for (int r = 0; r < DMA_RUNS; ++r) {
+                    if ((uint32_t)(16 * r) <= m) {
+                        if ((dirty >> (2 * r)) & 1u) dst4[2 * r] = src4[r * RUN_U4];
+                        if ((dirty >> (2 * r + 1)) & 1u) dst4[2 * r + 1] = src4[r * RUN_U4 + 1];
+                    }
                 }
             }
             if (m != m0) gfs->mask[p] = m;
@@ -2071,6 +2075,7 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
             if (u != u0) gfs->used[p] = u;
             return true;
         }
+        // (never in place: the copy reads the stage while it rewrites the table)
         const uint4 unused = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
 #pragma unroll 1
         for (uint32_t i = 0; i < newsize / 8; ++i) dst4[i] = unused;
@@ -2089,6 +2094,7 @@ __device__ __forceinline__ bool place_frontier_dma(FsLane* fl, int p, int16_t* s
         }
         return true;
     }
+    if (inplace) return false;  // (the ops ran on the table: past its 256 slots)
     if (!fs_run_ops<BATCH>(fs_ref(gfs, p, htab), fl->tmp, cells, real, lds_tmp(ltk, 80u))) return false;
     return RECOPY ? fs_recopy_global(fl, p, htab) : true;
 }
@@ -3538,7 +3544,7 @@ template <bool RECOPY, int RUN_U4 = DMA_RUN_DWORDS / 4, typename Mark = NoMark>
 __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, int gs, int ar, FsLane* T,
                                                 const uint64_t* htab, const uint32_t (&pm)[5],
                                                 const int32_t (&cells)[5], uint64_t real, int16_t* lk,
-                                                int16_t* stage_q = nullptr, Mark mark = Mark()) {
+                                                int16_t* stage_q = nullptr, Mark mark = Mark(), bool inplace = false) {
     const uint32_t info = kInfo[gs];
     const int n = (int)((info >> 8) & 0xFFu);
     {  // every row load issued before any store (one memory latency, not one per row)
@@ -3562,7 +3568,7 @@ __device__ __forceinline__ bool mc_place_staged(Mc& m, const Slab& slab, int p, 
     // 2, resize through the record's tmp: the scratch measured 1-2 % slower there,
     // profiles/r05/sweeps/r05u)
     const bool ok = stage_q ? place_frontier_dma<RECOPY, RUN_U4>(T, p, stage_q, htab, cells, real, mark,
-                                                                 RUN_U4 == 2 ? nullptr : lk)
+                                                                 RUN_U4 == 2 ? nullptr : lk, inplace)
                             : place_frontier<BK_FS_STAGE_MCTS, RECOPY>(T, p, lk, htab, cells, real);
     m.cells.set(p, m.cells.get(p) + (uint32_t)n);
     m.used.set(p, m.used.get(p) | (1u << ((info & 0xFFu) - 1u)));
@@ -4212,6 +4218,9 @@ __global__ void k_mcts_h(MctsArgs a);
 // run both kernels on the same batches).
 // ------------------------------------------------------------------------------------
 #define COOP_WAVES 2                             // searches (waves) per block
+#ifndef BK_COOP_ML_LDS
+#define BK_COOP_ML_LDS 1  // k_mcts_coop_h keeps the search's McLane in LDS
+#endif
 #ifndef BK_COOP_SLAB_LDS
 #define BK_COOP_SLAB_LDS 1  // the cooperative kernels keep the search's slab in LDS
 #endif
@@ -4588,6 +4597,13 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // orientations are evaluated: locate / walk read it and the set operations run on it
     __shared__ __attribute__((aligned(16))) int16_t coop_stage[COOP_WAVES][16 * DMA_RUNS];
     __shared__ __attribute__((aligned(16))) uint32_t coop_slab[COOP_WAVES][SLAB_WORDS];
+    // k_mcts_coop_h: the search's McLane (frontier tables of the node / sim board, the
+    // root's tables, the path) lives in LDS too -- it is rebuilt at every search start,
+    // so no launch leaves anything in it for the next -- and the mover's table is then
+    // used in place (no LDS-DMA stage, no write-back).  (k_mcts_coop keeps it in HBM: the
+    // 4.9 KB per wave would cost it a block per CU.)
+    constexpr bool ML_LDS = HEUR && BK_COOP_ML_LDS;
+    __shared__ __attribute__((aligned(16))) McLane coop_ml[ML_LDS ? COOP_WAVES : 1];
     const bool coop_walk_on = a.coop_walk != 0;
     // the wave index is uniform (readfirstlane): the wave's LDS area, slab and McLane
     // addresses live in scalar registers
@@ -4602,7 +4618,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // the search's board (the slab: planes, occupancy) lives in LDS, one per wave: it
     // is rebuilt from the root at every iteration, so nothing outside the wave reads it
     const Slab slab{BK_COOP_SLAB_LDS ? coop_slab[wv] : a.slab + (size_t)slot * SLAB_WORDS};
-    McLane* L = a.lanes + slot;
+    McLane* L = ML_LDS ? &coop_ml[ML_LDS ? wv : 0] : a.lanes + slot;
     Mc m;
     m.game = -1;
     m.mode = MC_SELECT;
@@ -4660,11 +4676,13 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
 #pragma unroll
         for (int R = 0; R < 20; ++R) rows_lds[R * WAVE] = make_uint2(P.b(R), P.c(R));
         const bool staged = tmask < 16u * DMA_RUNS;  // uniform: one search per wave
-        if (staged) {
+        if (!ML_LDS && staged) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the table's last stores have landed
             if (lane < 16)  // 16 lanes x 16 bytes = the 128-slot table
                 __builtin_amdgcn_global_load_lds((const void*)(L->A.s.key[p] + 8 * lane), (void*)coop_stage[wv], 16, 0, 0);
         }
+        // (ML_LDS: the table itself, in LDS, is the stage)
+        int16_t* const stage_w = ML_LDS ? L->A.s.key[p] : coop_stage[wv];
         const uint32_t avail = ~m.used.get(p) & 0x1FFFFFu;
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         // Board.move_count of the rollout board: placements on the way from the root
@@ -4738,7 +4756,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         }
         FsLane* T = &L->A;  // the node board at expansion, the rollout's sim board after it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
-        const int16_t* tkey = staged ? coop_stage[wv] : T->s.key[p];
+        const int16_t* tkey = staged ? stage_w : T->s.key[p];
         int ar, ac;
         SECT(3);
         int16_t* rank = coop_rank[wv];
@@ -4794,9 +4812,19 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             pool[c] = ch;
             if (m.depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; m.mode = MC_SELECT; continue; }
         }
-        int16_t* sq = staged ? coop_stage[wv] : nullptr;
-        if (expand) ok &= mc_place_staged<true, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
-        else ok &= mc_place_staged<false, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq);
+        int16_t* sq = staged ? stage_w : nullptr;
+        bool inpl = false;
+        if constexpr (ML_LDS) {
+            if (staged && expand) {  // the expansion's copy needs the table as a separate stage
+                if (lane < 16)
+                    reinterpret_cast<uint4*>(coop_stage[wv])[lane] = reinterpret_cast<const uint4*>(T->s.key[p])[lane];
+                sq = coop_stage[wv];
+            } else {
+                inpl = staged;
+            }
+        }
+        if (expand) ok &= mc_place_staged<true, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, NoMark(), inpl);
+        else ok &= mc_place_staged<false, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, NoMark(), inpl);
         if (expand) {
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
