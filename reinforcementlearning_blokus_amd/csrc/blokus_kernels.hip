@@ -4622,6 +4622,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     Mc m;
     m.game = -1;
     m.mode = MC_SELECT;
+    int root_mc = 0;  // Board.move_count of the search's root
     // section timers (-DBK_SECTION_PROF): 0 tree, 1 derive + rows, 2 lane orientations +
     // scan, 3 draw + pick, 4 locate / heuristic walk, 5 frontier ops + place + expansion
     SECT_DECL
@@ -4644,6 +4645,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
                 next = __shfl(next, 0);
                 if (next >= a.n_games) { done = true; break; }
                 mc_start_game(a, m, L, next, htab);
+                root_mc = (int)a.roots[next].move_count;  // (constant for the search)
             }
             const bool timed_out = a.cfg.time_limit_us > 0 && wall_clock64() - m.t0 >= a.limit_ticks;
             const bool chunk_end = a.cfg.iter_stop > 0 && m.it >= a.cfg.iter_stop;
@@ -4686,7 +4688,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         const uint32_t avail = ~m.used.get(p) & 0x1FFFFFu;
         const bool hroll = HEUR && m.mode == MC_ROLLOUT;
         // Board.move_count of the rollout board: placements on the way from the root
-        const int edge_w = (int)(a.roots[m.game].move_count + m.depth + m.plies) < 30 ? 6 : 3;
+        const int edge_w = root_mc + m.depth + m.plies < 30 ? 6 : 3;
         uint32_t h_pre0 = 0u, h_pre1 = 0u;  // the heuristic draw's two MT words, loaded early
         if (hroll && m.mt_pos + 2u <= (uint32_t)FM_N) {
             const uint32_t* st = a.mt + (size_t)m.game * (FM_N + 1);
