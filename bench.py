@@ -67,6 +67,12 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 20; config5: 1)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default: 3; config5: 1, "
                                                               "a 64-iteration chunk)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="rehearsal of the N-rank path on a one-GPU box: every rank runs on cuda:0 and the "
+                         "process group is gloo (tests only; never a scaling number)")
+    ap.add_argument("--check-gather", action="store_true",
+                    help="config3, N ranks: rank 0 checks the gathered records against one launch of the "
+                         "whole job's games")
     ap.add_argument("--workload", choices=("config3", "config5", "config2", "config4"), default="config3")
     ap.add_argument("--games", type=int, default=None, help="config3: 256; config5: 65536; config4: 8192 (whole job)")
     ap.add_argument("--rollouts", type=int, default=1024)
@@ -286,11 +292,13 @@ def setup(args):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     import torch
     dist = None
+    if args.share_device:  # hardware rehearsal of the N-rank path on one GPU (RCCL wants one rank per GPU)
+        local = 0
     if not args.selftest:
         torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        if args.selftest:
+        if args.selftest or args.share_device:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -355,38 +363,11 @@ def _config3_measure(args, order, gpu, plan, dev, dist):
     CPython frontier-set tables), then per step 262,144 arena playouts (k_rollout /
     k_rollout_fr) on the plan's playout streams.  Timed region: barrier + synchronize on
     both sides; HIP events on the launching stream around every launch."""
-    import numpy as np
     import torch
 
-    from reinforcementlearning_blokus_amd import _native as N
-    from reinforcementlearning_blokus_amd.gpu import empty_state
-    games = plan.games
-    sets_np = sets = None
-    if order == "frontier":
-        roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), games,
-                                                 semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=plan.seed,
-                                                 max_plies=args.root_plies,
-                                                 root_index=np.zeros(games, dtype=np.int32),
-                                                 stream_base=plan.root_stream_base)
-        sets = torch.from_numpy(sets_np.view(np.uint8).reshape(games, -1).copy()).to(dev)
-    else:
-        roots_np = gpu.advance(empty_state(), games, args.root_plies, seed=plan.seed,
-                               root_index=np.zeros(games, dtype=np.int32), stream_base=plan.root_stream_base)
-    roots = torch.from_numpy(roots_np.view(np.uint8).reshape(games, 256)).to(dev)
-    n = plan.n_playouts
-    # game j's rollouts are contiguous (one wave plays 64 rollouts of the same game)
-    idx = torch.from_numpy(plan.root_index()).to(dev)
-    out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    roots_np, sets_np, n, out, step = _config3_prepare(args, order, gpu, plan, dev)
     stream = torch.cuda.Stream(dev)  # our kernels and the timing events share this stream
     plies_acc = torch.zeros(1, dtype=torch.int64, device=dev)
-
-    def step(k):
-        if order == "frontier":
-            gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k),
-                                 root_index=idx, out=out, stream_base=plan.playout_stream_base)
-        else:
-            gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k), root_index=idx,
-                        out=out, stream_base=plan.playout_stream_base)
 
     def count_plies():
         plies_acc.add_(out[:, 10:12].contiguous().view(torch.int16).to(torch.int64).sum())
@@ -411,6 +392,66 @@ def _config3_measure(args, order, gpu, plan, dev, dist):
     elapsed, (sims, all_plies) = reduce_max_sum(dist, dev, elapsed, [n * args.steps, int(plies_acc.item())])
     return {"elapsed": elapsed, "sims": sims, "plies": all_plies, "kernel_ms": kernel_ms, "out": out,
             "roots_np": roots_np, "sets_np": sets_np, "n": n}
+
+
+def _config3_prepare(args, order, gpu, plan, dev):
+    """The plan's roots on the GPU (and, frontier order, their frontier-set tables), the
+    output buffer, and step(k): one launch of the plan's playouts with step seed k."""
+    import numpy as np
+    import torch
+
+    from reinforcementlearning_blokus_amd import _native as N
+    from reinforcementlearning_blokus_amd.gpu import empty_state
+    games = plan.games
+    sets_np = sets = None
+    if order == "frontier":
+        roots_np, sets_np = gpu.rollout_frontier(empty_state(), N.fset_new(1), games,
+                                                 semantics=N.SEM_ADVANCE, rng=N.RNG_PHILOX, seed=plan.seed,
+                                                 max_plies=args.root_plies,
+                                                 root_index=np.zeros(games, dtype=np.int32),
+                                                 stream_base=plan.root_stream_base)
+        sets = torch.from_numpy(sets_np.view(np.uint8).reshape(games, -1).copy()).to(dev)
+    else:
+        roots_np = gpu.advance(empty_state(), games, args.root_plies, seed=plan.seed,
+                               root_index=np.zeros(games, dtype=np.int32), stream_base=plan.root_stream_base)
+    roots = torch.from_numpy(roots_np.view(np.uint8).reshape(games, 256)).to(dev)
+    n = plan.n_playouts
+    # game j's rollouts are contiguous (one wave plays 64 rollouts of the same game)
+    idx = torch.from_numpy(plan.root_index()).to(dev)
+    out = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+
+    def step(k):
+        if order == "frontier":
+            gpu.rollout_frontier(roots, sets, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k),
+                                 root_index=idx, out=out, stream_base=plan.playout_stream_base)
+        else:
+            gpu.rollout(roots, n, semantics=N.SEM_ARENA, rng=N.RNG_PHILOX, seed=plan.step_seed(k), root_index=idx,
+                        out=out, stream_base=plan.playout_stream_base)
+
+    return roots_np, sets_np, n, out, step
+
+
+def _config3_check_gather(args, order, gpu, m, rank, world, dist, dev):
+    """All-gather every rank's last-step records and, on rank 0, compare them with ONE
+    launch of the whole job's N x games games (Config3Plan rank 0 of N x games): the
+    weak-scaling claim that an N-rank job equals a 1-rank run of its games, checked on
+    the device (`--check-gather`).  Returns "ok" or a description of the first mismatch."""
+    import torch
+
+    from reinforcementlearning_blokus_amd.shard import gather_blocks
+    from reinforcementlearning_blokus_amd.workloads import Config3Plan
+    got = gather_blocks(m["out"], rank, world, dist)
+    if rank != 0:
+        return None
+    games = args.games or 256
+    _, _, n, out, step = _config3_prepare(args, order, gpu, Config3Plan(args.seed, games * world, args.rollouts, 0),
+                                          dev)
+    step(1000 + args.steps - 1)
+    torch.cuda.synchronize()
+    if got.shape != out.shape:
+        return f"gathered {tuple(got.shape)} records, one-rank run has {tuple(out.shape)}"
+    bad = (got != out).any(dim=1).nonzero().flatten()
+    return "ok" if bad.numel() == 0 else f"{bad.numel()} of {n} records differ (first: playout {int(bad[0])})"
 
 
 def _config3_fields(args, order, m, world):
@@ -470,7 +511,13 @@ def run_config3(args, world, rank, local, dist):
     mf = None
     if args.order == "naive" and not args.no_frontier_order:
         mf = _config3_measure(args, "frontier", gpu, plan, dev, dist)
-    if dist:
+    checks = {}
+    if dist and args.check_gather:
+        checks["gather_check"] = _config3_check_gather(args, args.order, gpu, m, rank, world, dist, dev)
+        if mf is not None:
+            checks["frontier_gather_check"] = _config3_check_gather(args, "frontier", gpu, mf, rank, world, dist,
+                                                                    dev)
+    elif dist:
         # RCCL gather of the last step's terminal results (32 B per playout) over xGMI,
         # outside the timed region; rank r's playouts are the global block r
         from reinforcementlearning_blokus_amd.shard import gather_blocks
@@ -487,6 +534,9 @@ def run_config3(args, world, rank, local, dist):
                    "parallelism": f"dp{world} (independent games per rank)"},
         "roofline": f["roofline"], "compute_roofline": f["compute_roofline"],
     }
+    line.update(checks)
+    if args.share_device:
+        line["config"]["parallelism"] += f"; rehearsal: {world} ranks share cuda:0 over gloo"
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = _config3_cpu(args, args.order, m, plan, f["value"])
     if mf is not None:
@@ -548,6 +598,9 @@ def run_config5(args, world, rank, local, dist):
         dist, dev, elapsed, [sims_local, plies_local * args.steps, int(res["tt_hits"].sum()) * args.steps,
                              int(res["rollouts"].sum()) * args.steps, unc_local])
     del stream
+    check = None
+    if dist and args.check_gather:
+        check = _config5_check_gather(args, gpu, batch, policy, mine, roots_all, sets_all, rank, world, dist)
     if rank != 0:
         return None
     value = sims / elapsed
@@ -583,6 +636,10 @@ def run_config5(args, world, rank, local, dist):
         # VALU instructions of one launch of this line's size over the average launch time
         "compute_roofline": compute_roofline(valu_insts, kernel_ms / max(1, len(kms))),
     }
+    if check is not None:
+        line["gather_check"] = check
+    if args.share_device:
+        line["config"]["parallelism"] += f"; rehearsal: {world} ranks share cuda:0 over gloo"
     if heur:  # no C restatement of the heuristic search to time: the reference's own numbers
         line["reference"] = {"published": {"value": 40.9, "unit": "sims/s", "what": "MCTSAgent (heuristic "
                                            "rollouts, TT), 200 ms/move, MacBook (BASELINE.md)"},
@@ -597,6 +654,35 @@ def run_config5(args, world, rank, local, dist):
                                             "MCTSAgent + RandomAgent rollouts, 100 iterations (one search)")
         line["cpu_baseline"] = cb
     return line
+
+
+def _config5_check_gather(args, gpu, batch, policy, mine, roots_all, sets_all, rank, world, dist):
+    """Gather every rank's search records (games r mod W) and, on rank 0, compare them with
+    one batch searching all the job's games in one process (`--check-gather`): the
+    strong-scaling claim that a sharded job equals a single-process run, on the device.
+    Returns "ok" or the record fields that differ."""
+    import numpy as np
+
+    from reinforcementlearning_blokus_amd.workloads import MctsBatch
+    parts = [None] * world
+    dist.all_gather_object(parts, (mine.tolist(), batch.results().tobytes()))
+    if rank != 0:
+        return None
+    total = len(roots_all)
+    one = MctsBatch(gpu, roots_all, sets_all, iterations=args.iterations, seed0=0, index=np.arange(total))
+    one.run(chunk=args.chunk, rollout_policy=policy)
+    ref = one.results()
+    got = np.zeros_like(ref)
+    seen = np.zeros(total, dtype=bool)
+    for idx, raw in parts:
+        got[np.asarray(idx, dtype=np.int64)] = np.frombuffer(raw, dtype=ref.dtype)
+        seen[np.asarray(idx, dtype=np.int64)] = True
+    if not seen.all():
+        return f"{int((~seen).sum())} games gathered from no rank"
+    if got.tobytes() == ref.tobytes():
+        return "ok"
+    diff = [f for f in ref.dtype.names if not np.array_equal(got[f], ref[f])]
+    return "records differ in " + ", ".join(diff)
 
 
 def cpu_baseline_mcts(roots, sets, batch, seconds):
@@ -685,9 +771,18 @@ def run_config4(args, world, rank, local, dist):
     elapsed, (games, all_sims, all_moves) = reduce_max_sum(dist, dev, elapsed,
                                                            [len(recs) * args.steps, sims * args.steps,
                                                             moves * args.steps])
+    check = None
     if dist:
         gathered = [None] * world
-        dist.all_gather_object(gathered, [(r["game_index"], r["final_scores"]) for r in recs])
+        dist.all_gather_object(gathered, [(r["game_index"], r["final_scores"], r["moves_made"]) for r in recs])
+        if args.check_gather and rank == 0:
+            # the sharded job against one process playing all its games (strong scaling)
+            one = {r["game_index"]: (r["game_index"], r["final_scores"], r["moves_made"])
+                   for r in run_games_batched(cfg, list(range(total)), device=local)}
+            got = {g[0]: tuple(g) for part in gathered for g in part}
+            bad = sorted(i for i in one if got.get(i) != one[i])
+            check = "ok" if not bad and len(got) == total else \
+                f"{len(bad)} of {total} games differ ({len(got)} gathered; first {bad[:4]})"
     if rank != 0:
         return None
     # roofline of the dominant kernel, the bk_mcts kernel with the most launch time
@@ -725,6 +820,10 @@ def run_config4(args, world, rank, local, dist):
                              "what": "a 4-random-agent game with the reference's default telemetry (20.3 s), "
                                      "measured in the build container (SURVEY.md 6); MCTS seats are slower"},
     }
+    if check is not None:
+        line["gather_check"] = check
+    if args.share_device:
+        line["config"]["parallelism"] += f"; rehearsal: {world} ranks share cuda:0 over gloo"
     if not args.no_cpu_baseline and world == 1:
         cb = cpu_baseline_config4(cfg, args.cpu_seconds, recs)
         cb["gpu_over_cpu"] = line["value"] / cb["value"]

@@ -106,6 +106,8 @@ def hash_states(states: np.ndarray, keys: np.ndarray) -> np.ndarray:
     if not per_state:
         keys = keys.reshape(-1)
     n = len(states)
+    if n == 0:  # (a rank's shard may hold no game of some table: games r mod W, tables i mod 8)
+        return np.zeros(0, np.uint64)
     cells = np.arange(400)
     word, bit = cells // 64, (cells % 64).astype(np.uint64)
     grid = np.zeros((n, 400), np.int64)

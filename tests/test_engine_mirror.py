@@ -147,6 +147,9 @@ def test_hash_states_matches_reference_zobrist():
         got = hash_states(st, keys)
         assert [str(x) for x in got] == rec["hashes"]
         assert [int(z.hash_board(b)) for b in boards] == [int(x) for x in got]
+        # an empty selection (a rank's shard with no game of some key table) hashes to []
+        assert hash_states(st[:0], keys).shape == (0,)
+        assert hash_states(st[:0], np.zeros((0, 2088), np.uint64)).shape == (0,)
 
 
 def test_mcts_tt_load_and_reserve_keep_entries():
