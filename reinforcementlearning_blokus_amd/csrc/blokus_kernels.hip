@@ -401,6 +401,11 @@ struct StencilClass {
 #ifndef FR_BLOCKS_PER_CU
 #define FR_BLOCKS_PER_CU 4
 #endif
+// rollout_body: launder the slot / lane index per ply (bit 0: k_rollout_fr(_h), bit 1:
+// k_rollout / k_advance)
+#ifndef BK_ROLL_OPAQUE
+#define BK_ROLL_OPAQUE 3
+#endif
 // tables probed in global memory read 8-slot chunks (FsetRef::gchunk, fs_probe)
 #ifndef BK_GLOBAL_CHUNK
 #define BK_GLOBAL_CHUNK 1
@@ -2894,20 +2899,22 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     // fits 4 blocks per CU); HEUR: + the policy's exp tables
     constexpr bool HT_LDS = FR && (HEUR || BK_FR_HTAB_LDS);
     __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + (HT_LDS ? 2 * BK_CELLS : 0) + HS_WORDS];
-    const int lane = threadIdx.x & (WAVE - 1), wv = threadIdx.x / WAVE;
-    uint32_t* my = lds + wv * AREA;
-    uint2* rows_lds = reinterpret_cast<uint2*>(lds + wv * AREA) + lane;  // + R * WAVE
+    const int lane0 = threadIdx.x & (WAVE - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     uint64_t* htab_lds = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
     const uint64_t* htab = HT_LDS ? htab_lds : kCellHash;
     HeurShared* hs = reinterpret_cast<HeurShared*>(lds + AREA * (BLK / WAVE) + (HT_LDS ? 2 * BK_CELLS : 0));
-    double* psum = reinterpret_cast<double*>(lds + wv * AREA + HEUR_PSUM * WAVE) + lane;  // + piece * WAVE
     if constexpr (HT_LDS) {
         for (int i = threadIdx.x; i < BK_CELLS; i += BLK) htab_lds[i] = kCellHash[i];
     }
     if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
     if constexpr (HT_LDS || HEUR) __syncthreads();
-    const uint32_t slot = blockIdx.x * BLK + threadIdx.x;
-    const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
+    const uint32_t slot0 = blockIdx.x * BLK + threadIdx.x;
+    // BK_ROLL_OPAQUE (bit 0: frontier-order kernels, bit 1: naive): the lane's slot and
+    // lane index are laundered once per ply, so the addresses derived from them (slab,
+    // frontier record, LDS columns) are recomputed in the loop instead of being held in
+    // registers for the whole kernel (spilled across the stencil)
+    constexpr bool OPAQUE = (BK_ROLL_OPAQUE >> (FR ? 0 : 1)) & 1;
+    uint32_t* const my = lds + wv * AREA;
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
     const bool advance = a.cfg.semantics == BK_SEM_ADVANCE;
 
@@ -2917,6 +2924,12 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     uint32_t handed = 0;  // playouts this slot has taken (handout 1, 2)
     SECT_DECL
     for (uint32_t iter = 0;; ++iter) {
+        uint32_t slot = slot0;
+        int lane = lane0;
+        if constexpr (OPAQUE) asm volatile("" : "+v"(slot), "+v"(lane));
+        const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
+        uint2* const rows_lds = reinterpret_cast<uint2*>(my) + lane;  // + R * WAVE
+        double* const psum = reinterpret_cast<double*>(my + HEUR_PSUM * WAVE) + lane;  // + piece * WAVE
         SECT(0);
         // ---- make sure this lane has a game whose current player may still move
         for (int guard = 0; guard < 3 && !done; ++guard) {
