@@ -415,12 +415,21 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
     its iteration count, exploration constant and random.Random state.  None if some agent
     cannot be replayed on the device (wall-clock budgets, rollout agents the kernels do not
     implement): run_games_batched then plays the host-staged loop."""
+    from .. import mt19937
     from ..mcts.mcts_agent import _search_policy
     from ..mcts.zobrist import flat_keys
     cfgs = {a.name: a for a in run_config.agents}
     mcts, fast = [], []  # (game i, name, ...)
     seat_agent = np.full((len(idx), 4), -1, np.int64)  # index into mcts / fast
     seat_kind = np.zeros((len(idx), 4), np.int8)  # 0 random/heuristic, 1 mcts, 2 fast
+    # An MCTSAgent's seed only seeds its ZobristHash and its rollout HeuristicAgent, two
+    # RandomState(seed) streams (build_agent).  The first agent of each name is built and
+    # checked against mt19937 (keys = the first 2,088 uint64 draws, rollout state = the
+    # fresh state); the others take its seed-independent fields and get their keys and
+    # states from mt19937 for all seeds at once (RandomState construction was ~0.2 ms per
+    # agent).  A name whose first agent does not match is built agent by agent.
+    tmpl: Dict[str, Optional[Dict[str, Any]]] = {}
+    lazy: List[Tuple[int, int]] = []  # (index into mcts, seed)
     for i, gi in enumerate(idx):
         st = seats_of[i]
         # RunConfig holds exactly 4 distinct agents (arena_runner.py:125-200), so an agent
@@ -435,7 +444,14 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
             if kind not in _SEARCH_KINDS:
                 continue
             if name not in done:
-                ad = build_agent(c, agent_seed(run_config.seed, gi, name))
+                seed = agent_seed(run_config.seed, gi, name)
+                if kind == "mcts" and tmpl.get(name) is not None and 0 <= seed <= 0xFFFFFFFF:
+                    mcts.append(dict(tmpl[name], i=i, zob=None, mt=None))
+                    lazy.append((len(mcts) - 1, seed))
+                    done[name] = (1, len(mcts) - 1)
+                    seat_kind[i, p], seat_agent[i, p] = done[name]
+                    continue
+                ad = build_agent(c, seed)
                 if isinstance(ad, _SelectActionAdapter) and isinstance(ad.agent, MCTSAgent):
                     a = ad.agent
                     pol = _search_policy(a.rollout_agent) if a.rollout_backend == "search" else None
@@ -448,6 +464,13 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
                                  "c": float(a.exploration_constant), "tt": bool(a.use_transposition_table),
                                  "policy": int(pol), "zob": flat_keys(a.zobrist_hash), "mt": mt})
                     done[name] = (1, len(mcts) - 1)
+                    if kind == "mcts" and name not in tmpl:
+                        ok = 0 <= seed <= 0xFFFFFFFF
+                        if ok:
+                            s0 = mt19937.seed_states([seed])
+                            ok = (np.array_equal(mcts[-1]["zob"], mt19937.uint64_draws([seed], 2088, s0)[0])
+                                  and np.array_equal(mt[:624], s0[0]) and int(mt[624]) == 624)
+                        tmpl[name] = {k: v for k, v in mcts[-1].items() if k not in ("i", "zob", "mt")} if ok else None
                 elif isinstance(ad, (_FastMCTSAdapter, _GameplayFastMCTSAdapter)):
                     if not ad.deterministic_time_budget:
                         return None
@@ -463,6 +486,12 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
                 else:
                     return None
             seat_kind[i, p], seat_agent[i, p] = done[name]
+    if lazy:
+        states = mt19937.seed_states([sd for _, sd in lazy])
+        zob = mt19937.uint64_draws(None, 2088, states)
+        mts = np.concatenate([states, np.full((len(lazy), 1), 624, np.uint32)], axis=1)
+        for j, (k, _) in enumerate(lazy):
+            mcts[k]["zob"], mcts[k]["mt"] = zob[j], mts[j]
     return mcts, fast, seat_kind, seat_agent
 
 

@@ -67,12 +67,11 @@ class Config3Plan:
 def numpy_mt_states(seeds) -> np.ndarray:
     """uint32[n, 625]: numpy RandomState(seed) MT19937 key + pos per seed (the rollout
     agent's stream, agents/random_agent.py:29)."""
-    seeds = list(seeds)
+    from .mt19937 import seed_states
+    seeds = np.asarray([int(s) for s in seeds], dtype=np.int64)
     out = np.zeros((len(seeds), 625), np.uint32)
-    for i, s in enumerate(seeds):
-        st = np.random.RandomState(int(s)).get_state()
-        out[i, :624] = st[1]
-        out[i, 624] = st[2]
+    out[:, :624] = seed_states(seeds)  # (RandomState(seed) for all seeds at once)
+    out[:, 624] = 624
     return out
 
 

@@ -1,0 +1,68 @@
+"""reinforcementlearning_blokus_amd.mt19937 (numpy's legacy MT19937 for arrays of seeds)
+against np.random.RandomState itself, and the arena's device agents built with it
+against agents built one by one (arena/runner.py _device_agents)."""
+import numpy as np
+import pytest
+
+from reinforcementlearning_blokus_amd import mt19937
+
+
+SEEDS = [0, 1, 5489, 2**31, 2**32 - 1] + np.random.RandomState(7).randint(0, 2**32, size=60,
+                                                                           dtype=np.uint64).tolist()
+
+
+def test_seed_states_equal_randomstate():
+    st = mt19937.seed_states(SEEDS)
+    for i, s in enumerate(SEEDS):
+        keys, pos = np.random.RandomState(s).get_state()[1:3]
+        assert np.array_equal(st[i], keys) and pos == 624
+
+
+@pytest.mark.parametrize("k", [1, 311, 312, 2088])
+def test_uint64_draws_equal_randomstate(k):
+    got = mt19937.uint64_draws(SEEDS, k)
+    assert got.dtype == np.uint64 and got.shape == (len(SEEDS), k)
+    for i, s in enumerate(SEEDS):
+        assert np.array_equal(got[i], np.random.RandomState(s).randint(0, 2**64, size=k, dtype=np.uint64))
+
+
+def test_uint32_draws_cross_many_twists():
+    got = mt19937.uint32_draws(mt19937.seed_states([42, 43]), 3000)
+    for i, s in enumerate([42, 43]):
+        assert np.array_equal(got[i], np.random.RandomState(s).randint(0, 2**32, size=3000, dtype=np.uint64))
+
+
+@pytest.mark.parametrize("bad", [[-1], [2**32], [1.5]])
+def test_out_of_range_seeds_raise(bad):
+    with pytest.raises(ValueError):
+        mt19937.seed_states(bad)
+
+
+def test_device_agents_equal_agents_built_one_by_one(monkeypatch):
+    import bench
+    from reinforcementlearning_blokus_amd.arena import runner as R
+    from reinforcementlearning_blokus_amd.arena.config import RunConfig
+    cfg = RunConfig.from_dict({"agents": bench.CONFIG4_AGENTS, "num_games": 48, "seed": 20260301,
+                               "seat_policy": "round_robin"})
+    idx = list(range(5, 53))
+    seats = [R.seat_assignment_for_game(cfg.agent_names, gi, R.game_seed_from_run_seed(cfg.seed, gi),
+                                        cfg.seat_policy) for gi in idx]
+    fast = R._device_agents(cfg, seats, idx)
+    # a generator that disagrees with the first agent: every agent is built (the old path)
+    monkeypatch.setattr(mt19937, "uint64_draws", lambda *a, **k: np.zeros((1, 2088), np.uint64))
+    slow = R._device_agents(cfg, seats, idx)
+    assert len(fast[0]) == len(slow[0]) > 1
+    for a, b in zip(fast[0], slow[0]):
+        assert a.keys() == b.keys()
+        for key in a:
+            assert np.array_equal(np.asarray(a[key]), np.asarray(b[key])), key
+    assert np.array_equal(fast[2], slow[2]) and np.array_equal(fast[3], slow[3])
+
+
+def test_numpy_mt_states_equal_randomstate():
+    from reinforcementlearning_blokus_amd.workloads import numpy_mt_states
+    got = numpy_mt_states(SEEDS[:12])
+    for i, s in enumerate(SEEDS[:12]):
+        keys, pos = np.random.RandomState(s).get_state()[1:3]
+        assert np.array_equal(got[i, :624], keys) and got[i, 624] == pos
+    assert numpy_mt_states([]).shape == (0, 625)

@@ -1,0 +1,34 @@
+"""Host time of the config-4 driver's agent setup (arena/runner.py _device_agents) for
+1,024 games: MCTSAgent keys and rollout states from mt19937 for all seeds at once, against
+building every agent (RandomState per agent).  Prints one JSON line."""
+import json
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
+import bench  # noqa: E402
+from reinforcementlearning_blokus_amd import mt19937  # noqa: E402
+from reinforcementlearning_blokus_amd.arena import runner as R  # noqa: E402
+from reinforcementlearning_blokus_amd.arena.config import RunConfig  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+cfg = RunConfig.from_dict({"agents": bench.CONFIG4_AGENTS, "num_games": n, "seed": 20260301,
+                           "seat_policy": "round_robin"})
+idx = list(range(n))
+seats = [R.seat_assignment_for_game(cfg.agent_names, gi, R.game_seed_from_run_seed(cfg.seed, gi), cfg.seat_policy)
+         for gi in idx]
+out = {"games": n}
+for rep in range(2):
+    t = time.perf_counter()
+    R._device_agents(cfg, seats, idx)
+    out[f"vectorised_s_{rep}"] = time.perf_counter() - t
+orig = mt19937.uint64_draws
+mt19937.uint64_draws = lambda *a, **k: np.zeros((1, 2088), np.uint64)  # every agent built
+for rep in range(2):
+    t = time.perf_counter()
+    R._device_agents(cfg, seats, idx)
+    out[f"built_s_{rep}"] = time.perf_counter() - t
+mt19937.uint64_draws = orig
+print(json.dumps(out))
