@@ -947,6 +947,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         warnings.warn(f"run_games_batched: {prof['uncertified_heuristic']} HeuristicAgent draw(s) fell within 2^-40 "
                       "of a probability boundary (choice not certified equal to the reference's on every host)",
                       RuntimeWarning, stacklevel=2)
+    prof["t_end"] = time.perf_counter()
     final = states_d.cpu().numpy().view(N.STATE_DTYPE).reshape(n)
     out = []
     for i, gi in enumerate(idx):
@@ -988,6 +989,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
         return []
     cfgs = {a.name: a for a in run_config.agents}
     if os.environ.get("BK_ARENA_DEVICE", "1") != "0":
+        t_in = time.perf_counter()
         seats_d, gseeds_d = [], []
         for gi in idx:
             gs = game_seed_from_run_seed(run_config.seed, gi)
@@ -998,8 +1000,14 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
             gseeds_d.append(gs)
         ag = _device_agents(run_config, seats_d, idx)
         if ag is not None:
-            return _run_games_device(run_config, idx, seats_d, gseeds_d, ag, run_id=run_id, device=device,
-                                     progress=progress)
+            agents_s = time.perf_counter() - t_in
+            out = _run_games_device(run_config, idx, seats_d, gseeds_d, ag, run_id=run_id, device=device,
+                                    progress=progress)
+            # host time around the device loop: seats + agents before it, records after it
+            LAST_BATCH_PROFILE.update(agents_s=agents_s, records_s=time.perf_counter() - LAST_BATCH_PROFILE["t_end"],
+                                      call_s=time.perf_counter() - t_in)
+            del LAST_BATCH_PROFILE["t_end"]
+            return out
     gpu = BlokusGPU(device)
     t0 = time.perf_counter()
     states = np.repeat(empty_state(), n)
