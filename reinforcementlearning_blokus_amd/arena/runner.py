@@ -427,9 +427,11 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
     # checked against mt19937 (keys = the first 2,088 uint64 draws, rollout state = the
     # fresh state); the others take its seed-independent fields and get their keys and
     # states from mt19937 for all seeds at once (RandomState construction was ~0.2 ms per
-    # agent).  A name whose first agent does not match is built agent by agent.
+    # agent).  A name whose first agent does not match is built agent by agent.  Likewise
+    # a FastMCTSAgent, whose seed only seeds its random.Random (python_random_states).
     tmpl: Dict[str, Optional[Dict[str, Any]]] = {}
     lazy: List[Tuple[int, int]] = []  # (index into mcts, seed)
+    lazy_fast: List[Tuple[int, int]] = []  # (index into fast, seed): FastMCTSAgent's random.Random state
     for i, gi in enumerate(idx):
         st = seats_of[i]
         # RunConfig holds exactly 4 distinct agents (arena_runner.py:125-200), so an agent
@@ -449,6 +451,12 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
                     mcts.append(dict(tmpl[name], i=i, zob=None, mt=None))
                     lazy.append((len(mcts) - 1, seed))
                     done[name] = (1, len(mcts) - 1)
+                    seat_kind[i, p], seat_agent[i, p] = done[name]
+                    continue
+                if kind == "fast_mcts" and tmpl.get(name) is not None and seed >= 0:
+                    fast.append(dict(tmpl[name], i=i, mt=None))
+                    lazy_fast.append((len(fast) - 1, seed))
+                    done[name] = (2, len(fast) - 1)
                     seat_kind[i, p], seat_agent[i, p] = done[name]
                     continue
                 ad = build_agent(c, seed)
@@ -483,6 +491,9 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
                     fast.append({"i": i, "name": name, "iters": max(1, int(round(ad.iterations_per_ms * budget))),
                                  "c": float(fa.exploration_constant), "mt": fa._rng_words()})
                     done[name] = (2, len(fast) - 1)
+                    if kind == "fast_mcts" and name not in tmpl:  # (its seed only seeds random.Random)
+                        ok = seed >= 0 and np.array_equal(fast[-1]["mt"], mt19937.python_random_states([seed])[0])
+                        tmpl[name] = {k: v for k, v in fast[-1].items() if k not in ("i", "mt")} if ok else None
                 else:
                     return None
             seat_kind[i, p], seat_agent[i, p] = done[name]
@@ -492,6 +503,10 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
         mts = np.concatenate([states, np.full((len(lazy), 1), 624, np.uint32)], axis=1)
         for j, (k, _) in enumerate(lazy):
             mcts[k]["zob"], mcts[k]["mt"] = zob[j], mts[j]
+    if lazy_fast:
+        words = mt19937.python_random_states([sd for _, sd in lazy_fast])
+        for j, (k, _) in enumerate(lazy_fast):
+            fast[k]["mt"] = words[j]
     return mcts, fast, seat_kind, seat_agent
 
 

@@ -91,3 +91,41 @@ def uint64_draws(seeds, k: int, states=None) -> np.ndarray:
     pairs[:, :, 0] = w[:, 1::2]
     pairs[:, :, 1] = w[:, 0::2]
     return pairs.view("<u8").reshape(w.shape[0], k).astype(np.uint64, copy=False)
+
+
+def python_random_states(seeds) -> np.ndarray:
+    """uint32[n, 625]: random.Random(seed).getstate()[1] for each non-negative integer seed
+    (CPython's init_by_array over the seed's 32-bit words, least significant first; the
+    position word is 624).  Seeds with different word counts run as separate groups."""
+    seeds = [int(s) for s in seeds]
+    out = np.zeros((len(seeds), N + 1), np.uint32)
+    out[:, N] = N
+    if any(s < 0 for s in seeds):  # (random.seed takes abs(); the arena's seeds are >= 0)
+        raise ValueError("python_random_states: negative seed")
+    nwords = [max(1, (s.bit_length() + 31) // 32) for s in seeds]
+    for kl in sorted(set(nwords)):
+        rows = np.array([i for i, w in enumerate(nwords) if w == kl], np.int64)
+        key = np.array([[(seeds[i] >> (32 * j)) & 0xFFFFFFFF for j in range(kl)] for i in rows], np.uint32)
+        mt = np.repeat(seed_states([19650218]), len(rows), axis=0)
+        with np.errstate(over="ignore"):
+            i, j = 1, 0
+            for _ in range(max(N, kl)):
+                prev = mt[:, i - 1]
+                mt[:, i] = (mt[:, i] ^ ((prev ^ (prev >> np.uint32(30))) * np.uint32(1664525))) + key[:, j] + \
+                    np.uint32(j)
+                i, j = i + 1, j + 1
+                if i >= N:
+                    mt[:, 0] = mt[:, N - 1]
+                    i = 1
+                if j >= kl:
+                    j = 0
+            for _ in range(N - 1):
+                prev = mt[:, i - 1]
+                mt[:, i] = (mt[:, i] ^ ((prev ^ (prev >> np.uint32(30))) * np.uint32(1566083941))) - np.uint32(i)
+                i += 1
+                if i >= N:
+                    mt[:, 0] = mt[:, N - 1]
+                    i = 1
+        mt[:, 0] = 0x80000000
+        out[rows, :N] = mt
+    return out

@@ -48,14 +48,16 @@ def test_device_agents_equal_agents_built_one_by_one(monkeypatch):
     seats = [R.seat_assignment_for_game(cfg.agent_names, gi, R.game_seed_from_run_seed(cfg.seed, gi),
                                         cfg.seat_policy) for gi in idx]
     fast = R._device_agents(cfg, seats, idx)
-    # a generator that disagrees with the first agent: every agent is built (the old path)
+    # generators that disagree with the first agents: every agent is built (the old path)
     monkeypatch.setattr(mt19937, "uint64_draws", lambda *a, **k: np.zeros((1, 2088), np.uint64))
+    monkeypatch.setattr(mt19937, "python_random_states", lambda *a, **k: np.zeros((1, 625), np.uint32))
     slow = R._device_agents(cfg, seats, idx)
-    assert len(fast[0]) == len(slow[0]) > 1
-    for a, b in zip(fast[0], slow[0]):
-        assert a.keys() == b.keys()
-        for key in a:
-            assert np.array_equal(np.asarray(a[key]), np.asarray(b[key])), key
+    for got, ref in ((fast[0], slow[0]), (fast[1], slow[1])):  # MCTSAgents, FastMCTSAgents
+        assert len(got) == len(ref) > 1
+        for a, b in zip(got, ref):
+            assert a.keys() == b.keys()
+            for key in a:
+                assert np.array_equal(np.asarray(a[key]), np.asarray(b[key])), key
     assert np.array_equal(fast[2], slow[2]) and np.array_equal(fast[3], slow[3])
 
 
@@ -66,3 +68,11 @@ def test_numpy_mt_states_equal_randomstate():
         keys, pos = np.random.RandomState(s).get_state()[1:3]
         assert np.array_equal(got[i, :624], keys) and got[i, 624] == pos
     assert numpy_mt_states([]).shape == (0, 625)
+
+
+def test_python_random_states_equal_random_random():
+    import random
+    seeds = [0, 1, 2**32 - 1, 2**32, 2**40 + 5, 2**63 - 1] + [random.Random(1).getrandbits(63) for _ in range(20)]
+    got = mt19937.python_random_states(seeds)
+    for i, s in enumerate(seeds):
+        assert np.array_equal(got[i], np.array(random.Random(s).getstate()[1], dtype=np.uint32)), s

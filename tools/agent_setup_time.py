@@ -1,5 +1,6 @@
 """Host time of the config-4 driver's agent setup (arena/runner.py _device_agents) for
-1,024 games: MCTSAgent keys and rollout states from mt19937 for all seeds at once, against
+1,024 games: MCTSAgent keys and rollout states and FastMCTSAgent states from mt19937 for all
+seeds at once, against
 building every agent (RandomState per agent).  Prints one JSON line."""
 import json
 import sys
@@ -24,11 +25,12 @@ for rep in range(2):
     t = time.perf_counter()
     R._device_agents(cfg, seats, idx)
     out[f"vectorised_s_{rep}"] = time.perf_counter() - t
-orig = mt19937.uint64_draws
+orig = mt19937.uint64_draws, mt19937.python_random_states
 mt19937.uint64_draws = lambda *a, **k: np.zeros((1, 2088), np.uint64)  # every agent built
+mt19937.python_random_states = lambda *a, **k: np.zeros((1, 625), np.uint32)
 for rep in range(2):
     t = time.perf_counter()
     R._device_agents(cfg, seats, idx)
     out[f"built_s_{rep}"] = time.perf_counter() - t
-mt19937.uint64_draws = orig
+mt19937.uint64_draws, mt19937.python_random_states = orig
 print(json.dumps(out))
