@@ -8,6 +8,7 @@ same run seed and game index.  ``run_single_game`` is the reference loop itself
 """
 from __future__ import annotations
 
+import gc
 import json
 import random
 import os
@@ -1013,13 +1014,27 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
                 raise ValueError(f"game {gi}: seating {st} cannot be batched; use run_single_game")
             seats_d.append(st)
             gseeds_d.append(gs)
-        ag = _device_agents(run_config, seats_d, idx)
+        t_seats = time.perf_counter()
+        gc0 = sum(g["collections"] for g in gc.get_stats())
+        # no collections during the agent setup: over the caller's heap (torch, earlier
+        # records) they cost ~0.02 s per 1,024 games and free nothing the setup made
+        # (profiles/r05/sweeps/r05an)
+        gc_on = gc.isenabled()
+        if gc_on:
+            gc.disable()
+        try:
+            ag = _device_agents(run_config, seats_d, idx)
+        finally:
+            if gc_on:
+                gc.enable()
         if ag is not None:
             agents_s = time.perf_counter() - t_in
+            setup_gc = sum(g["collections"] for g in gc.get_stats()) - gc0
             out = _run_games_device(run_config, idx, seats_d, gseeds_d, ag, run_id=run_id, device=device,
                                     progress=progress)
             # host time around the device loop: seats + agents before it, records after it
-            LAST_BATCH_PROFILE.update(agents_s=agents_s, records_s=time.perf_counter() - LAST_BATCH_PROFILE["t_end"],
+            LAST_BATCH_PROFILE.update(agents_s=agents_s, seats_s=t_seats - t_in, agents_gc=setup_gc,
+                                      records_s=time.perf_counter() - LAST_BATCH_PROFILE["t_end"],
                                       call_s=time.perf_counter() - t_in)
             del LAST_BATCH_PROFILE["t_end"]
             return out

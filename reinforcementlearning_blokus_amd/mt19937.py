@@ -21,6 +21,7 @@ from __future__ import annotations
 import numpy as np
 
 N, M = 624, 397
+ROWS = 48  # seeds per block in uint64_draws: 48 x 624 x 4 B = 117 KB
 _MATRIX_A = np.uint32(0x9908B0DF)
 _UPPER, _LOWER = np.uint32(0x80000000), np.uint32(0x7FFFFFFF)
 _ONE = np.uint32(1)
@@ -86,11 +87,17 @@ def uint64_draws(seeds, k: int, states=None) -> np.ndarray:
     """uint64[n, k]: RandomState(seed).randint(0, 2**64, size=k, dtype=np.uint64) for each
     seed (next_uint64 = high word << 32 | low word); `states`: seed_states(seeds), if the
     caller has them."""
-    w = uint32_draws(seed_states(seeds) if states is None else states, 2 * k)
-    pairs = np.empty((w.shape[0], k, 2), np.uint32)  # (low, high) words: a little-endian uint64
-    pairs[:, :, 0] = w[:, 1::2]
-    pairs[:, :, 1] = w[:, 0::2]
-    return pairs.view("<u8").reshape(w.shape[0], k).astype(np.uint64, copy=False)
+    states = seed_states(seeds) if states is None else np.asarray(states, np.uint32)
+    n = states.shape[0]
+    pairs = np.empty((n, k, 2), np.uint32)  # (low, high) words: a little-endian uint64
+    # blocks of ROWS seeds: the generator's temporaries stay below glibc's mmap threshold
+    # (128 KB), so they come from the heap instead of fresh pages (a first call over
+    # 1,024 seeds otherwise spends most of its time in page faults)
+    for r0 in range(0, n, ROWS):
+        w = uint32_draws(states[r0:r0 + ROWS], 2 * k)
+        pairs[r0:r0 + ROWS, :, 0] = w[:, 1::2]
+        pairs[r0:r0 + ROWS, :, 1] = w[:, 0::2]
+    return pairs.view("<u8").reshape(n, k).astype(np.uint64, copy=False)
 
 
 def python_random_states(seeds) -> np.ndarray:
