@@ -611,21 +611,27 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     masks = np.zeros(n, np.uint8)
     quick = np.zeros(n, np.uint8)
     rng = np.zeros((n, 16), np.uint32)
+    cur_at, cur_seed = [], []  # (game, seat) of each random / heuristic seat, its agent seed
     for i, gi in enumerate(idx):
         for p in range(4):
             name = seats[i][str(p + 1)]
             kind = cfgs[name].type.lower()
             if kind in ("random", "heuristic"):
-                rng[i, 4 * p:4 * p + 4] = N.mt_cursors([agent_seed(run_config.seed, gi, name)])[0]
+                cur_at.append((i, p))
+                cur_seed.append(agent_seed(run_config.seed, gi, name))
                 if kind == "heuristic":
                     masks[i] |= 1 << p
             else:
                 masks[i] |= 16 << p
                 if seat_kind[i, p] == 2:
                     quick[i] |= 1 << p
+    if cur_at:  # the seats' MT cursors in one call
+        cursors = N.mt_cursors(cur_seed)
+        for (i, p), c in zip(cur_at, cursors):
+            rng[i, 4 * p:4 * p + 4] = c
     up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
     states_d = up(np.repeat(empty_state(), n).view(np.uint8).reshape(n, 256))
-    sets_d = up(N.fset_new(n).view(np.uint8).reshape(n, -1))
+    sets_d = up(np.repeat(N.fset_new(1), n).view(np.uint8).reshape(n, -1))  # (every game starts from Board())
     masks_d, quick_d, rng_d = up(masks), up(quick), up(rng.view(np.int32))
     forced_d = torch.full((n,), -1, dtype=torch.int32, device=dev)
     out_d = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
