@@ -972,22 +972,35 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     prof["t_end"] = time.perf_counter()
     final = states_d.cpu().numpy().view(N.STATE_DTYPE).reshape(n)
     out = []
+    gc_on = gc.isenabled()  # (the records are new objects only: no collection can free any)
+    if gc_on:
+        gc.disable()
+    try:
+        _device_records(out, idx, results, per_agent, final, seats, gseeds, run_config, run_id, dt, n)
+    finally:
+        if gc_on:
+            gc.enable()
+    return out
+
+
+def _device_records(out, idx, results, per_agent, final, seats, gseeds, run_config, run_id, dt, n):
+    """The per-game records of _run_games_device (arena_runner.py's record fields)."""
+    used, moves_made = final["used"].astype(np.int64).tolist(), final["move_count"].tolist()
     for i, gi in enumerate(idx):
         r, turns, passes, truncated = results[i]
-        scores = {p + 1: int(r["scores"][p]) for p in range(4)}
+        scores = {p + 1: int(v) for p, v in enumerate(r["scores"].tolist())}
         winners = [p for p, sc in scores.items() if sc == max(scores.values())]
         pa = per_agent[i]
         for p in range(4):
-            pa[seats[i][str(p + 1)]]["moves"] += float(bin(int(final["used"][i, p])).count("1"))
+            pa[seats[i][str(p + 1)]]["moves"] += float(bin(used[i][p]).count("1"))
         total_moves = max(sum(e["moves"] for e in pa.values()), 1.0)
         for e in pa.values():
             e["total_time_ms"] = dt / n * (e["moves"] / total_moves) * 1000.0
         _finish_stats(pa)
         out.append(_record(run_id=run_id, game_index=gi, game_seed=gseeds[i], run_config=run_config, seats=seats[i],
                            scores=scores, winner_ids=winners, is_tie=len(winners) > 1,
-                           moves_made=int(final["move_count"][i]), turn_count=turns, passes=passes, invalid=0,
+                           moves_made=int(moves_made[i]), turn_count=turns, passes=passes, invalid=0,
                            duration=dt / n, truncated=truncated, per_agent=pa, error=None))
-    return out
 
 
 def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
