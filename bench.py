@@ -5,7 +5,15 @@ Default workload (`--workload config3`, BASELINE.json configs[2]) -- one "step" 
 concurrent self-play games x 1,024 random rollouts per game-move = 262,144 terminal
 random playouts (arena semantics: pass when stuck, game over when nobody can move,
 GameResult scoring) from 256 synthetic mid-game positions (20 random plies from the
-empty board), all resident in HBM before the timed region.
+empty board), all resident in HBM before the timed region.  The line's `value` is the
+reference as shipped: its default frontier move order (BLOKUS_USE_FRONTIER_MOVEGEN=1,
+engine/move_generator.py:66, :148; kernel k_rollout_fr).  The default line also carries:
+  naive_order  the same measurement in naive order (BLOKUS_USE_FRONTIER_MOVEGEN=0, k_rollout)
+  config5      BASELINE configs[4]: 65,536 MCTSAgent searches x 4,096 iterations (one
+               launch after a 64-iteration warmup), strong scaling over the ranks
+  config4      BASELINE configs[3]: 1,024 arena games per rank (8,192 at 8 GPUs) after one
+               warm-up batch
+each with its own value, ms_per_step, roofline and (one GPU) cpu_baseline.
 
 Other workloads (one JSON line each, same contract):
   --workload config5  BASELINE.json configs[4]: 65,536 concurrent MCTSAgent searches x
@@ -97,17 +105,25 @@ def parse(argv=None):
                          "each rank's host phases and worker threads are pinned to its own cores)")
     ap.add_argument("--search-streams", type=int, default=None,
                     help="config4: MCTS searches in flight on this many streams while the other games play on "
-                         "(BK_ARENA_MCTS_STREAMS; default: the driver's)")
+                         "(ArenaOptions.search_streams, 1..16; default: the driver's 8)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="config4: HIP hardware queues of this rank (GPU_MAX_HW_QUEUES, <= 32; default 16), so the "
                          "search streams, the FastMCTS handle and the main stream do not share in-order queues "
                          "(HIP's default is 4); 0 leaves the environment's setting")
-    ap.add_argument("--order", choices=("naive", "frontier"), default="naive",
-                    help="config3 in-kernel move order of the line's value: naive (default) or the reference's "
-                         "frontier order (CPython set tables carried per game)")
-    ap.add_argument("--no-frontier-order", action="store_true",
-                    help="config3, naive order: skip the line's frontier_order object (the same measurement in the "
-                         "reference's default move order)")
+    ap.add_argument("--order", choices=("naive", "frontier"), default="frontier",
+                    help="config3 in-kernel move order of the line's value: the reference's default frontier order "
+                         "(CPython set tables carried per game; default) or naive")
+    ap.add_argument("--no-second-order", "--no-naive-order", "--no-frontier-order", dest="no_second_order",
+                    action="store_true",
+                    help="config3: skip the line's object for the other move order (naive_order / frontier_order)")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="config3: skip the line's config5 and config4 objects")
+    ap.add_argument("--extra-config5-games", type=int, default=65536,
+                    help="config3 line's config5 object: searches of the whole job (strong scaling)")
+    ap.add_argument("--extra-config5-iterations", type=int, default=4096,
+                    help="config3 line's config5 object: MCTS iterations per search (one launch)")
+    ap.add_argument("--extra-config4-games", type=int, default=1024,
+                    help="config3 line's config4 object: arena games per rank (weak scaling; 8 ranks = 8,192)")
     a = ap.parse_args(argv)
     if a.steps is None:
         a.steps = 1 if a.workload in ("config5", "config4") else (200 if a.workload == "config2" else 20)
@@ -149,18 +165,22 @@ def ref_python(value, per_core, cores, what):
             "gpu_over_ref_1core": value / per_core, "gpu_over_ref_all_cores": value / (per_core * cores)}
 
 
-def cpu_baseline_playouts(roots_np, seconds, order, rollouts, seed=None, gpu_out=None):
+def cpu_baseline_playouts(roots_np, seconds, order, rollouts, seed=None, gpu_out=None, fast_naive=False):
     """oracle/blokus_oracle.c (C restatement of the reference engine) timed on this
     host's cores on a bounded sample of the same workload, in the SAME move order as the
     GPU line, game-over check after every move like the reference.  Naive order: the
     sample is the first playouts of the last timed step -- same roots (root i //
     rollouts), same Philox streams (seed, playout id) -- so the CPU plays exactly the
     GPU's games, and their result records are compared (gpu_out: that step's uint8
-    [n, 32] results)."""
+    [n, 32] results).  fast_naive: the naive list is built from the frontier set's
+    anchors and sorted row-major (OR_ORDER_NAIVE_VIA_FRONTIER, the same list, ~5x faster
+    than the 400-anchor scan), so the ratio is against the fastest CPU path the oracle has."""
     from oracle import pyoracle as O
     cpu = host_cpu()
     threads = cpu["cores"]
     o = O.ORDER_NAIVE if order == "naive" else O.ORDER_FRONTIER
+    if order == "naive" and fast_naive:
+        o = O.ORDER_NAIVE_VIA_FRONTIER
     same = order == "naive" and seed is not None
     st = (O.State * len(roots_np)).from_buffer_copy(roots_np.tobytes())
     kw = dict(threads=threads, order=o)
@@ -179,7 +199,8 @@ def cpu_baseline_playouts(roots_np, seconds, order, rollouts, seed=None, gpu_out
     out = {"value": n2 / dt, "unit": "sims/s", "cores": threads, "kind": "port", "cpu_model": cpu["model"],
            "host": cpu, "order": order,
            "sample": f"{n2} arena playouts from the same {len(roots_np)} roots, oracle/blokus_oracle.c in "
-                     f"{order} move order, {threads} threads (one per usable core), {dt:.1f} s"}
+                     f"{order} move order{' (list from frontier anchors, sorted)' if o == 2 else ''}, "
+                     f"{threads} threads (one per usable core), {dt:.1f} s"}
     if same and gpu_out is not None:
         g = gpu_out[:n2].cpu().numpy().tobytes()
         out["sample"] += "; the GPU's own games (same roots and Philox streams as the last timed step)"
@@ -330,6 +351,32 @@ def reduce_max_sum(dist, dev, tmax, sums):
     return float(t.item()), [float(x) for x in s.tolist()]
 
 
+def rank_times(dist, dev, t):
+    """Every rank's elapsed seconds (all-gathered), in rank order."""
+    import torch
+    if not dist:
+        return [float(t)]
+    x = torch.tensor([t], dtype=torch.float64, device=dev)
+    parts = [torch.empty_like(x) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, x)
+    return [float(p.item()) for p in parts]
+
+
+def ranks_fields(dist, rank_elapsed, steps, check=None, sha=None):
+    """The N-rank self-check of a line: the world size and backend the
+    process group reports, per-rank ms_per_step (min / max), the SHA-256 of the gathered
+    records in global order, and whether every global index arrived exactly once."""
+    ms = [t / steps * 1e3 for t in rank_elapsed]
+    out = {"world_size_reported": dist.get_world_size() if dist else 1,
+           "backend": dist.get_backend() if dist else None,
+           "ms_per_step_min": min(ms), "ms_per_step_max": max(ms), "ms_per_step_by_rank": ms}
+    if sha is not None:
+        out["records_sha256"] = sha
+    if check is not None:
+        out.update(check)
+    return out
+
+
 def traffic_for(kernel, units_per_launch):
     """PMC HBM bytes and VALU instructions of ONE launch of `kernel` holding
     `units_per_launch` units of work (playouts, board-players or simulations), from the
@@ -392,9 +439,10 @@ def _config3_measure(args, order, gpu, plan, dev, dist):
         barrier_sync(dist)
         elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in events]
+    per_rank = rank_times(dist, dev, elapsed)
     elapsed, (sims, all_plies) = reduce_max_sum(dist, dev, elapsed, [n * args.steps, int(plies_acc.item())])
     return {"elapsed": elapsed, "sims": sims, "plies": all_plies, "kernel_ms": kernel_ms, "out": out,
-            "roots_np": roots_np, "sets_np": sets_np, "n": n}
+            "roots_np": roots_np, "sets_np": sets_np, "n": n, "rank_elapsed": per_rank}
 
 
 def _config3_prepare(args, order, gpu, plan, dev):
@@ -483,9 +531,9 @@ def _config3_cpu(args, order, m, plan, value):
     if order == "frontier":
         cb = cpu_baseline_frontier(m["roots_np"], m["sets_np"], args.cpu_seconds, args.rollouts,
                                    plan.step_seed(1000 + args.steps - 1), m["out"])
-    else:
+    else:  # the naive list built the fastest way the oracle has (frontier anchors + sort)
         cb = cpu_baseline_playouts(m["roots_np"], args.cpu_seconds, order, args.rollouts,
-                                   seed=plan.step_seed(1000 + args.steps - 1), gpu_out=m["out"])
+                                   seed=plan.step_seed(1000 + args.steps - 1), gpu_out=m["out"], fast_naive=True)
     cb["gpu_over_cpu"] = value / cb["value"]
     cb["reference_python"] = ref_python(value, REF_PY_ARENA_SIMS_PER_CORE, cb["cores"],
                                         "terminal random playout from ply 20, telemetry off")
@@ -493,15 +541,18 @@ def _config3_cpu(args, order, m, plan, value):
 
 
 def run_config3(args, world, rank, local, dist):
-    """The default line.  Its value is the --order run (default naive: the reference with
-    BLOKUS_USE_FRONTIER_MOVEGEN=0); with the default order the line also carries a
-    `frontier_order` object, the same measurement in the reference's DEFAULT move order
-    (engine/move_generator.py:261-559 over the CPython frontier sets of
-    engine/board.py:315-367, k_rollout_fr) on the same plan (seeds, streams, steps), with
-    its own value, roofline and same-games CPU baseline."""
+    """The default line.  Its value is the --order run (default: the reference's default
+    frontier order, engine/move_generator.py:261-559 over the CPython frontier sets of
+    engine/board.py:315-367, k_rollout_fr); the line also carries the other order's
+    measurement on the same plan (seeds, streams, steps) -- `naive_order` (the reference
+    with BLOKUS_USE_FRONTIER_MOVEGEN=0, k_rollout) or `frontier_order` -- with its own
+    value, roofline and same-games CPU baseline, and (unless --no-extra-configs) the
+    config5 and config4 objects (run_extra_configs)."""
+    import numpy as np
     import torch
 
     from reinforcementlearning_blokus_amd.gpu import BlokusGPU
+    from reinforcementlearning_blokus_amd.shard import check_indices, gather_blocks, records_sha256
     from reinforcementlearning_blokus_amd.workloads import Config3Plan
     games = args.games or 256
     gpu = BlokusGPU(local)
@@ -510,21 +561,25 @@ def run_config3(args, world, rank, local, dist):
     # r * games .. (r + 1) * games - 1 (workloads.Config3Plan), so the N-rank job's
     # gathered records equal a 1-rank run of the same N * games games
     plan = Config3Plan(args.seed, games, args.rollouts, rank)
+    other = "naive" if args.order == "frontier" else "frontier"
     m = _config3_measure(args, args.order, gpu, plan, dev, dist)
-    mf = None
-    if args.order == "naive" and not args.no_frontier_order:
-        mf = _config3_measure(args, "frontier", gpu, plan, dev, dist)
-    checks = {}
-    if dist and args.check_gather:
-        checks["gather_check"] = _config3_check_gather(args, args.order, gpu, m, rank, world, dist, dev)
-        if mf is not None:
-            checks["frontier_gather_check"] = _config3_check_gather(args, "frontier", gpu, mf, rank, world, dist,
-                                                                    dev)
-    elif dist:
+    mo = None if args.no_second_order else _config3_measure(args, other, gpu, plan, dev, dist)
+    checks, ranks = {}, None
+    if dist:
         # RCCL gather of the last step's terminal results (32 B per playout) over xGMI,
         # outside the timed region; rank r's playouts are the global block r
-        from reinforcementlearning_blokus_amd.shard import gather_blocks
-        gather_blocks(m["out"], rank, world, dist)
+        got = gather_blocks(m["out"], rank, world, dist)
+        idx = check_indices(np.arange(plan.first_game, plan.first_game + games), games * world, world, dist)
+        ranks = ranks_fields(dist, m["rank_elapsed"], args.steps, idx, records_sha256(got) if rank == 0 else None)
+        if mo is not None:
+            goto = gather_blocks(mo["out"], rank, world, dist)
+            ranks[f"{other}_order"] = ranks_fields(dist, mo["rank_elapsed"], args.steps, None,
+                                                   records_sha256(goto) if rank == 0 else None)
+        if args.check_gather:
+            checks["gather_check"] = _config3_check_gather(args, args.order, gpu, m, rank, world, dist, dev)
+            if mo is not None:
+                checks[f"{other}_gather_check"] = _config3_check_gather(args, other, gpu, mo, rank, world, dist, dev)
+    extras = {} if args.no_extra_configs else run_extra_configs(args, world, rank, local, dist)
     if rank != 0:
         return None
     f = _config3_fields(args, args.order, m, world)
@@ -533,26 +588,61 @@ def run_config3(args, world, rank, local, dist):
         "warmup": args.warmup, "ms_per_step": f["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
         "config": {"workload": f["workload"], "games": games, "rollouts_per_game": args.rollouts,
-                   "root_plies": args.root_plies, "playouts_per_step": m["n"],
+                   "root_plies": args.root_plies, "playouts_per_step": m["n"], "move_order": args.order,
                    "parallelism": f"dp{world} (independent games per rank)"},
         "roofline": f["roofline"], "compute_roofline": f["compute_roofline"],
     }
     line.update(checks)
+    if ranks is not None:
+        line["ranks"] = ranks
     if args.share_device:
         line["config"]["parallelism"] += f"; rehearsal: {world} ranks share cuda:0 over gloo"
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = _config3_cpu(args, args.order, m, plan, f["value"])
-    if mf is not None:
-        ff = _config3_fields(args, "frontier", mf, world)
+    if mo is not None:
+        ff = _config3_fields(args, other, mo, world)
+        order_txt = {"frontier": "the reference's default (BLOKUS_USE_FRONTIER_MOVEGEN=1): per (piece, orientation), "
+                                 "anchors by the CPython iteration rank of the mover's frontier set",
+                     "naive": "BLOKUS_USE_FRONTIER_MOVEGEN=0 (engine/move_generator.py:153-259): piece, orientation, "
+                              "anchor row-major"}[other]
         fo = {"value": ff["value"], "unit": "sims/s", "ms_per_step": ff["ms_per_step"], "steps": args.steps,
-              "warmup": args.warmup, "workload": ff["workload"],
-              "order": "the reference's default (BLOKUS_USE_FRONTIER_MOVEGEN=1): per (piece, orientation), "
-                       "anchors by the CPython iteration rank of the mover's frontier set",
+              "warmup": args.warmup, "workload": ff["workload"], "order": order_txt,
               "roofline": ff["roofline"], "compute_roofline": ff["compute_roofline"]}
         if not args.no_cpu_baseline and world == 1:
-            fo["cpu_baseline"] = _config3_cpu(args, "frontier", mf, plan, ff["value"])
-        line["frontier_order"] = fo
+            fo["cpu_baseline"] = _config3_cpu(args, other, mo, plan, ff["value"])
+        line[f"{other}_order"] = fo
+    line.update(extras)
     return line
+
+
+def run_extra_configs(args, world, rank, local, dist):
+    """The default line's config5 and config4 objects, run after the
+    config-3 measurement on the same ranks: config 5 = one 65,536 x 4,096 search launch of
+    the whole job (strong scaling) after a 64-iteration warmup; config 4 = 1,024 arena
+    games per rank (weak scaling: 8 ranks play BASELINE's 8,192) after one warm-up batch.
+    A failure is recorded in the object (the config-3 line still prints)."""
+    import copy
+    import traceback
+
+    import torch
+    out = {}
+    for name, fn, kw in (("config5", run_config5, dict(games=args.extra_config5_games, iterations=args.extra_config5_iterations,
+                                                        chunk=args.extra_config5_iterations,
+                                                        rollout_policy="random")),
+                         ("config4", run_config4, dict(games=args.extra_config4_games * world))):
+        sub = copy.copy(args)
+        sub.__dict__.update(kw, steps=1, warmup=1, workload=name, check_gather=False)
+        try:
+            obj = fn(sub, world, rank, local, dist)
+        except Exception as e:  # noqa: BLE001 -- reported in the line, never hidden
+            obj = {"error": f"{type(e).__name__}: {e}", "traceback": traceback.format_exc()[-2000:]}
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        if rank == 0 and obj is not None:
+            for k in ("n_gpus", "higher_is_better", "vs_baseline", "data"):
+                obj.pop(k, None)
+            out[name] = obj
+    return out
 
 
 # ------------------------------------------------------------------ config 5
@@ -597,9 +687,19 @@ def run_config5(args, world, rank, local, dist):
     sims_local = int(res["iterations_run"].sum()) * args.steps
     plies_local = int(res["rollout_plies"].astype(np.int64).sum())
     unc_local = int(((res["status"] & N.MCTS_EUNCERT) != 0).sum())  # heuristic rollouts only
-    elapsed, (sims, plies, hits, rollouts, unc) = reduce_max_sum(
+    bad_local = int(((res["status"] & ~np.uint32(N.MCTS_EUNCERT)) != 0).sum())
+    ranks = None
+    if dist:
+        # RCCL gather of the 32-byte search records (bk_mcts_out) over xGMI, after the
+        # timed region, in global game order; every game index must arrive exactly once
+        from reinforcementlearning_blokus_amd.shard import check_indices, gather_results, records_sha256
+        loc = torch.from_numpy(np.ascontiguousarray(res).view(np.uint8).reshape(len(res), -1).copy()).to(dev)
+        got = gather_results(loc, total, rank, world, dist)
+        ranks = ranks_fields(dist, rank_times(dist, dev, elapsed), args.steps,
+                             check_indices(mine, total, world, dist), records_sha256(got) if rank == 0 else None)
+    elapsed, (sims, plies, hits, rollouts, unc, bad) = reduce_max_sum(
         dist, dev, elapsed, [sims_local, plies_local * args.steps, int(res["tt_hits"].sum()) * args.steps,
-                             int(res["rollouts"].sum()) * args.steps, unc_local])
+                             int(res["rollouts"].sum()) * args.steps, unc_local, bad_local])
     del stream
     check = None
     if dist and args.check_gather:
@@ -632,6 +732,7 @@ def run_config5(args, world, rank, local, dist):
                    # searches with a HeuristicAgent draw within 2^-40 of a probability boundary
                    # (BK_MCTS_EUNCERT; 0 = every choice certified equal to the reference's)
                    "uncertified_searches": int(unc) if heur else None,
+                   "failed_searches": int(bad),  # any BK_MCTS_E* status but EUNCERT (0 expected)
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
@@ -641,6 +742,8 @@ def run_config5(args, world, rank, local, dist):
     }
     if check is not None:
         line["gather_check"] = check
+    if ranks is not None:
+        line["ranks"] = ranks
     if args.share_device:
         line["config"]["parallelism"] += f"; rehearsal: {world} ranks share cuda:0 over gloo"
     if heur:  # no C restatement of the heuristic search to time: the reference's own numbers
@@ -757,15 +860,17 @@ def run_config4(args, world, rank, local, dist):
                   file=sys.stderr, flush=True)
 
     from reinforcementlearning_blokus_amd.mcts.mcts_agent import SEARCH_TOTALS, reset_search_totals
+    opts = {} if args.search_streams is None else {"search_streams": args.search_streams}
     for _ in range(args.warmup):
-        run_games_batched(cfg, mine[:64], device=local)
+        run_games_batched(cfg, mine[:64], device=local, **opts)
     barrier_sync(dist)
     reset_search_totals()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        recs = run_games_batched(cfg, mine, device=local, progress=progress)
+        recs = run_games_batched(cfg, mine, device=local, progress=progress, **opts)
     barrier_sync(dist)
     elapsed = time.perf_counter() - t0
+    per_rank = rank_times(dist, dev, elapsed)
     st = dict(SEARCH_TOTALS)
     from reinforcementlearning_blokus_amd.arena.runner import LAST_BATCH_PROFILE
     phases = dict(LAST_BATCH_PROFILE)
@@ -774,10 +879,15 @@ def run_config4(args, world, rank, local, dist):
     elapsed, (games, all_sims, all_moves) = reduce_max_sum(dist, dev, elapsed,
                                                            [len(recs) * args.steps, sims * args.steps,
                                                             moves * args.steps])
-    check = None
+    check = ranks = None
     if dist:
+        from reinforcementlearning_blokus_amd.shard import check_indices, records_sha256
         gathered = [None] * world
         dist.all_gather_object(gathered, [(r["game_index"], r["final_scores"], r["moves_made"]) for r in recs])
+        canon = sorted((g[0], [g[1][k] for k in sorted(g[1])], g[2]) for part in gathered for g in part)
+        ranks = ranks_fields(dist, per_rank, args.steps, check_indices([r["game_index"] for r in recs], total, world,
+                                                                       dist),
+                             records_sha256(json.dumps(canon).encode()) if rank == 0 else None)
         if args.check_gather and rank == 0:
             # the sharded job against one process playing all its games (strong scaling)
             one = {r["game_index"]: (r["game_index"], r["final_scores"], r["moves_made"])
@@ -809,8 +919,7 @@ def run_config4(args, world, rank, local, dist):
                    "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
                    "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
                    "rank0_phase_seconds": phases, "host_cores_per_rank": host,
-                   "search_streams": os.environ.get("BK_ARENA_MCTS_STREAMS", "8"),
-                   "pipelined": os.environ.get("BK_ARENA_PIPELINE", "1") != "0",
+                   "search_streams": args.search_streams or 8, "pipelined": True,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default"),
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -825,6 +934,8 @@ def run_config4(args, world, rank, local, dist):
     }
     if check is not None:
         line["gather_check"] = check
+    if ranks is not None:
+        line["ranks"] = ranks
     if args.share_device:
         line["config"]["parallelism"] += f"; rehearsal: {world} ranks share cuda:0 over gloo"
     if not args.no_cpu_baseline and world == 1:
@@ -1055,22 +1166,31 @@ def run_selftest(args, world, rank, local, dist):
 
     if os.environ.get("BENCH_SELFTEST_FAIL_RANK") == str(rank):  # failure injection (tests)
         raise SystemExit(3)
+    from reinforcementlearning_blokus_amd.shard import check_indices, records_sha256
+    t0 = time.perf_counter()
     mine = shard_indices(total, rank, world)
     got = gather_results(torch.from_numpy(records(mine)), total, rank, world, dist) if dist else \
         torch.from_numpy(records(mine))
     plan = Config3Plan(args.seed, c3_games, c3_rollouts, rank)
     c3 = torch.from_numpy(c3_records(plan, 1000))
     c3_got = gather_blocks(c3, rank, world, dist) if dist else c3
+    # the N-rank fields the GPU lines carry (ranks_fields), on the same gathers
+    ranks = ranks_fields(dist, rank_times(dist, "cpu", time.perf_counter() - t0), 1,
+                         check_indices(mine, total, world, dist), records_sha256(got))
+    c3_ranks = check_indices(np.arange(plan.first_game, plan.first_game + c3_games), c3_games * world, world, dist)
     if rank != 0:
         return None
+    if records_sha256(got) != records_sha256(torch.from_numpy(records(range(total)))):
+        raise SystemExit("bench.py --selftest: gathered records' SHA-256 differs from the one-process records'")
     if not np.array_equal(got.numpy(), records(range(total))):
         raise SystemExit("bench.py --selftest: gathered records differ from the one-process records")
     whole = Config3Plan(args.seed, c3_games * world, c3_rollouts, 0)
     if not np.array_equal(c3_got.numpy(), c3_records(whole, 1000)):
         raise SystemExit("bench.py --selftest: gathered config-3 records differ from a one-rank run of the job")
     return {"selftest": "ok", "n_ranks": world, "backend": "gloo" if dist else "none", "games": total,
-            "shard_sizes": [len(shard_indices(total, r, world)) for r in range(world)],
-            "config3": {"games_per_rank": c3_games, "rollouts": c3_rollouts, "job_playouts": whole.n_playouts}}
+            "shard_sizes": [len(shard_indices(total, r, world)) for r in range(world)], "ranks": ranks,
+            "config3": {"games_per_rank": c3_games, "rollouts": c3_rollouts, "job_playouts": whole.n_playouts,
+                        "ranks": c3_ranks}}
 
 
 def main():
@@ -1078,9 +1198,9 @@ def main():
     n = args.gpus or 1
     if "WORLD_SIZE" not in os.environ and n > 1:
         sys.exit(launch_ranks(n, sys.argv[1:]))
-    if args.workload == "config4":  # before the HIP runtime starts (setup imports torch)
-        if args.search_streams is not None:
-            os.environ["BK_ARENA_MCTS_STREAMS"] = str(args.search_streams)
+    # config 4 (alone or as the default line's config4 object): its search streams need
+    # their own hardware queues, set before the HIP runtime starts (setup imports torch)
+    if args.workload == "config4" or (args.workload == "config3" and not args.no_extra_configs):
         if args.hw_queues:
             if not 1 <= args.hw_queues <= 32:
                 raise SystemExit("bench.py: --hw-queues must be in 0..32")

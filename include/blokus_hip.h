@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 5
+#define BK_ABI_VERSION 6
 #define BK_BOARD 20
 #define BK_CELLS 400
 #define BK_PLAYERS 4
@@ -38,6 +38,7 @@ extern "C" {
 #define BK_EHIP -2
 #define BK_ENOMEM -3
 #define BK_EOVERFLOW -4
+#define BK_ECHECK -5 /* a device-side consistency check failed (bk_debug_mcts_failure, ABI 6) */
 
 /* Pointer residency for buffer arguments */
 #define BK_MEM_HOST 0
@@ -74,8 +75,8 @@ typedef struct bk_state {
 /* Legal-move list order used to turn a random index into a move */
 #define BK_ORDER_NAIVE 0    /* piece asc, orientation asc, anchor row-major:
                                LegalMoveGenerator._get_legal_moves_naive, move_generator.py:153 */
-#define BK_ORDER_FRONTIER 1 /* reference default frontier order (move_generator.py:261) -- not yet
-                               available on the GPU path; bk_rollout returns BK_EINVAL */
+#define BK_ORDER_FRONTIER 1 /* reference default frontier order (move_generator.py:261): the
+                               bk_rollout_frontier entry (bk_rollout returns BK_EINVAL for it) */
 
 /* Random streams */
 #define BK_RNG_PHILOX 0   /* native: Philox4x32-10 keyed (seed, playout), counter = draw */
@@ -144,7 +145,8 @@ int bk_stream_create(bk_handle h, const uint32_t* cu_mask, int32_t mask_words, v
    kernel ends, so their input errors and guard trips surface here: BK_EOVERFLOW if a
    persistent kernel's iteration guard tripped (results incomplete), BK_EINVAL if a
    root_index entry was outside [0, n_roots) (that playout ran from root 0 with status
-   bit 2); both cleared once reported. */
+   bit 2); both cleared once reported.  BK_ECHECK: a bk_mcts search broke a tree invariant
+   (bk_debug_mcts_failure has the record). */
 int bk_synchronize(bk_handle h);
 int bk_last_error(bk_handle h, char* buf, size_t len);
 
@@ -259,8 +261,9 @@ int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap);
 /* Diagnostics (tests): one set operation on player's set, set.add((r, c)) (add = 1) or
    set.discard((r, c)) (add = 0), key = r*20+c: the probe / insert / resize code every
    frontier-order kernel runs; add | 2: resize through a small scratch, as the kernels'
-   LDS-staged tables do (tables of <= 128 slots).  BK_EOVERFLOW: the table outgrew its 256
-   slots (128 with add | 2). */
+   LDS-staged tables do (tables of <= 128 slots, a 32-key scratch).  Returns BK_OK, or 1 when
+   the op resized through that scratch (add | 2, <= 32 active keys: the test counts them).
+   BK_EOVERFLOW: the table outgrew its 256 slots (128 with add | 2). */
 int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add);
 
 /*
@@ -488,6 +491,39 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
             int32_t n_zobrist, const int32_t* zobrist_index, uint32_t* mt_state, uint64_t* tt_keys,
             double* tt_vals, int32_t* tt_count, const double* log_table, int32_t log_len,
             bk_mcts_node* nodes, double* rewards, uint8_t* hit_flags, bk_mcts_out* out, int mem);
+
+/*
+ * Failure record of a bk_mcts search whose tree broke an invariant (ABI 6; no reference
+ * counterpart -- the reference's dict-and-object tree cannot be written by another
+ * search).  A node with more visits than the log table allows (BK_MCTS_ELOG: a correct
+ * search of I iterations never exceeds I) or a root whose visits differ from the
+ * iterations run (BK_MCTS_EINTERNAL; mcts/mcts_agent.py:572-582 backpropagates every
+ * iteration through the root) means the search's node pool was written by something
+ * else.  The first such search of a launch records what it saw in a sticky device
+ * buffer; bk_synchronize (and a host-memory bk_mcts) then return BK_ECHECK once, and
+ * bk_debug_mcts_failure copies the record: returns 1 with out[0..n) filled, 0 if no
+ * search ever failed on this handle.  Words: see BK_DIAG_*.
+ */
+#define BK_DIAG_WORDS 64
+#define BK_DIAG_REASON 0      /* BK_MCTS_ELOG or BK_MCTS_EINTERNAL                      */
+#define BK_DIAG_KERNEL 1      /* BK_DIAG_K_*                                            */
+#define BK_DIAG_LAUNCH 2      /* bk_mcts launch number on this handle (1, 2, ...)       */
+#define BK_DIAG_GAME 3        /* the search's index in its launch                       */
+#define BK_DIAG_NODE 4        /* node index in the search's pool (0 = root)             */
+#define BK_DIAG_VISITS 5      /* that node's visits, n_exp, n_legal, child0: words 5..8 */
+#define BK_DIAG_ITERATION 9   /* iterations the search had run                          */
+#define BK_DIAG_DEPTH 10      /* selection depth when it fired (ELOG)                   */
+#define BK_DIAG_LOG_LEN 11
+#define BK_DIAG_HANDOUT 12    /* the launch's game hand-out counter when it fired       */
+#define BK_DIAG_NODE_CAP 13   /* node_cap, nodes_used, cfg.iterations: words 13..15     */
+#define BK_DIAG_PATH_LEN 16   /* root-to-node path entries recorded (<= 22)             */
+#define BK_DIAG_PATH 18       /* path node indices: words 18..39; their visits: 40..61  */
+#define BK_DIAG_K_LANE 0      /* k_mcts      */
+#define BK_DIAG_K_PAIR 1      /* k_mcts_pair */
+#define BK_DIAG_K_H 2         /* k_mcts_h    */
+#define BK_DIAG_K_COOP 3      /* k_mcts_coop */
+#define BK_DIAG_K_COOP_H 4    /* k_mcts_coop_h */
+int bk_debug_mcts_failure(bk_handle h, uint32_t* out, int32_t n);
 
 /* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
    stream, measured with HIP events around that launch. */

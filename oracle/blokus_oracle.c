@@ -366,6 +366,7 @@ int or_legal_moves(const or_board* b, int player, int order, int32_t* out, int c
         const or_orient_t* o = &g_or[g];
         if (b->used[player] >> (o->piece_id - 1) & 1) continue;
         memset(seen + g * 400, 0, 400);
+        const int n0 = n;
         for (int i = 0; i < nf; ++i) {
             int fr_r = fr[i] / 20, fr_c = fr[i] % 20;
             for (int k = 0; k < o->n; ++k) {
@@ -378,6 +379,12 @@ int or_legal_moves(const or_board* b, int player, int order, int32_t* out, int c
                 ++n;
             }
         }
+        if (order == OR_ORDER_NAIVE_VIA_FRONTIER && n <= cap)
+            for (int i = n0 + 1; i < n; ++i) { /* anchors of g row-major: the naive list's order */
+                int32_t v = out[i], j = i - 1;
+                while (j >= n0 && out[j] > v) { out[j + 1] = out[j]; --j; }
+                out[j + 1] = v;
+            }
     }
     return n;
 }

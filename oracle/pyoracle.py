@@ -47,6 +47,9 @@ class MT(C.Structure):
 assert C.sizeof(State) == 256 and C.sizeof(Result) == 32
 
 ORDER_NAIVE, ORDER_FRONTIER = 0, 1
+# the naive list built from the frontier set + a row-major sort (oracle only; bench.py's
+# naive-order CPU baseline): OR_ORDER_NAIVE_VIA_FRONTIER in blokus_oracle.h
+ORDER_NAIVE_VIA_FRONTIER = 2
 SEM_ARENA, SEM_ROLLOUT = 0, 1
 
 

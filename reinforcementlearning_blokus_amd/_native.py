@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # BK_LIB_PATH: load an alternative in-tree build (kernel tuning experiments)
 LIB_PATH = os.environ.get("BK_LIB_PATH") or os.path.join(_HERE, "_lib", "libblokus_hip.so")
 
-OK, EINVAL, EHIP, ENOMEM, EOVERFLOW = 0, -1, -2, -3, -4
+OK, EINVAL, EHIP, ENOMEM, EOVERFLOW, ECHECK = 0, -1, -2, -3, -4, -5
 STATUS_CAP, STATUS_UNCERT, STATUS_STOP, STATUS_BADFORCE = 8, 16, 32, 64  # bk_result.status bits
 FORCE_INDEX = 0x40000000  # bk_arena_step forced[i]: the k-th entry of the legal list (BK_FORCE_INDEX | k)
 FORCE_SKIP = -2  # bk_arena_step forced[i]: leave game i untouched (its search is in flight)
@@ -35,7 +35,11 @@ EXPORTS = (
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
     "bk_arena_step", "bk_mt_cursor_init", "bk_set_tuning", "bk_get_tuning", "bk_debug_fset_op",
+    "bk_debug_mcts_failure",
 )
+# bk_debug_mcts_failure record (include/blokus_hip.h BK_DIAG_*)
+DIAG_WORDS = 64
+DIAG_KERNELS = ("k_mcts", "k_mcts_pair", "k_mcts_h", "k_mcts_coop", "k_mcts_coop_h")
 # bk_set_tuning keys (include/blokus_hip.h BK_TUNE_*), by the environment variable name
 # bk_create reads each from once
 TUNE_KEYS = {name: i for i, name in enumerate((
@@ -119,7 +123,7 @@ RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("statu
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
 assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
 
-ABI_VERSION = 5  # include/blokus_hip.h BK_ABI_VERSION
+ABI_VERSION = 6  # include/blokus_hip.h BK_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -187,6 +191,7 @@ def load():
             "bk_debug_sections": (C.c_int, [vp, vp, C.c_int32, C.c_int32]),
             "bk_set_tuning": (C.c_int, [vp, C.c_int32, C.c_int64]),
             "bk_debug_fset_op": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int32]),
+            "bk_debug_mcts_failure": (C.c_int, [vp, vp, C.c_int32]),
             "bk_get_tuning": (C.c_int, [vp, C.c_int32, P(C.c_int64)]),
         }
         for name, (res, args) in sigs.items():
@@ -350,6 +355,24 @@ class Handle:
 
     def synchronize(self):
         self.check(self._L.bk_synchronize(self._h), "bk_synchronize")
+
+    def mcts_failure(self):
+        """The handle's bk_mcts failure record (bk_debug_mcts_failure) as a dict, or None if
+        no search on it ever broke a tree invariant."""
+        w = (C.c_uint32 * DIAG_WORDS)()
+        rc = self._L.bk_debug_mcts_failure(self._h, w, DIAG_WORDS)
+        if rc < 0:
+            self.check(rc, "bk_debug_mcts_failure")
+        if rc == 0:
+            return None
+        w = list(w)
+        np_ = min(int(w[16]), 22)
+        return {"reason": {16: "ELOG", 32: "EINTERNAL"}.get(w[0], w[0]),
+                "kernel": DIAG_KERNELS[w[1]] if w[1] < len(DIAG_KERNELS) else w[1], "launch": w[2],
+                "game_in_launch": w[3], "node": w[4], "visits": w[5], "n_exp": w[6], "n_legal": w[7],
+                "child0": C.c_int32(w[8]).value, "iterations_done": w[9], "depth": w[10], "log_len": w[11],
+                "handout_counter": w[12], "node_cap": w[13], "nodes_used": w[14], "iterations": w[15],
+                "path": w[18:18 + np_], "path_visits": w[40:40 + np_]}
 
     def set_tuning(self, name: str, value: int | None):
         """bk_set_tuning by environment-variable name (TUNE_KEYS); None = automatic."""

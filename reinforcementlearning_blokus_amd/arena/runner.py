@@ -16,6 +16,7 @@ import time
 import warnings
 import traceback
 from concurrent.futures import ThreadPoolExecutor
+from dataclasses import dataclass
 from datetime import datetime
 from pathlib import Path
 from typing import Any, Dict, List, Mapping, Optional, Sequence, Tuple
@@ -392,7 +393,7 @@ def _mcts_worker() -> ThreadPoolExecutor:
 
 
 class _InlineWorker:
-    """BK_ARENA_SERIAL=1: the MCTS searches run on the calling thread (profiling: cProfile
+    """ArenaOptions.serial_worker: the MCTS searches run on the calling thread (profiling: cProfile
     sees one thread), the same work in the same order."""
 
     @staticmethod
@@ -511,8 +512,8 @@ def _device_agents(run_config: RunConfig, seats_of: Sequence[Mapping[str, str]],
     return mcts, fast, seat_kind, seat_agent
 
 
-def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, log_tables) -> str:
-    """Diagnostics for a search launch that returned a failed search (BK_ARENA_CAPTURE).
+def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, log_tables, record=None) -> str:
+    """Diagnostics for a search launch that returned a failed search (ArenaOptions.capture_dir).
     Saves the launch's inputs as the kernel saw them, its outputs and the failed searches'
     node pools, then replays on a fresh handle and stream with nothing else running:
     (a) the whole launch, (b) the failed searches alone, (c) the whole launch over node
@@ -565,7 +566,7 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
     fields = ["best_move", "iterations_run", "tt_hits", "rollouts", "nodes_used", "status"]
     report = {"seq": job["seq"], "n": int(n), "bad_idx": bad_idx.tolist(), "slot": job["slot"],
               "inflight_at_launch": job["inflight_at_launch"], "key": [iters, roll, c, use_tt, policy],
-              "orig_status": orig["status"][bad_idx].tolist()}
+              "orig_status": orig["status"][bad_idx].tolist(), "failure_record": record}
     runs = [("whole", np.arange(n), False), ("bad_alone", bad_idx, False)]
     if job["nodes"] is not None:
         runs.append(("whole_dirty_pool", np.arange(n), True))
@@ -583,7 +584,8 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
 
 
 def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping[str, str]], gseeds: List[int],
-                      agents_dev, *, run_id: str, device: int, progress=None) -> List[Dict[str, Any]]:
+                      agents_dev, *, run_id: str, device: int, progress=None,
+                      opts: "ArenaOptions") -> List[Dict[str, Any]]:
     """run_games_batched with every position, frontier table and agent stream resident in
     HBM for the whole run.  A round is: bk_arena_step over all games (each first places
     the move its stop seat chose last round, then plays random / heuristic seats to the
@@ -663,26 +665,25 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     forced = np.full(n, -1, np.int32)
     caller = torch.cuda.current_stream(dev)
     stream = caller
-    if os.environ.get("BK_ARENA_DEVICE_PRIORITY", "1") != "0":
+    if opts.high_priority:
         # the per-step kernels (bk_arena_step, FastMCTS, gathers) on a high-priority stream:
         # when a search block frees a CU they are dispatched before queued search blocks
         stream = torch.cuda.Stream(dev, priority=-1)
         stream.wait_stream(caller)
         torch.cuda.set_stream(stream)
-    # MCTS searches run on their own streams and handles (BK_ARENA_MCTS_STREAMS, default
-    # 8) and are not waited for: a game whose search is in flight sits at its stop seat
+    # MCTS searches run on their own streams and handles (opts.search_streams) and are
+    # not waited for: a game whose search is in flight sits at its stop seat
     # (BK_FORCE_SKIP: arena_step does not touch it) while the other games play on and
     # launch their own searches; its move is placed in the first step after the search
     # ends.  FastMCTS seats are decided on the device in the step that stops at them
-    # (fast_on_device), so the next step places their move.  BK_ARENA_PIPELINE=0: one
+    # (fast_on_device), so the next step places their move.  opts.pipeline False: one
     # search at a time on the main stream, waited for at once, FastMCTS host-staged.
-    pipeline = os.environ.get("BK_ARENA_PIPELINE", "1") != "0"
-    # at most 32: torch hands out streams round-robin from a pool of 32 per priority
-    n_slots = min(32, max(1, int(os.environ.get("BK_ARENA_MCTS_STREAMS", "8")))) if pipeline else 1
-    job_games = max(1, int(os.environ.get("BK_ARENA_JOB_GAMES", "1000000"))) if pipeline else 1 << 30
+    pipeline = opts.pipeline
+    n_slots = opts.search_streams if pipeline else 1
+    job_games = opts.job_games if pipeline else 1 << 30
     engines = [BlokusGPU(device) for _ in range(n_slots)] if pipeline else [gpu]
     jstreams = [torch.cuda.Stream(dev) for _ in range(n_slots)] if pipeline else [stream]
-    reserve = int(os.environ.get("BK_ARENA_RESERVE_CUS", "0")) if pipeline else 0
+    reserve = opts.reserve_cus if pipeline else 0
     if reserve > 0:  # search streams may not use `reserve` CUs, spread over the chip (bk_stream_create)
         n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
         step = max(1, n_cu // reserve)
@@ -693,9 +694,9 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         jstreams = [torch.cuda.ExternalStream(e.handle.stream_create(mask), device=dev) for e in engines]
     free_slots = list(range(n_slots))
     jobs: List[Dict[str, Any]] = []
-    # BK_ARENA_CAPTURE=<dir> (diagnostics): keep every search launch's inputs; a launch
-    # that returns a failed search is saved there and replayed alone (_capture_failed_job)
-    capture_dir = os.environ.get("BK_ARENA_CAPTURE", "")
+    # opts.capture_dir (diagnostics): keep every search launch's inputs; a launch that
+    # returns a failed search is saved there and replayed alone (_capture_failed_job)
+    capture_dir = opts.capture_dir or ""
     fast_eng = BlokusGPU(device) if pipeline else gpu
     inflight = np.zeros(n, bool)
 
@@ -754,17 +755,26 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         tl["mcts_job_s"] += time.perf_counter() - job["t0"]
         tl["mcts_job_games"] += len(job["games"])
         eng = engines[job["slot"]]
-        eng.synchronize()  # sticky launch errors
+        sync_err = None
+        try:
+            eng.synchronize()  # sticky launch errors, a failure record (BK_ECHECK)
+        except RuntimeError as e:
+            sync_err = e
         games, aid = job["games"], job["aid"]
         o = job["o_d"].cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(len(games))
         bad = o["status"] & ~np.uint32(N.MCTS_EUNCERT)
-        if bad.any():
+        if bad.any() or sync_err is not None:
+            rec = eng.mcts_failure()  # what the failing search saw (bk_debug_mcts_failure)
+            if rec is not None:
+                rec.update(games=[int(idx[games[rec["game_in_launch"]]])] if rec["game_in_launch"] < len(games) else [],
+                           slot=job["slot"], inflight_at_launch=job["inflight_at_launch"], job_seq=job["seq"])
             where = ""
             if capture_dir:
                 where = " (inputs and replays in " + _capture_failed_job(capture_dir, job, o, bad, zob_d,
-                                                                      log_tables) + ")"
+                                                                      log_tables, rec) + ")"
             raise RuntimeError(f"bk_mcts: {int(np.count_nonzero(bad))} searches stopped early, status bits "
-                               f"{int(np.bitwise_or.reduce(bad))}{where}")
+                               f"{int(np.bitwise_or.reduce(bad)) if bad.any() else 0}; failure record {rec}; "
+                               f"synchronize: {sync_err}{where}")
         prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
         its = o["iterations_run"].astype(np.int64)
         kms, kplies = eng.last_kernel_ms(), int(o["rollout_plies"].astype(np.int64).sum())
@@ -828,7 +838,7 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             e["total_simulations"] += it
             e["moves_with_simulations"] += 1
 
-    def fast_launch(games, aid, nl, counts, quick, ce):  # BK_ARENA_PIPELINE=0: host-staged, waited for
+    def fast_launch(games, aid, nl, counts, quick, ce):  # opts.pipeline False: host-staged, waited for
         mt = np.ascontiguousarray(mtf[aid])
         r = gpu.fastmcts(nl.tolist(), counts, quick.tolist(), mt, _log_table(max(counts) + 1), ce)
         mtf[aid] = mt
@@ -1003,8 +1013,45 @@ def _device_records(out, idx, results, per_agent, final, seats, gseeds, run_conf
                            duration=dt / n, truncated=truncated, per_agent=pa, error=None))
 
 
+@dataclass(frozen=True)
+class ArenaOptions:
+    """How run_games_batched drives the games (never what they play: every setting gives
+    the same records).  Explicit arguments, so nothing in a caller's environment changes
+    the pipeline; the one environment read is the BK_ARENA_CAPTURE diagnostics switch,
+    the default of capture_dir.
+    * device_driver: positions, tables and agent streams resident in HBM for the whole
+      run (bk_arena_step); False: the round-3 host-staged rounds (bk_arena_advance).
+    * pipeline: MCTS searches in flight on `search_streams` streams while the other games
+      play on; False: one search at a time, waited for at once.
+    * search_streams: 1..16.  16 is the most any test has validated (tests/
+      test_gpu_config4_queues.py); round 4's BK_MCTS_ELOG failures came at 24.
+    * job_games: at most this many searches per bk_mcts launch.
+    * reserve_cus: search streams may not use this many CUs (bk_stream_create; slower).
+    * high_priority: the per-step kernels on a high-priority stream.
+    * serial_worker: host-staged driver's searches on the calling thread (profiling).
+    * capture_dir: keep each search launch's inputs; save and replay a failed one."""
+    device_driver: bool = True
+    pipeline: bool = True
+    search_streams: int = 8
+    job_games: int = 1_000_000
+    reserve_cus: int = 0
+    high_priority: bool = True
+    serial_worker: bool = False
+    capture_dir: Optional[str] = None
+
+    def __post_init__(self):
+        if not 1 <= int(self.search_streams) <= MAX_SEARCH_STREAMS:
+            raise ValueError(f"search_streams must be in 1..{MAX_SEARCH_STREAMS}")
+        if int(self.job_games) < 1 or int(self.reserve_cus) < 0:
+            raise ValueError("job_games must be >= 1 and reserve_cus >= 0")
+
+
+MAX_SEARCH_STREAMS = 16
+
+
 def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run_id: str = "gpu",
-                      device: int = 0, progress=None) -> List[Dict[str, Any]]:
+                      device: int = 0, progress=None, options: Optional[ArenaOptions] = None,
+                      **option_kw) -> List[Dict[str, Any]]:
     """Mixed seatings (Random / Heuristic / MCTS / FastMCTS, config 4) in lockstep batches:
     every game's random and heuristic turns run inside bk_arena_advance (one launch
     advances all games to their next search-seat turn, each seat drawing from its own
@@ -1013,7 +1060,8 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     (FastMCTSAgent.think_many), their moves are placed, and the loop repeats.  Records
     equal run_single_game's (arena_runner.py:578-777): same agents, seeds, streams and
     move order.  Per-move times are launch shares.  progress(round, games_left, profile),
-    if given, is called at the start of every round."""
+    if given, is called at the start of every round.  options (or the same fields as
+    keywords, e.g. search_streams=4): ArenaOptions."""
     from .. import _native as N
     from ..engine.move_generator import frontier_ranks, order_moves, order_moves_many
     from ..engine.pieces import ORIENT_CELLS, ORIENT_LIST
@@ -1023,7 +1071,12 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     if n == 0:
         return []
     cfgs = {a.name: a for a in run_config.agents}
-    if os.environ.get("BK_ARENA_DEVICE", "1") != "0":
+    if options is None:
+        option_kw.setdefault("capture_dir", os.environ.get("BK_ARENA_CAPTURE") or None)
+        options = ArenaOptions(**option_kw)
+    elif option_kw:
+        raise TypeError("pass ArenaOptions or its fields as keywords, not both")
+    if options.device_driver:
         t_in = time.perf_counter()
         seats_d, gseeds_d = [], []
         for gi in idx:
@@ -1050,7 +1103,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
             agents_s = time.perf_counter() - t_in
             setup_gc = sum(g["collections"] for g in gc.get_stats()) - gc0
             out = _run_games_device(run_config, idx, seats_d, gseeds_d, ag, run_id=run_id, device=device,
-                                    progress=progress)
+                                    progress=progress, opts=options)
             # host time around the device loop: seats + agents before it, records after it
             LAST_BATCH_PROFILE.update(agents_s=agents_s, seats_s=t_seats - t_in, agents_gc=setup_gc,
                                       records_s=time.perf_counter() - LAST_BATCH_PROFILE["t_end"],
@@ -1098,7 +1151,7 @@ def run_games_batched(run_config: RunConfig, game_indices: Sequence[int], *, run
     # but a host's rounding could pick the neighbour (HeuristicAgent)
     prof.update(setup_s=time.perf_counter() - t0, advance_s=0.0, mcts_s=0.0, fast_s=0.0, host_s=0.0, rounds=0,
                 uncertified_heuristic=0)
-    worker = _InlineWorker() if os.environ.get("BK_ARENA_SERIAL") == "1" else _mcts_worker()
+    worker = _InlineWorker() if options.serial_worker else _mcts_worker()
     while len(active):
         prof["rounds"] += 1
         if progress is not None:

@@ -3466,6 +3466,9 @@ struct MctsArgs {
     int32_t spread;        // only lanes with lane % spread == 0 take searches (more waves, fewer lanes each)
     int32_t coop_walk;     // k_mcts_coop(_h): frontier walk split over the wave (coop_walk), else serial
     int32_t coop_balanced; // k_mcts_coop_h: balanced HeuristicAgent pass (coop_heur_balanced), else per lane
+    uint32_t* diag;        // the handle's failure record (BK_DIAG_WORDS; mc_diag), sticky until read
+    uint32_t launch_seq;   // this launch's number on the handle (recorded in a failure record)
+    uint32_t kernel_id;    // BK_DIAG_K_*: which search kernel runs (recorded in a failure record)
 };
 
 struct Mc {
@@ -3609,6 +3612,51 @@ __device__ __forceinline__ void mc_move_split(uint32_t mv, int& gs, int& ar, int
     ac = cell - 20 * ar;
 }
 
+// Failure record of a search whose tree breaks an invariant: a node
+// visited more often than the log table allows (BK_MCTS_ELOG: a correct search of I
+// iterations has every node's visits <= I < log_len), or a root whose visits differ from
+// the iterations run (BK_MCTS_EINTERNAL: every iteration backpropagates through the root,
+// mcts_agent.py:572-582).  Either means the search's node pool was written by something
+// other than this search.  The first failing search of a launch writes what it saw into
+// the handle's sticky buffer (atomicCAS on word 0; the cooperative kernels' 64 redundant
+// lanes race for it and one wins); bk_synchronize reports it as BK_ECHECK and
+// bk_debug_mcts_failure returns it.  Costs nothing unless it fires.  Words (BK_DIAG_*):
+// 0 reason (BK_MCTS_ELOG / EINTERNAL), 1 kernel, 2 launch number on the handle, 3 the
+// search's game index in the launch, 4 node, 5 node visits, 6 n_exp, 7 n_legal, 8 child0,
+// 9 iterations done, 10 depth, 11 log_len, 12 the game hand-out counter when it fired,
+// 13 node_cap, 14 nodes_used, 15 cfg.iterations, 16 path length recorded, 17 the
+// search's first-touch wall clock (low word), 18..39 the path's nodes from the root,
+// 40..61 their visits.
+__device__ __forceinline__ void mc_diag(const MctsArgs& a, const Mc& m, const int32_t* path, int depth, uint32_t why,
+                                     int32_t node, const bk_mcts_node& nd) {
+    if (!a.diag || atomicCAS(&a.diag[0], 0u, why) != 0u) return;
+    uint32_t* d = a.diag;
+    const bk_mcts_node* pool = a.nodes + (size_t)m.game * a.cfg.node_cap;
+    d[1] = a.kernel_id;
+    d[2] = a.launch_seq;
+    d[3] = (uint32_t)m.game;
+    d[4] = (uint32_t)node;
+    d[5] = nd.visits;
+    d[6] = nd.n_exp;
+    d[7] = nd.n_legal;
+    d[8] = (uint32_t)nd.child0;
+    d[9] = (uint32_t)m.it;
+    d[10] = (uint32_t)depth;
+    d[11] = (uint32_t)a.log_len;
+    d[12] = __hip_atomic_load(&a.counter[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    d[13] = (uint32_t)a.cfg.node_cap;
+    d[14] = (uint32_t)m.nodes_used;
+    d[15] = (uint32_t)a.cfg.iterations;
+    const int np = path ? (depth + 1 < 22 ? depth + 1 : 22) : 0;
+    d[16] = (uint32_t)np;
+    d[17] = (uint32_t)m.t0;
+    for (int k = 0; k < np; ++k) {
+        d[18 + k] = (uint32_t)path[k];
+        d[40 + k] = pool[path[k]].visits;
+    }
+    __threadfence();
+}
+
 // root.board into the lane: rows from the state, tables = the search's root copy
 __device__ __forceinline__ void mc_load_root(const MctsArgs& a, Mc& m, const Slab& slab, McLane* L) {
     const bk_state* s = a.roots + m.game;
@@ -3692,6 +3740,10 @@ __device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m) {
     const int32_t g = m.game;
     const bk_mcts_node* pool = a.nodes + (size_t)g * a.cfg.node_cap;
     const bk_mcts_node root = pool[0];
+    if (root.visits != (uint32_t)m.it && !MC_FATAL(m.status)) {  // every iteration went through the root
+        m.status |= BK_MCTS_EINTERNAL;
+        mc_diag(a, m, nullptr, 0, BK_MCTS_EINTERNAL, 0, root);
+    }
     int32_t best = -1;
     uint32_t bv = 0;
     for (int k = 0; k < (int)root.n_exp; ++k) {  // get_best_move: max visits, first on ties
@@ -3822,7 +3874,11 @@ __device__ __forceinline__ bool mc_select(const MctsArgs& a, Mc& m, McLane* L, c
         const bk_mcts_node nd = pool[u];
         if (!(nd.flags & BK_MCTS_NODE_EVALUATED) || nd.n_legal > nd.n_exp) break;  // expand it
         if (nd.n_exp == 0) { m.node = u; m.depth = depth; m.hash = h; return true; }
-        if ((int32_t)nd.visits >= a.log_len) { m.status |= BK_MCTS_ELOG; break; }
+        if ((int32_t)nd.visits >= a.log_len) {
+            m.status |= BK_MCTS_ELOG;
+            mc_diag(a, m, L->path, depth, BK_MCTS_ELOG, u, nd);
+            break;
+        }
         if (depth >= BK_MCTS_MAX_DEPTH) { m.status |= BK_MCTS_EPATH; break; }
         const double lg = a.log_table[nd.visits];
         const int best = nd.child0 + mc_ucb_best(pool + nd.child0, (int)nd.n_exp, lg, a.cfg.exploration);
@@ -4904,6 +4960,10 @@ struct bk_handle_s {
     void* d_rh = nullptr; size_t d_rh_cap = 0;       // bk_mcts: root hashes computed on the device
     void* d_step = nullptr; size_t d_step_cap = 0;   // bk_arena_step: staged extras
     uint32_t* d_counter = nullptr;
+    uint32_t* d_diag = nullptr;        // bk_mcts failure record (mc_diag), sticky until reported
+    uint32_t diag_host[BK_DIAG_WORDS] = {0};  // the last record bk_synchronize reported
+    bool diag_seen = false;
+    uint32_t mcts_launches = 0;
     int num_cu = 0;
     int rollout_blocks_per_cu = 0;
     int fr_blocks_per_cu = 0;    // k_rollout_fr
@@ -4946,6 +5006,17 @@ static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
         if (_e != hipSuccess) return set_err((h), BK_EHIP, #call ": %s", hipGetErrorString(_e)); \
     } while (0)
 
+// A host-memory launch reports its own device error synchronously, so it clears only its
+// own sticky bit (`own`): any other bit still pending from an earlier device-path launch on
+// the handle (BK_STICKY_GUARD / _ROOT / _FASTMCTS) stays for bk_synchronize to report
+// (clearing the whole word lost them).
+static int clear_own_sticky(bk_handle h, uint32_t sticky, uint32_t own) {
+    if (!(sticky & own)) return BK_OK;
+    const uint32_t rest = sticky & ~own;
+    HIPCHK(h, hipMemcpy(h->d_counter + 2, &rest, sizeof rest, hipMemcpyHostToDevice));
+    return BK_OK;
+}
+
 // every launching entry point: the handle's scratch may be in use by an asynchronous
 // bk_mcts search (BK_MCTS_ASYNC) until bk_synchronize
 #define BK_IDLE(h, name)                                                                \
@@ -4954,6 +5025,22 @@ static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
             return set_err((h), BK_EINVAL, name ": an asynchronous bk_mcts search is still running on " \
                                            "this handle (bk_synchronize first)%s", "");  \
     } while (0)
+
+// A pending bk_mcts failure record (mc_diag) moves to the host copy and is reported once
+// as BK_ECHECK; bk_debug_mcts_failure returns it afterwards.
+static int take_diag(bk_handle h) {
+    uint32_t rec[BK_DIAG_WORDS];
+    HIPCHK(h, hipMemcpy(rec, h->d_diag, sizeof rec, hipMemcpyDeviceToHost));
+    if (!rec[0]) return BK_OK;
+    HIPCHK(h, hipMemset(h->d_diag, 0, sizeof rec));
+    memcpy(h->diag_host, rec, sizeof rec);
+    h->diag_seen = true;
+    char msg[256];
+    snprintf(msg, sizeof msg, "search %u of launch %u (kernel %u) broke a tree invariant (status %u): node %u has %u "
+             "visits after %u iterations (log_len %u, n_exp %u, n_legal %u)", rec[3], rec[2], rec[1], rec[0], rec[4],
+             rec[5], rec[9], rec[11], rec[6], rec[7]);
+    return set_err(h, BK_ECHECK, "bk_mcts: %s; bk_debug_mcts_failure has the record", msg);
+}
 
 static int grow(bk_handle h, void** p, size_t* cap, size_t need) {
     if (need <= *cap) return BK_OK;
@@ -4995,6 +5082,8 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
     if (e == hipSuccess) e = hipEventCreate(&h->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_counter, 4 * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemset(h->d_counter, 0, 4 * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMalloc((void**)&h->d_diag, BK_DIAG_WORDS * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(h->d_diag, 0, BK_DIAG_WORDS * sizeof(uint32_t));
     hipDeviceProp_t prop;
     if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) {
@@ -5037,7 +5126,7 @@ int bk_destroy(bk_handle h) {
     if (h->busy) (void)hipStreamSynchronize(h->busy_stream);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh};
+                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh, h->d_diag};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -5077,6 +5166,7 @@ int bk_synchronize(bk_handle h) {
         h->busy_stream = nullptr;
     }
     HIPCHK(h, hipStreamSynchronize(h->cur));
+    if (int rc = take_diag(h)) return rc;
     uint32_t sticky = 0;
     HIPCHK(h, hipMemcpy(&sticky, h->d_counter + 2, sizeof sticky, hipMemcpyDeviceToHost));
     if (sticky) {
@@ -5089,6 +5179,18 @@ int bk_synchronize(bk_handle h) {
         return set_err(h, BK_EINVAL, "device-path launch: root_index entry outside [0, n_roots)%s", "");
     }
     return BK_OK;
+}
+
+int bk_debug_mcts_failure(bk_handle h, uint32_t* out, int32_t n) {
+    if (!h || !out || n < 1) return BK_EINVAL;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!h->busy) {  // a record still on the device (nobody synchronized since): take it now
+        HIPCHK(h, hipStreamSynchronize(h->cur));
+        (void)take_diag(h);
+    }
+    const int32_t k = n < BK_DIAG_WORDS ? n : BK_DIAG_WORDS;
+    for (int32_t i = 0; i < n; ++i) out[i] = i < k && h->diag_seen ? h->diag_host[i] : 0u;
+    return h->diag_seen ? 1 : 0;
 }
 
 int bk_last_error(bk_handle h, char* buf, size_t len) {
@@ -5498,7 +5600,7 @@ static int launch_playouts(bk_handle h, const bk_state* roots, int32_t n_roots, 
         uint32_t ctr[4];
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipStreamSynchronize(h->cur));
-        if (ctr[2]) HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof(uint32_t)));  // reported here
+        if (int rc = clear_own_sticky(h, ctr[2], BK_STICKY_GUARD)) return rc;  // reported here
         if (ctr[1]) return set_err(h, BK_EOVERFLOW, "bk_rollout: iteration guard tripped%s", "");
     }
     return BK_OK;
@@ -5623,13 +5725,21 @@ int bk_debug_fset_op(bk_fset* s, int32_t player, int32_t key, int32_t add) {
     if (!s || player < 0 || player > 3 || key < 0 || key >= BK_CELLS || s->mask[player] + 1u > BK_FSET_SLOTS)
         return BK_EINVAL;
     int16_t tmp[BK_FSET_SLOTS];
-    // add bit 1: the staged kernels' resize (fs_resize_lds, tables of <= 128 slots)
+    // add bit 1: the staged kernels' resize (fs_resize_lds, tables of <= 128 slots) with a
+    // 32-key scratch, k_mcts_pair's (k_rollout_fr's holds 16: lds_tmp callers).  A resize of
+    // up to 32 active keys then goes through fs_resize_lds (fs_resize_any's choice), and the
+    // call returns 1 so the test can count that the path really ran.
     FsetRef t = fs_ref(s, player, kCellHashHost), lt{};
     if (add & 2) {
         t.cap = 128;
         lt.key = tmp;
+        lt.cap = 32;
     }
-    return fs_op_h(t, tmp, (int16_t)key, (add & 1) != 0, kCellHashHost[key], lt) ? BK_OK : BK_EOVERFLOW;
+    // fs_op_h, spelled out: the op, then the resize it asked for (fs_resize_any's choice)
+    if (!fs_op_nr(t, (int16_t)key, (add & 1) != 0, kCellHashHost[key])) return BK_OK;
+    const bool lds_path = lt.key && *t.used <= lt.cap;
+    if (!fs_resize_any(t, tmp, lt)) return BK_EOVERFLOW;
+    return lds_path ? 1 : BK_OK;
 }
 
 int bk_fset_list(const bk_fset* s, int32_t player, int32_t* out, int32_t cap) {
@@ -5825,7 +5935,7 @@ int bk_fastmcts(bk_handle h, int32_t n_games, const int32_t* legal_offset, const
                                      hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
         HIPCHK(h, hipStreamSynchronize(h->cur));
-        if (ctr[2]) HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof(uint32_t)));  // reported here
+        if (int rc = clear_own_sticky(h, ctr[2], BK_STICKY_FASTMCTS)) return rc;  // reported here
         if (ctr[1]) return set_err(h, BK_EINVAL, "bk_fastmcts: too many children or log table too short%s", "");
     }
     return BK_OK;
@@ -5962,6 +6072,8 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (double*)sec[12].dev, (uint8_t*)sec[13].dev, (bk_mcts_out*)sec[14].dev,
                (uint32_t*)h->d_slab, (McLane*)h->d_mclane, h->d_counter, steps,
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1, 1};
+    a.diag = h->d_diag;
+    a.launch_seq = ++h->mcts_launches;
     a.coop_walk = (int)tune_or(h, BK_TUNE_COOP_WALK, a.coop_walk);
     a.coop_balanced = (int)tune_or(h, BK_TUNE_COOP_BAL, a.coop_balanced);
     // spread 2: the idle odd lane of each pair splits the even lane's stencil (k_mcts_pair)
@@ -5969,15 +6081,19 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     HIPCHK(h, mark_start(h));
     if (coop && heur) {
         h->last_kernel = "k_mcts_coop_h";
+        a.kernel_id = BK_DIAG_K_COOP_H;
         hipLaunchKernelGGL(k_mcts_coop_h, dim3(blocks), dim3(blk), 0, h->cur, a);
     } else if (coop) {
         h->last_kernel = "k_mcts_coop";
+        a.kernel_id = BK_DIAG_K_COOP;
         hipLaunchKernelGGL(k_mcts_coop, dim3(blocks), dim3(blk), 0, h->cur, a);
     } else if (heur) {
         h->last_kernel = "k_mcts_h";
+        a.kernel_id = BK_DIAG_K_H;
         hipLaunchKernelGGL(k_mcts_h, dim3(blocks), dim3(HBLOCK), 0, h->cur, a);
     } else if (spread == 2 && pair) {
         h->last_kernel = "k_mcts_pair";
+        a.kernel_id = BK_DIAG_K_PAIR;
         hipLaunchKernelGGL(k_mcts_pair, dim3(blocks), dim3(BLOCK), 0, h->cur, a);
     } else {
         h->last_kernel = "k_mcts";
@@ -5999,8 +6115,9 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
     }
     HIPCHK(h, hipMemcpyAsync(ctr, h->d_counter, sizeof ctr, hipMemcpyDeviceToHost, h->cur));
     HIPCHK(h, hipStreamSynchronize(h->cur));
-    if (ctr[2]) HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof(uint32_t)));  // reported here
+    if (int rc = clear_own_sticky(h, ctr[2], BK_STICKY_GUARD)) return rc;  // reported here
     if (ctr[1]) return set_err(h, BK_EOVERFLOW, "bk_mcts: step guard tripped%s", "");
+    if (int rc = take_diag(h)) return rc;  // a search broke a tree invariant (mc_diag)
     return BK_OK;
 }
 

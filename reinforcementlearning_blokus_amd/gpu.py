@@ -61,8 +61,15 @@ class BlokusGPU:
 
     def synchronize(self):
         """Wait for this handle's launches; raises if a device-path launch tripped its
-        iteration guard or read a bad root_index (bk_synchronize)."""
+        iteration guard or read a bad root_index, or a search broke a tree invariant
+        (bk_synchronize; mcts_failure() then has the record)."""
         self.handle.synchronize()
+
+    def mcts_failure(self):
+        """The record of the first bk_mcts search on this handle whose tree broke an
+        invariant (a node visited more often than the iterations allow, or root visits !=
+        iterations run), or None (bk_debug_mcts_failure)."""
+        return self.handle.mcts_failure()
 
     def tune(self, **overrides):
         """Set tuning / test overrides of this handle by their environment-variable names

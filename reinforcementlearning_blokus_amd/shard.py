@@ -48,3 +48,30 @@ def gather_blocks(local, rank: int, world: int, dist, device=None):
     parts = [torch.empty_like(local) for _ in range(world)]
     dist.all_gather(parts, local.contiguous())
     return torch.cat([p.to(device or local.device) for p in parts], dim=0)
+
+
+def check_indices(local_ids, n_total: int, world: int, dist):
+    """Every global index 0..n_total-1 arrived from exactly one rank: all-gather each
+    rank's index list (after the timed region) and count.  Returns, on every rank,
+    {"indices": n_total, "every_index_once": bool, "missing": k, "duplicates": k}."""
+    ids = [int(i) for i in np.asarray(local_ids, dtype=np.int64).ravel()]
+    parts = [None] * world
+    if dist is not None:
+        dist.all_gather_object(parts, ids)
+    else:
+        parts = [ids]
+    allv = np.concatenate([np.asarray(p, dtype=np.int64) for p in parts]) if parts else np.zeros(0, np.int64)
+    inside = allv[(allv >= 0) & (allv < n_total)]
+    cnt = np.bincount(inside, minlength=n_total)
+    missing = int((cnt == 0).sum())
+    dup = int((cnt > 1).sum()) + int(len(allv) - len(inside))
+    return {"indices": int(n_total), "every_index_once": missing == 0 and dup == 0, "missing": missing,
+            "duplicates": dup}
+
+
+def records_sha256(records) -> str:
+    """SHA-256 of gathered records in global order (a torch tensor or bytes)."""
+    import hashlib
+    if hasattr(records, "cpu"):
+        records = records.contiguous().cpu().numpy().tobytes()
+    return hashlib.sha256(bytes(records)).hexdigest()

@@ -114,3 +114,23 @@ def test_mt_state_views_match_get_state():
     assert r.get_state()[2:] == ref.get_state()[2:]
     assert r.randint(0, 1000, size=50).tolist() == ref.randint(0, 1000, size=50).tolist()
     assert r.standard_normal() == ref.standard_normal()
+
+
+def test_arena_options_are_arguments_not_environment(monkeypatch):
+    """run_games_batched's pipeline settings are explicit ArenaOptions fields (VERDICT r05
+    item 8): the runner reads one environment variable, the BK_ARENA_CAPTURE diagnostics
+    switch, and rejects stream counts above the validated 16."""
+    import re
+    from pathlib import Path
+
+    from reinforcementlearning_blokus_amd.arena import runner
+    src = Path(runner.__file__).read_text()
+    assert re.findall(r"os\.environ[^\n]*", src) == ['os.environ.get("BK_ARENA_CAPTURE") or None)']
+    assert runner.ArenaOptions().search_streams == 8
+    for bad in (0, 17, 32):
+        with pytest.raises(ValueError):
+            runner.ArenaOptions(search_streams=bad)
+    with pytest.raises(ValueError):
+        runner.ArenaOptions(job_games=0)
+    monkeypatch.setenv("BK_ARENA_MCTS_STREAMS", "24")  # ignored: no longer read
+    assert runner.ArenaOptions().search_streams == 8

@@ -166,7 +166,7 @@ def test_set_operations_slot_for_slot(inplace):
     rnd = random.Random(77)
     cap = 128 if inplace else N.FSET_SLOTS
     cells = [(r, c) for r in range(20) for c in range(20)]
-    ops = long_chains = 0
+    ops = long_chains = lds_resizes = 0
     for trial in range(300):
         s, e = {(0, 0)}, PySet()
         e.add((0, 0))
@@ -183,7 +183,10 @@ def test_set_operations_slot_for_slot(inplace):
             if e.mask + 1 > cap:  # beyond the library's storage: the trial ends here
                 break
             rc = L.bk_debug_fset_op(fs.ctypes.data, 0, k[0] * 20 + k[1], int(add) | (2 if inplace else 0))
-            assert rc == N.OK, rc
+            assert rc in ((N.OK, 1) if inplace else (N.OK,)), rc
+            if rc == 1:  # fs_resize_lds ran (the table resized through the 32-key scratch)
+                assert inplace and int(fs["used"][0, 0]) <= 32 and int(fs["fill"][0, 0]) == int(fs["used"][0, 0])
+                lds_resizes += 1
             ops += 1
             m = int(fs["mask"][0, 0])
             assert m == e.mask and int(fs["fill"][0, 0]) == e.fill and int(fs["used"][0, 0]) == e.used
@@ -193,3 +196,5 @@ def test_set_operations_slot_for_slot(inplace):
             assert N.fset_list(fs, 0) == [r * 20 + c for r, c in s]
         long_chains += e.mask >= 63 and e.fill - e.used > e.used // 2
     assert ops > 50000 and long_chains > 10
+    if inplace:  # most resizes (<= 32 active keys) go through the kernels' scratch path
+        assert lds_resizes > 200, lds_resizes

@@ -1,5 +1,5 @@
 """The config-4 driver with its searches spread over many hardware queues, in a fresh
-process: GPU_MAX_HW_QUEUES=32 and 16 search streams (BK_ARENA_MCTS_STREAMS), the
+process: GPU_MAX_HW_QUEUES=32 and 16 search streams (ArenaOptions.search_streams), the
 setting under which round 4's pipelined driver returned BK_MCTS_ELOG searches
 (profiles/r04/sweeps/r04p/c4_s16_q32.err).  HIP reads GPU_MAX_HW_QUEUES
 when it starts, so the run happens in a child process (started as a child, never an
@@ -34,7 +34,7 @@ from reinforcementlearning_blokus_amd.arena.config import RunConfig
 from reinforcementlearning_blokus_amd.arena.runner import run_games_batched, LAST_BATCH_PROFILE
 cfg = RunConfig.from_dict({{"agents": bench.CONFIG4_AGENTS, "num_games": {n}, "seed": 20260301,
                            "seat_policy": "round_robin"}})
-recs = run_games_batched(cfg, list(range({n})))
+recs = run_games_batched(cfg, list(range({n})), search_streams=16)
 json.dump({{"records": recs, "timeline": LAST_BATCH_PROFILE.get("timeline")}}, open({out!r}, "w"))
 """
 
@@ -43,7 +43,7 @@ json.dump({{"records": recs, "timeline": LAST_BATCH_PROFILE.get("timeline")}}, o
 def child_run(tmp_path_factory):
     d = tmp_path_factory.mktemp("c4q")
     out = str(d / "records.json")
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="32", BK_ARENA_MCTS_STREAMS="16", BK_ARENA_CAPTURE=str(d / "capture"))
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32", BK_ARENA_CAPTURE=str(d / "capture"))
     p = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT, n=N_GAMES, out=out)], env=env,
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-4000:]

@@ -240,3 +240,55 @@ def test_agent_time_limit_ignores_iterations():
     assert move_to_int(mv) in {move_to_int(m) for m in legal}
     assert agent.stats["iterations_run"] > 4
     assert agent.stats["iteration_bound"] >= 4000 and not agent.stats["iteration_bound_reached"]
+
+
+@pytest.mark.parametrize("coop", [0, 1])
+def test_tree_invariant_failures_are_recorded(coop):
+    """Self-diagnosing searches.  A node visited more often than the
+    log table allows (BK_MCTS_ELOG; here forced by a log table shorter than the search on
+    roots with 2..4 legal moves, so the fully expanded root reaches it) and a root whose
+    visits differ from the iterations run (BK_MCTS_EINTERNAL; here a resumed search whose
+    saved pool does not hold the iterations its record claims) each make the first
+    failing search write a failure record: bk_mcts returns BK_ECHECK and
+    bk_debug_mcts_failure names the launch, search, node, visits and root path.  Both the
+    per-lane and the cooperative kernel (one wave per search, 64 lanes racing to record)."""
+    from reinforcementlearning_blokus_amd.gpu import BlokusGPU, mcts_log_table
+    g = BlokusGPU(0)
+    g.tune(MCTS_COOP=coop)
+    assert g.mcts_failure() is None
+    boards = [b for b in oracle_states(40, seed0=500, lo=44, hi=64)
+              if 2 <= len(O.legal_moves(b, b.cur, O.ORDER_FRONTIER)) <= 4][:3]
+    assert len(boards) == 3
+    ztab = O.zobrist_table(4)
+    roots, sets, pl, h = _inputs(boards, [b.cur for b in boards], [ztab] * 3)
+    mt = np.stack([mt_array(O.numpy_mt(70 + i)) for i in range(3)])
+    with pytest.raises(RuntimeError, match=r"failed \(-5\).*broke a tree invariant"):
+        g.mcts(roots, sets, pl, h, iterations=64, zobrist=ztab[None], mt_state=mt, max_rollout_moves=6,
+               log_table=mcts_log_table(64)[:8])
+    rec = g.mcts_failure()
+    assert rec["reason"] == "ELOG" and rec["kernel"] == ("k_mcts_coop" if coop else "k_mcts_pair")
+    assert rec["launch"] == 1 and 0 <= rec["game_in_launch"] < 3
+    assert rec["node"] == 0 and rec["visits"] == 8 and rec["log_len"] == 8 and rec["iterations_done"] == 8
+    assert rec["path"] == [0] and rec["path_visits"] == [8] and rec["n_exp"] == rec["n_legal"] <= 4
+    # EINTERNAL: resume a search whose record says 5 iterations over an empty pool
+    cap = 4 * 64 + 1
+    out = np.zeros(3, dtype=N.MCTS_OUT_DTYPE)
+    out["iterations_run"] = 5
+    out["nodes_used"] = 1
+    nodes = np.zeros((3, cap), dtype=N.MCTS_NODE_DTYPE)
+    rewards = np.zeros((3, 64))
+    flags = np.zeros((3, 64), np.uint8)
+    lt = mcts_log_table(64)
+    zob = np.ascontiguousarray(ztab[None].astype(np.uint64))
+    zi = np.zeros(3, np.int32)
+    cfg = N.BkMctsCfg(64, 6, 1.414, 0, cap, 0, 0, 0, 1, N.MCTS_ROLLOUT_RANDOM, 0)
+    g.handle.set_stream(None)
+    with pytest.raises(RuntimeError, match=r"failed \(-5\)"):
+        g.handle.mcts(roots.ctypes.data, sets.ctypes.data, pl.ctypes.data, h.ctypes.data, 3, cfg, zob.ctypes.data, 1,
+                      zi.ctypes.data, mt.ctypes.data, 0, 0, 0, lt.ctypes.data, len(lt), nodes.ctypes.data,
+                      rewards.ctypes.data, flags.ctypes.data, out.ctypes.data, N.MEM_HOST)
+    rec = g.mcts_failure()
+    assert rec["reason"] == "EINTERNAL" and rec["launch"] == 2 and rec["node"] == 0
+    assert rec["iterations_done"] == 64 and rec["visits"] == 59
+    assert (out["status"] & N.MCTS_EINTERNAL).all()
+    g.synchronize()  # reported once: nothing pending now

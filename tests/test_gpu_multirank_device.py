@@ -32,13 +32,39 @@ def _bench(args, timeout=420):
     return json.loads(lines[0])
 
 
+def _ranks_ok(rk, n_indices):
+    """The N-rank self-check fields (bench.ranks_fields): the group's world size, per-rank
+    step times, the gathered records' SHA-256, every global index exactly once."""
+    assert rk["world_size_reported"] == 2 and rk["backend"] == "gloo"
+    assert len(rk["ms_per_step_by_rank"]) == 2 and 0 < rk["ms_per_step_min"] <= rk["ms_per_step_max"]
+    assert len(rk["records_sha256"]) == 64
+    assert rk["every_index_once"] and rk["indices"] == n_indices
+
+
 def test_config3_two_ranks_equal_one_launch_of_their_games():
-    d = _bench(["--workload", "config3", "--games", "16", "--rollouts", "64", "--steps", "2", "--warmup", "1"])
+    d = _bench(["--workload", "config3", "--games", "16", "--rollouts", "64", "--steps", "2", "--warmup", "1",
+                "--no-extra-configs"])
     assert d["n_gpus"] == 2 and d["value"] > 0
-    assert d["config"]["playouts_per_step"] == 16 * 64
+    assert d["config"]["playouts_per_step"] == 16 * 64 and d["config"]["move_order"] == "frontier"
     assert d["gather_check"] == "ok"
-    assert d["frontier_gather_check"] == "ok"
+    assert d["naive_gather_check"] == "ok"
     assert "rehearsal" in d["config"]["parallelism"]
+    _ranks_ok(d["ranks"], 32)
+    assert len(d["ranks"]["naive_order"]["records_sha256"]) == 64
+
+
+def test_default_line_extra_configs_two_ranks():
+    """The default line's config5 / config4 objects at N = 2 (small sizes): each carries
+    its own value and the N-rank fields; no error recorded."""
+    d = _bench(["--workload", "config3", "--games", "8", "--rollouts", "64", "--steps", "1", "--warmup", "1",
+                "--no-second-order", "--extra-config5-games", "66", "--extra-config5-iterations", "64",
+                "--extra-config4-games", "6"], timeout=600)
+    for name, n in (("config5", 66), ("config4", 12)):
+        o = d[name]
+        assert "error" not in o, o.get("traceback")
+        assert o["value"] > 0 and o["ms_per_step"] > 0 and "roofline" in o
+        _ranks_ok(o["ranks"], n)
+    assert d["config5"]["config"]["failed_searches"] == 0
 
 
 def test_config5_two_ranks_equal_one_process():
@@ -46,9 +72,11 @@ def test_config5_two_ranks_equal_one_process():
                 "--steps", "1", "--warmup", "1"])
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["gather_check"] == "ok"
+    _ranks_ok(d["ranks"], 129)
 
 
 def test_config4_two_ranks_equal_one_process():
     d = _bench(["--workload", "config4", "--games", "24", "--steps", "1", "--warmup", "0"], timeout=600)
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert d["gather_check"] == "ok"
+    _ranks_ok(d["ranks"], 24)

@@ -147,6 +147,23 @@ def test_bench_launches_n_ranks_selftest():
     assert len(lines) == 1
     line = json.loads(lines[0])
     assert line["selftest"] == "ok" and line["n_ranks"] == 2 and line["shard_sizes"] == [501, 500]
+    # the N-rank self-check fields every GPU line carries at N > 1 (bench.ranks_fields)
+    rk = line["ranks"]
+    assert rk["world_size_reported"] == 2 and rk["backend"] == "gloo"
+    assert len(rk["ms_per_step_by_rank"]) == 2 and rk["ms_per_step_min"] <= rk["ms_per_step_max"]
+    assert rk["every_index_once"] and rk["indices"] == 1001 and rk["missing"] == rk["duplicates"] == 0
+    assert len(rk["records_sha256"]) == 64
+    assert line["config3"]["ranks"]["every_index_once"] and line["config3"]["ranks"]["indices"] == 10
+
+
+def test_check_indices_counts_missing_and_duplicates():
+    """shard.check_indices: what rank 0 reports when an index is gathered twice or never."""
+    from reinforcementlearning_blokus_amd.shard import check_indices, records_sha256, shard_indices
+    ok = check_indices(shard_indices(10, 0, 1), 10, 1, None)
+    assert ok == {"indices": 10, "every_index_once": True, "missing": 0, "duplicates": 0}
+    bad = check_indices([0, 1, 1, 3, 12], 5, 1, None)
+    assert bad == {"indices": 5, "every_index_once": False, "missing": 2, "duplicates": 2}
+    assert records_sha256(b"abc") == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
 
 
 def test_bench_rejects_gpus_world_mismatch():

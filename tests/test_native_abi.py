@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bk_abi_version() == N.ABI_VERSION == 5
+    assert lib.bk_abi_version() == N.ABI_VERSION == 6
     assert lib.bk_tables_version() >= 1
 
 

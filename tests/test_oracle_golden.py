@@ -70,6 +70,7 @@ def test_legal_moves_sets_and_orders(idx):
         assert _sha(fr) == ref["sha_frontier"]
         assert _sha(nv) == ref["sha_naive"]
         assert sorted(fr) == sorted(nv)
+        assert O.legal_moves(b, p, O.ORDER_NAIVE_VIA_FRONTIER) == nv  # the naive CPU baseline's list
         if "frontier_list" in ref:
             assert fr == ref["frontier_list"]
             assert nv == ref["naive_list"]

@@ -75,3 +75,17 @@ def test_philox_advance_budget():
     res, trace = O.playout_arena_philox(b, 20260301, 3, max_plies=20)
     assert res.plies == 20 and len([m for m in trace if m >= 0]) == 20
     assert b.move_count == 20
+
+
+def test_naive_via_frontier_plays_the_naive_games():
+    """OR_ORDER_NAIVE_VIA_FRONTIER (bench.py's naive-order CPU baseline: frontier anchors,
+    then a row-major sort) plays exactly the games of the full 400-anchor naive scan."""
+    from tests.helpers import POS, replay, pack_many
+    roots = [replay(POS[i]) for i in (0, 4, 9, 17, 30)]
+    st = (O.State * len(roots)).from_buffer_copy(pack_many(roots).tobytes())
+    seed = 20260301 * 7919 + 1007
+    ridx = np.arange(40, dtype=np.int32) % len(roots)
+    a = O.batch_playouts(st, 40, seed, rng=O.RNG_PHILOX, root_index=ridx, threads=4, order=O.ORDER_NAIVE)
+    b = O.batch_playouts(st, 40, seed, rng=O.RNG_PHILOX, root_index=ridx, threads=4,
+                         order=O.ORDER_NAIVE_VIA_FRONTIER)
+    assert [bytes(r) for r in a] == [bytes(r) for r in b]

@@ -15,8 +15,8 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 step() { local rc=$1; shift; echo "$* rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 declare -A ARGS
-ARGS[config3]="--steps 5 --warmup 1 --no-cpu-baseline --no-frontier-order"
-ARGS[config3fr]="--order frontier --steps 5 --warmup 1 --no-cpu-baseline --no-frontier-order"
+ARGS[config3]="--order naive --steps 5 --warmup 1 --no-cpu-baseline --no-second-order --no-extra-configs"
+ARGS[config3fr]="--order frontier --steps 5 --warmup 1 --no-cpu-baseline --no-second-order --no-extra-configs"
 ARGS[config2]="--workload config2 --steps 50 --warmup 2 --no-cpu-baseline"
 ARGS[config5]="--workload config5 --steps 1 --warmup 0 --no-cpu-baseline"
 ARGS[config4]="--workload config4 --games 1024 --steps 1 --warmup 0 --no-cpu-baseline"
