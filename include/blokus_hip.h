@@ -517,7 +517,12 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
 #define BK_DIAG_HANDOUT 12    /* the launch's game hand-out counter when it fired       */
 #define BK_DIAG_NODE_CAP 13   /* node_cap, nodes_used, cfg.iterations: words 13..15     */
 #define BK_DIAG_PATH_LEN 16   /* root-to-node path entries recorded (<= 22)             */
-#define BK_DIAG_PATH 18       /* path node indices: words 18..39; their visits: 40..61  */
+#define BK_DIAG_PATH 18       /* path node indices: words 18..39; their visits: 40..61
+                                 (ELOG / EINTERNAL records)                             */
+/* Any kernel: a search handed out twice in one launch records BK_DIAG_DOUBLE_START: the
+   search (word 3), the hand-out counter (12), the value handed (17), the block and wave
+   that started it the second time (18, 19), the wave's HW_ID register (20), n_games (21). */
+#define BK_DIAG_DOUBLE_START 0x200u
 #define BK_DIAG_K_LANE 0      /* k_mcts      */
 #define BK_DIAG_K_PAIR 1      /* k_mcts_pair */
 #define BK_DIAG_K_H 2         /* k_mcts_h    */

@@ -366,9 +366,14 @@ class Handle:
         if rc == 0:
             return None
         w = list(w)
+        kern = DIAG_KERNELS[w[1]] if w[1] < len(DIAG_KERNELS) else w[1]
+        if w[0] == 0x200:  # BK_DIAG_DOUBLE_START
+            return {"reason": "DOUBLE_START", "kernel": kern, "launch": w[2], "game_in_launch": w[3],
+                    "handout_counter": w[12], "handed": w[17], "block": w[18], "wave": w[19], "hw_id": w[20],
+                    "n_games": w[21]}
         np_ = min(int(w[16]), 22)
         return {"reason": {16: "ELOG", 32: "EINTERNAL"}.get(w[0], w[0]),
-                "kernel": DIAG_KERNELS[w[1]] if w[1] < len(DIAG_KERNELS) else w[1], "launch": w[2],
+                "kernel": kern, "launch": w[2],
                 "game_in_launch": w[3], "node": w[4], "visits": w[5], "n_exp": w[6], "n_legal": w[7],
                 "child0": C.c_int32(w[8]).value, "iterations_done": w[9], "depth": w[10], "log_len": w[11],
                 "handout_counter": w[12], "node_cap": w[13], "nodes_used": w[14], "iterations": w[15],

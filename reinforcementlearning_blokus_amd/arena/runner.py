@@ -542,10 +542,12 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
                 zob=zob_d.index_select(0, cap["zidx"].long()).cpu().numpy(),
                 key=np.array([iters, roll, use_tt, policy], np.int64), c=np.array([c]))
 
-    def replay(sel, dirty=False):
+    def replay(sel, dirty=False, tune=None):
         s = torch.as_tensor(np.asarray(sel, np.int64), device=dev)
         k = len(sel)
         g = BlokusGPU(dev.index)
+        if tune:
+            g.tune(**tune)
         st = torch.cuda.Stream(dev)
         st.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(st):
@@ -559,24 +561,35 @@ def _capture_failed_job(capture_dir: str, job: Dict[str, Any], o, bad, zob_d, lo
                           tt_keys=tt[0], tt_vals=tt[1], tt_count=tt[2], max_rollout_moves=roll, exploration=c,
                           rollout_policy=policy, asynchronous=True)
         st.synchronize()
-        g.synchronize()
-        return out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(k), g.last_kernel()
+        err = None
+        try:
+            g.synchronize()
+        except RuntimeError as e:  # a failure record (BK_ECHECK): keep it with the replay
+            err = str(e)
+        return out.cpu().numpy().view(N.MCTS_OUT_DTYPE).reshape(k), g.last_kernel(), err, g.mcts_failure()
 
     orig = o
     fields = ["best_move", "iterations_run", "tt_hits", "rollouts", "nodes_used", "status"]
     report = {"seq": job["seq"], "n": int(n), "bad_idx": bad_idx.tolist(), "slot": job["slot"],
               "inflight_at_launch": job["inflight_at_launch"], "key": [iters, roll, c, use_tt, policy],
               "orig_status": orig["status"][bad_idx].tolist(), "failure_record": record}
-    runs = [("whole", np.arange(n), False), ("bad_alone", bad_idx, False)]
+    runs = [("whole", np.arange(n), False, None), ("bad_alone", bad_idx, False, None),
+            ("whole_one_block_per_cu", np.arange(n), False, {"COOP_BLOCKS_PER_CU": 1}),
+            ("whole_per_lane_kernel", np.arange(n), False, {"MCTS_COOP": 0})]
     if job["nodes"] is not None:
-        runs.append(("whole_dirty_pool", np.arange(n), True))
-    for name, sel, dirty in runs:
-        r, kname = replay(sel, dirty)
+        runs.append(("whole_dirty_pool", np.arange(n), True, None))
+    for name, sel, dirty, tune in runs:
+        if len(sel) == 0:
+            continue
+        r, kname, err, rec = replay(sel, dirty, tune)
         arrs["replay_" + name] = r.view(np.uint8)
         ref = orig[sel]
         diff = [int(i) for i in range(len(sel)) if any(r[f][i] != ref[f][i] for f in fields)]
         report[name] = {"kernel": kname, "status_bad": int(np.count_nonzero(r["status"] & ~np.uint32(N.MCTS_EUNCERT))),
-                        "differs_from_launch": [int(sel[i]) for i in diff][:64], "n_differs": len(diff)}
+                        "differs_from_launch": [int(sel[i]) for i in diff][:64], "n_differs": len(diff),
+                        "synchronize_error": err, "failure_record": rec,
+                        "best_move": r["best_move"].tolist(), "iterations_run": r["iterations_run"].tolist(),
+                        "status": r["status"].tolist()}
     np.savez_compressed(base + ".npz", **arrs)
     with open(base + ".json", "w") as f:
         json.dump(report, f, indent=1)

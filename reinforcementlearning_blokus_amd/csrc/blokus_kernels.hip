@@ -3469,6 +3469,7 @@ struct MctsArgs {
     uint32_t* diag;        // the handle's failure record (BK_DIAG_WORDS; mc_diag), sticky until read
     uint32_t launch_seq;   // this launch's number on the handle (recorded in a failure record)
     uint32_t kernel_id;    // BK_DIAG_K_*: which search kernel runs (recorded in a failure record)
+    uint32_t* started;     // one bit per search of the launch, set when a wave starts it (mc_mark_started)
 };
 
 struct Mc {
@@ -3683,6 +3684,33 @@ __device__ __forceinline__ void mc_load_root(const MctsArgs& a, Mc& m, const Sla
     for (int R = 0; R < 20; ++R) slab.at(4, R) = occ[R];
     m.first = s->first_move & 0xFu;
     copy_fset(&L->A.s, &L->root);
+}
+
+// A search is started exactly once per launch.  The launch's bitmap takes one atomicOr
+// per start (one lane per search); a bit already set means two waves / lanes were handed
+// the same search, which would interleave two searches over one node pool: the second
+// start writes a failure record (BK_DIAG_DOUBLE_START, with both hand-out values it can
+// see) and the caller stops that search with BK_MCTS_EINTERNAL.
+__device__ __forceinline__ bool mc_mark_started(const MctsArgs& a, int32_t g, uint32_t handed) {
+    if (!a.started) return false;
+    const uint32_t old = atomicOr(&a.started[(uint32_t)g >> 5], 1u << ((uint32_t)g & 31u));
+    if (!((old >> ((uint32_t)g & 31u)) & 1u)) return false;
+    if (a.diag && atomicCAS(&a.diag[0], 0u, BK_DIAG_DOUBLE_START) == 0u) {
+        uint32_t* d = a.diag;
+        d[1] = a.kernel_id;
+        d[2] = a.launch_seq;
+        d[3] = (uint32_t)g;
+        d[12] = __hip_atomic_load(&a.counter[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        d[17] = handed;
+        d[18] = (uint32_t)blockIdx.x;
+        d[19] = (uint32_t)(threadIdx.x / WAVE);
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        d[20] = hw;
+        d[21] = (uint32_t)a.n_games;
+        __threadfence();
+    }
+    return true;
 }
 
 __device__ __forceinline__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab) {
@@ -3981,7 +4009,9 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
             if (m.game < 0) {
                 const int32_t next = (int32_t)atomicAdd(&a.counter[0], 1u);
                 if (next >= a.n_games) { done = true; break; }
+                const bool twice = mc_mark_started(a, next, (uint32_t)next);
                 mc_start_game(a, m, L, next, htab);
+                if (twice) m.status |= BK_MCTS_EINTERNAL;
             }
             const bool timed_out = a.cfg.time_limit_us > 0 &&
                                    wall_clock64() - m.t0 >= a.limit_ticks;
@@ -4286,7 +4316,9 @@ __global__ void k_mcts_h(MctsArgs a);
 // orientation order.  The searches are the reference's, as in k_mcts / k_mcts_h (tests
 // run both kernels on the same batches).
 // ------------------------------------------------------------------------------------
+#ifndef COOP_WAVES
 #define COOP_WAVES 2                             // searches (waves) per block
+#endif
 #ifndef BK_COOP_ML_LDS
 #define BK_COOP_ML_LDS 1  // k_mcts_coop_h keeps the search's McLane in LDS
 #endif
@@ -4688,7 +4720,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // is rebuilt from the root at every iteration, so nothing outside the wave reads it
     const Slab slab{BK_COOP_SLAB_LDS ? coop_slab[wv] : a.slab + (size_t)slot * SLAB_WORDS};
     McLane* L = ML_LDS ? &coop_ml[ML_LDS ? wv : 0] : a.lanes + slot;
-    Mc m;
+    Mc m{};
     m.game = -1;
     m.mode = MC_SELECT;
     int root_mc = 0;  // Board.move_count of the search's root
@@ -4713,7 +4745,11 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
                 if (lane == 0) next = (int32_t)atomicAdd(&a.counter[0], 1u);
                 next = __shfl(next, 0);
                 if (next >= a.n_games) { done = true; break; }
+                uint32_t twice = 0;
+                if (lane == 0) twice = mc_mark_started(a, next, (uint32_t)next) ? 1u : 0u;
+                twice = __shfl(twice, 0);
                 mc_start_game(a, m, L, next, htab);
+                if (twice) m.status |= BK_MCTS_EINTERNAL;
                 root_mc = (int)a.roots[next].move_count;  // (constant for the search)
             }
             const bool timed_out = a.cfg.time_limit_us > 0 && wall_clock64() - m.t0 >= a.limit_ticks;
@@ -4961,6 +4997,7 @@ struct bk_handle_s {
     void* d_step = nullptr; size_t d_step_cap = 0;   // bk_arena_step: staged extras
     uint32_t* d_counter = nullptr;
     uint32_t* d_diag = nullptr;        // bk_mcts failure record (mc_diag), sticky until reported
+    void* d_started = nullptr; size_t d_started_cap = 0;  // bk_mcts: searches started (mc_mark_started)
     uint32_t diag_host[BK_DIAG_WORDS] = {0};  // the last record bk_synchronize reported
     bool diag_seen = false;
     uint32_t mcts_launches = 0;
@@ -5013,7 +5050,8 @@ static int set_err(bk_handle h, int code, const char* fmt, const char* detail) {
 static int clear_own_sticky(bk_handle h, uint32_t sticky, uint32_t own) {
     if (!(sticky & own)) return BK_OK;
     const uint32_t rest = sticky & ~own;
-    HIPCHK(h, hipMemcpy(h->d_counter + 2, &rest, sizeof rest, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpyAsync(h->d_counter + 2, &rest, sizeof rest, hipMemcpyHostToDevice, h->cur));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
     return BK_OK;
 }
 
@@ -5030,15 +5068,22 @@ static int clear_own_sticky(bk_handle h, uint32_t sticky, uint32_t own) {
 // as BK_ECHECK; bk_debug_mcts_failure returns it afterwards.
 static int take_diag(bk_handle h) {
     uint32_t rec[BK_DIAG_WORDS];
-    HIPCHK(h, hipMemcpy(rec, h->d_diag, sizeof rec, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpyAsync(rec, h->d_diag, sizeof rec, hipMemcpyDeviceToHost, h->cur));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
     if (!rec[0]) return BK_OK;
-    HIPCHK(h, hipMemset(h->d_diag, 0, sizeof rec));
+    HIPCHK(h, hipMemsetAsync(h->d_diag, 0, sizeof rec, h->cur));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
     memcpy(h->diag_host, rec, sizeof rec);
     h->diag_seen = true;
     char msg[256];
-    snprintf(msg, sizeof msg, "search %u of launch %u (kernel %u) broke a tree invariant (status %u): node %u has %u "
-             "visits after %u iterations (log_len %u, n_exp %u, n_legal %u)", rec[3], rec[2], rec[1], rec[0], rec[4],
-             rec[5], rec[9], rec[11], rec[6], rec[7]);
+    if (rec[0] == BK_DIAG_DOUBLE_START)
+        snprintf(msg, sizeof msg, "search %u of launch %u (kernel %u) was started twice (second start by block %u wave "
+                 "%u, hw_id 0x%x, hand-out counter %u, %u searches)", rec[3], rec[2], rec[1], rec[18], rec[19], rec[20],
+                 rec[12], rec[21]);
+    else
+        snprintf(msg, sizeof msg, "search %u of launch %u (kernel %u) broke a tree invariant (status %u): node %u has "
+                 "%u visits after %u iterations (log_len %u, n_exp %u, n_legal %u)", rec[3], rec[2], rec[1], rec[0],
+                 rec[4], rec[5], rec[9], rec[11], rec[6], rec[7]);
     return set_err(h, BK_ECHECK, "bk_mcts: %s; bk_debug_mcts_failure has the record", msg);
 }
 
@@ -5081,9 +5126,16 @@ int bk_create(int device, uint32_t flags, bk_handle* out) {
     if (e == hipSuccess) e = hipEventCreate(&h->ev0);
     if (e == hipSuccess) e = hipEventCreate(&h->ev1);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_counter, 4 * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(h->d_counter, 0, 4 * sizeof(uint32_t));
+    // The handle's device words are zeroed on its own stream and waited for HERE.  A plain
+    // hipMemset runs on the legacy null stream, which is not ordered with the
+    // non-blocking streams launches go to (torch's, bk_set_stream): under load it could
+    // land after the handle's first kernel had started and reset its hand-out counter
+    // mid-launch, handing searches out twice (the round-4 / round-6 BK_MCTS_ELOG failures,
+    // DESIGN.md 4).  No entry point touches device memory on the null stream.
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_counter, 0, 4 * sizeof(uint32_t), h->own);
     if (e == hipSuccess) e = hipMalloc((void**)&h->d_diag, BK_DIAG_WORDS * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemset(h->d_diag, 0, BK_DIAG_WORDS * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemsetAsync(h->d_diag, 0, BK_DIAG_WORDS * sizeof(uint32_t), h->own);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->own);
     hipDeviceProp_t prop;
     if (e == hipSuccess) e = hipGetDeviceProperties(&prop, device);
     if (e != hipSuccess) {
@@ -5126,7 +5178,7 @@ int bk_destroy(bk_handle h) {
     if (h->busy) (void)hipStreamSynchronize(h->busy_stream);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh, h->d_diag};
+                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh, h->d_diag, h->d_started};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -5168,9 +5220,11 @@ int bk_synchronize(bk_handle h) {
     HIPCHK(h, hipStreamSynchronize(h->cur));
     if (int rc = take_diag(h)) return rc;
     uint32_t sticky = 0;
-    HIPCHK(h, hipMemcpy(&sticky, h->d_counter + 2, sizeof sticky, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpyAsync(&sticky, h->d_counter + 2, sizeof sticky, hipMemcpyDeviceToHost, h->cur));
+    HIPCHK(h, hipStreamSynchronize(h->cur));
     if (sticky) {
-        HIPCHK(h, hipMemset(h->d_counter + 2, 0, sizeof sticky));
+        HIPCHK(h, hipMemsetAsync(h->d_counter + 2, 0, sizeof sticky, h->cur));
+        HIPCHK(h, hipStreamSynchronize(h->cur));
         if (sticky & BK_STICKY_GUARD)
             return set_err(h, BK_EOVERFLOW, "device-path launch: iteration guard tripped, results incomplete%s", "");
         if (sticky & BK_STICKY_FASTMCTS)
@@ -6074,6 +6128,13 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1, 1};
     a.diag = h->d_diag;
     a.launch_seq = ++h->mcts_launches;
+    {
+        const size_t sb = sizeof(uint32_t) * (((size_t)n_games + 31) / 32 + 1);
+        rc = grow(h, &h->d_started, &h->d_started_cap, sb);
+        if (rc) return rc;
+        HIPCHK(h, hipMemsetAsync(h->d_started, 0, sb, h->cur));
+        a.started = (uint32_t*)h->d_started;
+    }
     a.coop_walk = (int)tune_or(h, BK_TUNE_COOP_WALK, a.coop_walk);
     a.coop_balanced = (int)tune_or(h, BK_TUNE_COOP_BAL, a.coop_balanced);
     // spread 2: the idle odd lane of each pair splits the even lane's stencil (k_mcts_pair)
