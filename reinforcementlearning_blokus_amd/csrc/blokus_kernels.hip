@@ -68,29 +68,15 @@
 #define BK_TU 0
 #endif
 #define BK_DEF(u) (BK_TU == 0 || BK_TU == (u))
-// locate pass 2 skips frontier cells with no anchor row within the piece's height (A/B
-// build: -DBK_LOCATE_SKIP=0)
-#ifndef BK_LOCATE_SKIP
-#define BK_LOCATE_SKIP 1
-#endif
-// ... and compacts each 16-slot batch to the slots that can add an anchor before the
-// row reads, so the wave runs them max-over-lanes-of-relevant-slots times instead of 16:
-// frontier-order config 3 25.8 -> 27.9 M playouts/s, config 5 16.2 -> 17.2 M sims/s
-// (profiles/r04/sweeps/r04p; -DBK_LOCATE_COMPACT=0 for the per-slot walk)
-#ifndef BK_LOCATE_COMPACT
-#define BK_LOCATE_COMPACT 1
-#endif
-// place_frontier loads a <= BK_STAGE_EAGER_MAX-slot stage alongside the table's mask:
-// one memory latency instead of two.  Within noise for the 3-block k_rollout_fr
-// (profiles/r04/sweeps/r04p); +1.0 % for the 4-block one, 31.73 -> 32.03 M playouts/s
-// over three pairs of runs (profiles/r04/sweeps/r04v).  A/B: -DBK_STAGE_EAGER=0
-#ifndef BK_STAGE_EAGER
-#define BK_STAGE_EAGER 1
-#endif
-
-#ifndef BK_STAGE_EAGER_MAX
-#define BK_STAGE_EAGER_MAX 64
-#endif
+// Locate pass 2 skips frontier cells with no anchor row within the piece's height, and
+// compacts each 16-slot batch to the slots that can add an anchor before the row reads,
+// so the wave runs them max-over-lanes-of-relevant-slots times instead of 16
+// (frontier-order config 3 25.8 -> 27.9 M playouts/s, config 5 16.2 -> 17.2 M sims/s,
+// profiles/r04/sweeps/r04p).  place_frontier loads a stage of <= STAGE_EAGER_MAX slots
+// alongside the table's mask: one memory latency instead of two (+1.0 % for the 4-block
+// k_rollout_fr, profiles/r04/sweeps/r04v).  The measured-slower alternatives of these
+// and the other A/B knobs below are out of the source; DESIGN.md 4 keeps their numbers.
+#define STAGE_EAGER_MAX 64
 
 // Section timers (diagnostic build only, -DBK_SECTION_PROF): per-wave shader-clock
 // cycles spent in each section of a kernel's loop, summed over waves into
@@ -199,18 +185,15 @@ __device__ __forceinline__ uint32_t plane_row(const uint64_t* w, int R) {
 // adds one per-lane term), rows move as dwordx4; the record stays L1/L2-resident.
 #define SLAB_FIELDS 5
 #define SLAB_RNG_BASE (SLAB_FIELDS * 20)
-// BK_SLAB_PAD: each lane's record starts on a 128-byte line (512-byte stride instead of
-// 464): with FsLane's padding below, frontier-order config 3 31.9 -> 33.5 M playouts/s
+// Each lane's record starts on a 128-byte line (512-byte stride instead of 464): with
+// FsLane's padding below, frontier-order config 3 31.9 -> 33.5 M playouts/s
 // (profiles/r05/sweeps/r05b); the per-lane records of 262,144 resident lanes far exceed
 // the L2 and the Infinity Cache, so every line a ply touches is a memory round trip
-#ifndef BK_SLAB_PAD
-#define BK_SLAB_PAD 1
-#endif
 // frontier-order rollouts: the four players' table headers (mask, fill, used as uint16)
 // live in the slab, in the line the occupancy plane ends in (read every ply anyway),
 // instead of in the FsLane record's own header line
 #define SLAB_HDR_BASE (SLAB_RNG_BASE + 16)
-#define SLAB_WORDS (BK_SLAB_PAD ? 128 : SLAB_HDR_BASE + 8)
+#define SLAB_WORDS 128
 static_assert(SLAB_HDR_BASE + 6 <= SLAB_WORDS, "the table headers fit the slab");
 struct Slab {
     uint32_t* base;  // = slab + slot * SLAB_WORDS (16-byte aligned)
@@ -394,27 +377,10 @@ struct StencilClass {
 // of areas fill the CU's LDS: at 4 blocks/CU (128 VGPRs, 256 B/lane of scratch, spills
 // mostly on the cold paths) 31.8 M playouts/s vs 27.9 M at 3 blocks with the hashes in
 // LDS, 26.8 M at 3 blocks with them in global memory (profiles/r04/sweeps/r04r).
-// A/B: -DBK_FR_HTAB_LDS=1 -DFR_BLOCKS_PER_CU=3
-#ifndef BK_FR_HTAB_LDS
-#define BK_FR_HTAB_LDS 0
-#endif
-#ifndef FR_BLOCKS_PER_CU
 #define FR_BLOCKS_PER_CU 4
-#endif
-// rollout_body: launder the slot / lane index per ply (bit 0: k_rollout_fr(_h), bit 1:
-// k_rollout / k_advance)
-#ifndef BK_ROLL_OPAQUE
-#define BK_ROLL_OPAQUE 3
-#endif
-// tables probed in global memory read 8-slot chunks (FsetRef::gchunk, fs_probe)
-#ifndef BK_GLOBAL_CHUNK
-#define BK_GLOBAL_CHUNK 1
-#endif
+// Tables probed in global memory read 8-slot chunks (FsetRef::gchunk, fs_probe);
 // LDS-staged frontier tables resize through an LDS scratch (fs_resize_lds) where the
-// caller has one; 0: always through the record's global tmp (fs_resize)
-#ifndef BK_RESIZE_LDS
-#define BK_RESIZE_LDS 1
-#endif
+// caller has one, else through the record's global tmp (fs_resize).
 #ifndef MCTS_BLOCKS_PER_CU
 #define MCTS_BLOCKS_PER_CU 2
 #endif
@@ -765,7 +731,6 @@ __device__ __forceinline__ void locate_move_frontier(const OrientRow& orow, uint
         const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
         const uint4 na = k4[(nb0 >> 4) * RS], nb = k4[(nb0 >> 4) * RS + 1];
         const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-#if BK_LOCATE_COMPACT
         // the batch's slots that can add an anchor, then one divergent pass over just
         // those: the wave runs the row reads max-over-lanes-of-relevant-slots times
         uint32_t rel = 0;
@@ -784,16 +749,6 @@ __device__ __forceinline__ void locate_move_frontier(const OrientRow& orow, uint
             for (int q = 1; q < 8; ++q) wj = (j >> 1) == q ? w[q] : wj;
             const int f = (int)(int16_t)((j & 1) ? (wj >> 16) : (wj & 0xFFFFu));
             const int fr = f / 20, fc = f - 20 * fr;
-#else
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
-            if (hit_f >= 0 || f < 0 || b0 + j > mask) continue;
-            const int fr = f / 20, fc = f - 20 * fr;
-            // no anchor row among fr - H + 1 .. fr: this cell adds no anchors (skip the
-            // row reads); anchors counted later only clear bits, so arows stays a superset
-            if (BK_LOCATE_SKIP && !((arows >> (fr + 5 - H)) & hmask)) continue;
-#endif
             uint32_t hm[5], tot = 0;
 #pragma unroll
             for (int d = 0; d < 5; ++d) {
@@ -900,7 +855,6 @@ __device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2*
         const int nb0 = b0 + 16 <= mask ? b0 + 16 : b0;
         const uint4 na = k4[(nb0 >> 4) * RS], nb = k4[(nb0 >> 4) * RS + 1];
         const uint32_t w[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-#if BK_LOCATE_COMPACT
         uint32_t rel = 0;  // as locate_move_frontier (the pair's lanes hold the same mask)
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -917,14 +871,6 @@ __device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2*
             for (int q = 1; q < 8; ++q) wj = (j >> 1) == q ? w[q] : wj;
             const int f = (int)(int16_t)((j & 1) ? (wj >> 16) : (wj & 0xFFFFu));
             const int fr = f / 20, fc = f - 20 * fr;
-#else
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int f = (int)(int16_t)((j & 1) ? (w[j >> 1] >> 16) : (w[j >> 1] & 0xFFFFu));
-            if (hit_f >= 0 || f < 0 || b0 + j > mask) continue;
-            const int fr = f / 20, fc = f - 20 * fr;
-            if (BK_LOCATE_SKIP && !((arows >> (fr + 5 - H)) & hmask)) continue;
-#endif
             uint32_t hm[3], tot = 0;
 #pragma unroll
             for (int t = 0; t < 3; ++t) {
@@ -1868,7 +1814,7 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
 // for `keys` keys (none: nullptr)
 __device__ __forceinline__ FsetRef lds_tmp(int16_t* ltk, uint32_t keys) {
     FsetRef r{};
-    if (BK_RESIZE_LDS && ltk) {
+    if (ltk) {
         r.key = ltk;
         r.stride = 2 * WAVE;
         r.cap = keys;
@@ -1877,17 +1823,12 @@ __device__ __forceinline__ FsetRef lds_tmp(int16_t* ltk, uint32_t keys) {
 }
 
 // per-lane frontier record in the rollout kernel: the tables plus resize scratch.
-// BK_FSLANE_PAD: padded to whole 128-byte lines, so each player's table starts on a line
-// and a table of <= 64 slots is ONE line (2,592 -> 2,688 bytes; see BK_SLAB_PAD)
-#ifndef BK_FSLANE_PAD
-#define BK_FSLANE_PAD 1
-#endif
+// padded to whole 128-byte lines, so each player's table starts on a line and a table of
+// <= 64 slots is ONE line (2,592 -> 2,688 bytes; see the slab's padding)
 struct FsLane {
     bk_fset s;
     int16_t tmp[BK_FSET_SLOTS];
-#if BK_FSLANE_PAD
     int16_t pad[48];  // 2592 -> 2688 bytes
-#endif
 };
 
 // update_frontier_after_move (engine/board.py:315-367) of player p's table in fl for a
@@ -1964,10 +1905,10 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     uint16_t* const hm = hdr ? hdr : &gfs->mask[p];
     uint16_t* const hf = hdr ? hdr + 1 : &gfs->fill[p];
     uint16_t* const hu = hdr ? hdr + 2 : &gfs->used[p];
-    // BK_STAGE_EAGER: stages of <= 64 slots load all STAGE slots at once, alongside the
+    // stages of <= STAGE_EAGER_MAX slots load all STAGE slots at once, alongside the
     // mask (the storage holds BK_FSET_SLOTS >= STAGE): one memory latency instead of the
     // mask's, then the table's
-    constexpr bool EAGER = BK_STAGE_EAGER && STAGE > 0 && STAGE <= BK_STAGE_EAGER_MAX;
+    constexpr bool EAGER = STAGE > 0 && STAGE <= STAGE_EAGER_MAX;
     const bk_u4_alias* src4 = reinterpret_cast<const bk_u4_alias*>(gfs->key[p]);
     uint4 pre[EAGER ? STAGE / 8 : 1];
     if constexpr (EAGER) {
@@ -2029,7 +1970,7 @@ __device__ __forceinline__ bool place_frontier(FsLane* fl, int p, int16_t* lk, c
     // (a table too large for the stage: its resizes use the lane's whole column of the
     // area, STAGE keys, as their scratch -- the stage is not in use)
     FsetRef gt{gfs->key[p], 2, hm, hf, hu, BK_FSET_SLOTS, htab};
-    gt.gchunk = BK_GLOBAL_CHUNK && ltk != nullptr;  // (the playout kernels: k_rollout_fr)
+    gt.gchunk = ltk != nullptr;  // (the playout kernels: k_rollout_fr)
     if (!fs_run_ops(gt, fl->tmp, cells, real, lds_tmp(ltk ? lk : nullptr, (uint32_t)STAGE))) return false;
     if constexpr (RECOPY) return fs_recopy_global(fl, p, htab);  // (MCTS records: hdr is nullptr)
     return true;
@@ -2894,10 +2835,10 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     constexpr int BLK = HEUR ? HBLOCK : BLOCK;
     constexpr int AREA = HEUR ? HEUR_WORDS : FR ? ROLL_WORDS_FR : ROLL_WORDS_PER_WAVE;
     constexpr int HS_WORDS = HEUR ? (int)(sizeof(HeurShared) + 7) / 4 : 0;
-    // FR: + the CPython cell hashes (shared by the block) for the frontier tables (or,
-    // BK_FR_HTAB_LDS=0, read from global memory through the L1: k_rollout_fr's LDS then
-    // fits 4 blocks per CU); HEUR: + the policy's exp tables
-    constexpr bool HT_LDS = FR && (HEUR || BK_FR_HTAB_LDS);
+    // HEUR (k_rollout_fr_h): + the CPython cell hashes (shared by the block) for the
+    // frontier tables and the policy's exp tables; k_rollout_fr reads the hashes from
+    // global memory through the L1, so its LDS fits 4 blocks per CU
+    constexpr bool HT_LDS = FR && HEUR;
     __shared__ __attribute__((aligned(16))) uint32_t lds[AREA * (BLK / WAVE) + (HT_LDS ? 2 * BK_CELLS : 0) + HS_WORDS];
     const int lane0 = threadIdx.x & (WAVE - 1), wv = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
     uint64_t* htab_lds = reinterpret_cast<uint64_t*>(lds + AREA * (BLK / WAVE));
@@ -2909,11 +2850,9 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     if constexpr (HEUR) heur_shared_init(hs, threadIdx.x, BLK);
     if constexpr (HT_LDS || HEUR) __syncthreads();
     const uint32_t slot0 = blockIdx.x * BLK + threadIdx.x;
-    // BK_ROLL_OPAQUE (bit 0: frontier-order kernels, bit 1: naive): the lane's slot and
-    // lane index are laundered once per ply, so the addresses derived from them (slab,
-    // frontier record, LDS columns) are recomputed in the loop instead of being held in
-    // registers for the whole kernel (spilled across the stencil)
-    constexpr bool OPAQUE = (BK_ROLL_OPAQUE >> (FR ? 0 : 1)) & 1;
+    // The lane's slot and lane index are laundered once per ply, so the addresses derived
+    // from them (slab, frontier record, LDS columns) are recomputed in the loop instead of
+    // being held in registers for the whole kernel (spilled across the stencil)
     uint32_t* const my = lds + wv * AREA;
     const bool arena = a.cfg.semantics != BK_SEM_ROLLOUT;  // passes allowed
     const bool advance = a.cfg.semantics == BK_SEM_ADVANCE;
@@ -2926,7 +2865,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& a) {
     for (uint32_t iter = 0;; ++iter) {
         uint32_t slot = slot0;
         int lane = lane0;
-        if constexpr (OPAQUE) asm volatile("" : "+v"(slot), "+v"(lane));
+        asm volatile("" : "+v"(slot), "+v"(lane));
         const Slab slab{a.slab + (size_t)slot * SLAB_WORDS};
         uint2* const rows_lds = reinterpret_cast<uint2*>(my) + lane;  // + R * WAVE
         double* const psum = reinterpret_cast<double*>(my + HEUR_PSUM * WAVE) + lane;  // + piece * WAVE
@@ -4316,18 +4255,10 @@ __global__ void k_mcts_h(MctsArgs a);
 // orientation order.  The searches are the reference's, as in k_mcts / k_mcts_h (tests
 // run both kernels on the same batches).
 // ------------------------------------------------------------------------------------
-#ifndef COOP_WAVES
 #define COOP_WAVES 2                             // searches (waves) per block
-#endif
-#ifndef BK_COOP_ML_LDS
-#define BK_COOP_ML_LDS 1  // k_mcts_coop_h keeps the search's McLane in LDS
-#endif
-#ifndef BK_COOP_SLAB_LDS
-#define BK_COOP_SLAB_LDS 1  // the cooperative kernels keep the search's slab in LDS
-#endif
-#ifndef COOP_H_WAVES_PER_SIMD
-#define COOP_H_WAVES_PER_SIMD 1                  // k_mcts_coop_h waves per SIMD (2: <= 256 registers, spills)
-#endif
+// k_mcts_coop_h keeps the search's McLane in LDS, both cooperative kernels the search's
+// slab.  k_mcts_coop_h runs one wave per SIMD (a 2-wave build, <= 256 registers, spills:
+// 755 vs 832 games/s, profiles/r05/sweeps/r05g).
 #define COOP_AREA ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS)  // per-wave per-lane area (rows / staged table)
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
@@ -4703,7 +4634,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     // so no launch leaves anything in it for the next -- and the mover's table is then
     // used in place (no LDS-DMA stage, no write-back).  (k_mcts_coop keeps it in HBM: the
     // 4.9 KB per wave would cost it a block per CU.)
-    constexpr bool ML_LDS = HEUR && BK_COOP_ML_LDS;
+    constexpr bool ML_LDS = HEUR;
     __shared__ __attribute__((aligned(16))) McLane coop_ml[ML_LDS ? COOP_WAVES : 1];
     const bool coop_walk_on = a.coop_walk != 0;
     // the wave index is uniform (readfirstlane): the wave's LDS area, slab and McLane
@@ -4718,7 +4649,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
     const uint32_t slot = blockIdx.x * COOP_WAVES + wv;  // one slab / McLane per search
     // the search's board (the slab: planes, occupancy) lives in LDS, one per wave: it
     // is rebuilt from the root at every iteration, so nothing outside the wave reads it
-    const Slab slab{BK_COOP_SLAB_LDS ? coop_slab[wv] : a.slab + (size_t)slot * SLAB_WORDS};
+    const Slab slab{coop_slab[wv]};
     McLane* L = ML_LDS ? &coop_ml[ML_LDS ? wv : 0] : a.lanes + slot;
     Mc m{};
     m.game = -1;
@@ -4965,7 +4896,7 @@ __global__ __launch_bounds__(COOP_WAVES * WAVE) void k_mcts_coop(MctsArgs a) { m
 __global__ void k_mcts_coop(MctsArgs a);
 #endif
 #if BK_DEF(BK_U_COOP_H)
-__global__ __launch_bounds__(COOP_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(COOP_H_WAVES_PER_SIMD)))
+__global__ __launch_bounds__(COOP_WAVES * WAVE) __attribute__((amdgpu_waves_per_eu(1)))
 void k_mcts_coop_h(MctsArgs a) { mcts_coop_body<true>(a); }
 #else
 __global__ void k_mcts_coop_h(MctsArgs a);
