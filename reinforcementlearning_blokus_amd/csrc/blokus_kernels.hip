@@ -4411,6 +4411,34 @@ __device__ __forceinline__ void coop_list_moves(uint16_t* ml, uint32_t idx, uint
     }
 }
 
+// lane_ok_rows / locate_pass1 for the wave's ONE orientation gs (every lane's column holds
+// the same {B, C} rows): lane r < 20 computes anchor row r from its own column (5 LDS
+// reads, conflict-free), and the 20 rows are broadcast with v_readlane, so ok[] is
+// wave-uniform -- instead of every lane computing all 20 rows (100 LDS reads and ~240
+// VALU per lane).  All 64 lanes must be active (the cooperative kernels' uniform flow).
+__device__ __forceinline__ void coop_ok_rows(int gs, const uint2* rows, int lane, uint32_t (&ok)[20]) {
+    const uint32_t info = kInfo[gs];
+    const int n = (int)((info >> 8) & 0xFFu);
+    const int rlim = 20 - (int)((info >> 16) & 0xFFu);
+    const int r = lane < 20 ? lane : 0;
+    const int rr = r < rlim ? r : rlim;
+    uint2 v[5];
+    uint32_t sh[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const uint32_t cell = kCells[gs][k < n ? k : 0];
+        sh[k] = cell & 0xFFu;
+        v[k] = rows[(rr + (int)(cell >> 8)) * WAVE];
+    }
+    uint32_t ab = BITOP3(v[0].x >> sh[0], v[1].x >> sh[1], v[2].x >> sh[2], LUT_OR3);
+    uint32_t ac = BITOP3(v[0].y >> sh[0], v[1].y >> sh[1], v[2].y >> sh[2], LUT_OR3);
+    ab = BITOP3(ab, v[3].x >> sh[3], v[4].x >> sh[4], LUT_OR3);
+    ac = BITOP3(ac, v[3].y >> sh[3], v[4].y >> sh[4], LUT_OR3);
+    const uint32_t mine = r <= rlim ? (ac & ~ab) : 0u;
+#pragma unroll
+    for (int q = 0; q < 20; ++q) ok[q] = (uint32_t)__builtin_amdgcn_readlane((int)mine, q);
+}
+
 // Balanced HeuristicAgent pass A for the wave's search (k_mcts_coop_h): instead of each
 // lane summing e over its own two orientations' moves (the wave then iterates the
 // largest orientation's move count, ~1 legal move per lane-iteration), the ply's legal
@@ -4446,6 +4474,9 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double carry = 0.0;
+    // the B rows through this lane's own column: lanes read different rows, and column 0's
+    // rows all sit in one LDS bank (a 20-way conflict per read)
+    const uint2* const own = rows + lane;
 #pragma unroll 1
     for (uint32_t k0 = 0; k0 < n_moves; k0 += WAVE) {
         const uint32_t k = k0 + (uint32_t)lane;
@@ -4459,7 +4490,7 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
             int n;
             uint32_t cd[5], cc[5];
             orient_cells(g, n, cd, cc);
-            e = heur_e(n, cd, cc, cell / 20, cell % 20, rows, hs, edge_w);
+            e = heur_e(n, cd, cc, cell / 20, cell % 20, own, hs, edge_w);
         }
         const double incl = wave_incl_scan_f64(e, lane) + carry;
         const double up = __shfl_up(incl, 1);
@@ -4499,10 +4530,10 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
     if (L < 0) { R = 0.0; gs = -1; return true; }
     gs = L + WAVE * h;
     R = cumS[gs];
-    // the chosen orientation's legal rows, recomputed by every lane from the {B, C} rows
-    // (column 0: every lane's column holds the same rows): ok0 / ok1 then die once the
-    // moves are listed instead of staying live through the e pass (registers)
-    lane_ok_rows(gs, rows, gok);
+    // the chosen orientation's legal rows, recomputed from the {B, C} rows (coop_ok_rows,
+    // every lane's column holds the same rows): ok0 / ok1 then die once the moves are
+    // listed instead of staying live through the e pass (registers)
+    coop_ok_rows(gs, own, lane, gok);
     return true;
 }
 
@@ -4787,7 +4818,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
                 es[0] = cnt[0] ? lane_orient_sum(lane, okA, rows_lds, hs, edge_w) : 0.0;
                 es[1] = cnt[1] ? lane_orient_sum(lane + WAVE, okB, rows_lds, hs, edge_w) : 0.0;
                 gs = coop_heur_pick(es, lane, st, m.mt_pos, h_pre0, h_pre1, h_target, h_R, h_total, h_unc);
-                if (gs >= 0) lane_ok_rows(gs, rows_lds, h_ok);
+                if (gs >= 0) coop_ok_rows(gs, rows_lds, lane, h_ok);
             }
         } else {
             gs = coop_find(sc, k, kk);
@@ -4818,7 +4849,10 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             bool walked = false;
             if (coop_walk_on && tmask <= 2 * WAVE - 1) {
                 bool unc_unused = false;
-                locate_pass1(gs, rows_lds);
+                uint32_t okr[20];
+                coop_ok_rows(gs, rows_lds, lane, okr);  // locate_pass1 for the wave's one orientation
+#pragma unroll
+                for (int r = 0; r < 20; ++r) rows_lds[r * WAVE].y = okr[r];
                 walked = coop_walk<false>(gs, kk, rows_lds, tkey, (int)tmask, rank, lane, hs, 0, 0.0, 0.0,
                                           0.0, ar, ac, unc_unused);
             }
