@@ -4273,16 +4273,45 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
 // legal-move counts (and with E the e sums, HeuristicAgent pass A) of this lane's
 // orientations g = lane + 64 h; 0 for g >= 91 or a used piece.  rows = {B, C} in the
 // lane's column.
-template <bool E>
-__device__ __forceinline__ void coop_orients(const uint2* rows, uint32_t avail, int lane, const HeurShared* hs,
-                                             int edge_w, uint32_t (&cnt)[2], double (&es)[2]) {
+// The wave's live orientations (pieces the mover still holds), compacted onto its lanes:
+// lane k takes the k-th live orientation in g order for pass 0 and the (64 + k)-th for
+// pass 1 (og[h], -1 none), so a ply with <= 64 live orientations -- most rollout plies once
+// a few pieces are down -- runs ONE pass of the per-lane orientation work instead of two.
+// The order is g ascending, so scans over (pass 0 lanes, pass 1 lanes) run in the
+// reference's list order.  otab: 91 int16 of wave-private LDS (the walk's rank array,
+// which coop_walk re-initialises before use).  Returns the live count.
+__device__ __forceinline__ uint32_t coop_live_orients(uint32_t avail, int lane, int16_t* otab, int (&og)[2]) {
+    bool live[2];
+    uint64_t msk[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int g = lane + WAVE * h;
+        live[h] = g < BK_NUM_ORIENTS && ((avail >> ((kInfo[g < BK_NUM_ORIENTS ? g : 0] & 0xFFu) - 1u)) & 1u);
+        msk[h] = __ballot(live[h]);
+    }
+    const uint32_t n0 = (uint32_t)__popcll(msk[0]), n = n0 + (uint32_t)__popcll(msk[1]);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    if (live[0]) otab[__popcll(msk[0] & lt)] = (int16_t)lane;
+    if (live[1]) otab[n0 + (uint32_t)__popcll(msk[1] & lt)] = (int16_t)(lane + WAVE);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    og[0] = (uint32_t)lane < n ? (int)otab[lane] : -1;
+    og[1] = (uint32_t)(lane + WAVE) < n ? (int)otab[lane + WAVE] : -1;
+    return n;
+}
+
+template <bool E>
+__device__ __forceinline__ void coop_orients(const uint2* rows, const int (&og)[2], uint32_t nlive,
+                                             const HeurShared* hs, int edge_w, uint32_t (&cnt)[2],
+                                             double (&es)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
         cnt[h] = 0u;
         es[h] = 0.0;
-        const bool live = g < BK_NUM_ORIENTS && ((avail >> ((kInfo[g < BK_NUM_ORIENTS ? g : 0] & 0xFFu) - 1u)) & 1u);
-        if (live) {
+        if (h == 1 && nlive <= (uint32_t)WAVE) continue;  // (uniform) one pass holds them all
+        const int g = og[h];
+        if (g >= 0) {
             uint32_t ok[20];
             lane_ok_rows(g, rows, ok);
 #pragma unroll
@@ -4319,18 +4348,18 @@ __device__ __forceinline__ CoopScan coop_scan(const uint32_t (&cnt)[2], int lane
 
 // pick_orient for the wave's search: the orientation holding the k-th legal move (g
 // ascending) and the move's rank kk in it
-__device__ __forceinline__ int coop_find(const CoopScan& s, uint32_t k, uint32_t& kk) {
+__device__ __forceinline__ int coop_find(const CoopScan& s, const int (&og)[2], uint32_t k, uint32_t& kk) {
     const uint64_t b0 = __ballot(k < s.i0 && k >= s.i0 - s.c0);
     const uint64_t b1 = __ballot(k < s.i1 && k >= s.i1 - s.c1);
     int g = BK_NUM_ORIENTS - 1;
     uint32_t before = k;
     if (b0) {
         const int L = __ffsll((unsigned long long)b0) - 1;
-        g = L;
+        g = __shfl(og[0], L);
         before = __shfl(s.i0 - s.c0, L);
     } else if (b1) {
         const int L = __ffsll((unsigned long long)b1) - 1;
-        g = L + WAVE;
+        g = __shfl(og[1], L);
         before = __shfl(s.i1 - s.c1, L);
     }
     kk = k - before;
@@ -4342,7 +4371,8 @@ __device__ __forceinline__ int coop_find(const CoopScan& s, uint32_t k, uint32_t
 // target, by a wave scan; R = cumulative e before it, total = the sum of all.  The sums
 // differ from the per-piece serial ones by rounding only (the walk certifies the draw
 // against HEUR_MARGIN).  Uncertain when no crossing is found (rounding at the total).
-__device__ __forceinline__ int coop_heur_pick(const double (&es)[2], int lane, const uint32_t* st, uint32_t& pos,
+__device__ __forceinline__ int coop_heur_pick(const double (&es)[2], const int (&og)[2], int lane, const uint32_t* st,
+                                              uint32_t& pos,
                                               uint32_t pre0, uint32_t pre1, double& target, double& R,
                                               double& total, bool& uncertain) {
     const double i0 = wave_incl_scan_f64(es[0], lane);
@@ -4372,15 +4402,14 @@ __device__ __forceinline__ int coop_heur_pick(const double (&es)[2], int lane, c
     }
     if (L < 0) { R = 0.0; return -1; }
     R = __shfl(h ? i1 - es[1] : i0 - es[0], L);
-    return L + WAVE * h;
+    return __shfl(h ? og[1] : og[0], L);
 }
 
 // legal anchor rows and counts of this lane's orientations g = lane + 64 h (rows = {B, C}
 // in the lane's column); 0 rows for g >= 91 or a used piece.  The rows stay in registers
 // for the balanced heuristic pass.
-__device__ __forceinline__ uint32_t coop_ok_count1(const uint2* rows, uint32_t avail, int g, uint32_t (&ok)[20]) {
-    const bool live = g < BK_NUM_ORIENTS && ((avail >> ((kInfo[g < BK_NUM_ORIENTS ? g : 0] & 0xFFu) - 1u)) & 1u);
-    if (live) {
+__device__ __forceinline__ uint32_t coop_ok_count1(const uint2* rows, int g, uint32_t (&ok)[20]) {
+    if (g >= 0) {
         lane_ok_rows(g, rows, ok);
     } else {
 #pragma unroll
@@ -4392,10 +4421,16 @@ __device__ __forceinline__ uint32_t coop_ok_count1(const uint2* rows, uint32_t a
     return c;
 }
 
-__device__ __forceinline__ void coop_ok_counts(const uint2* rows, uint32_t avail, int lane, uint32_t (&ok0)[20],
-                                               uint32_t (&ok1)[20], uint32_t (&cnt)[2]) {
-    cnt[0] = coop_ok_count1(rows, avail, lane, ok0);
-    cnt[1] = coop_ok_count1(rows, avail, lane + WAVE, ok1);
+__device__ __forceinline__ void coop_ok_counts(const uint2* rows, const int (&og)[2], uint32_t nlive,
+                                               uint32_t (&ok0)[20], uint32_t (&ok1)[20], uint32_t (&cnt)[2]) {
+    cnt[0] = coop_ok_count1(rows, og[0], ok0);
+    if (nlive > (uint32_t)WAVE) {  // (uniform) a second pass only for > 64 live orientations
+        cnt[1] = coop_ok_count1(rows, og[1], ok1);
+    } else {
+        cnt[1] = 0u;
+#pragma unroll
+        for (int r = 0; r < 20; ++r) ok1[r] = 0u;
+    }
 }
 
 // orientation g's legal moves (rows ok) into the move list from index idx: naive order
@@ -4456,7 +4491,8 @@ __device__ __forceinline__ void coop_ok_rows(int gs, const uint2* rows, int lane
 #define COOP_CUM_DWORD (COOP_ML_DWORD + COOP_MOVE_CAP / 2)  // cumE[91], cumS[91] (doubles)
 template <typename Mark = NoMark>
 __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* area, int lane, const HeurShared* hs,
-                                                   int edge_w, const uint32_t (&ok0)[20], const uint32_t (&ok1)[20],
+                                                   int edge_w, const int (&og)[2], const uint32_t (&ok0)[20],
+                                                   const uint32_t (&ok1)[20],
                                                    const uint32_t (&cnt)[2], const CoopScan& sc, const uint32_t* st,
                                                    uint32_t& pos, uint32_t pre0, uint32_t pre1, double& target,
                                                    double& R, double& total, bool& uncertain, int& gs,
@@ -4467,8 +4503,8 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
     double* cumE = reinterpret_cast<double*>(area + COOP_CUM_DWORD);
     double* cumS = cumE + BK_NUM_ORIENTS;
     mark(3);
-    coop_list_moves(ml, sc.i0 - sc.c0, (uint32_t)lane, ok0);
-    coop_list_moves(ml, sc.i1 - sc.c1, (uint32_t)(lane + WAVE), ok1);
+    coop_list_moves(ml, sc.i0 - sc.c0, (uint32_t)(og[0] < 0 ? 0 : og[0]), ok0);  // (no moves when og < 0)
+    coop_list_moves(ml, sc.i1 - sc.c1, (uint32_t)(og[1] < 0 ? 0 : og[1]), ok1);
     mark(6);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -4514,8 +4550,8 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
         u = mc_random_sample(const_cast<uint32_t*>(st), pos);
     }
     target = u * total;
-    const double e0 = cnt[0] ? cumE[lane] : 0.0;
-    const double e1 = cnt[1] ? cumE[lane + WAVE] : 0.0;
+    const double e0 = cnt[0] ? cumE[og[0]] : 0.0;
+    const double e1 = cnt[1] ? cumE[og[1]] : 0.0;
     const uint64_t b0 = __ballot(cnt[0] != 0u && e0 > target);
     const uint64_t b1 = __ballot(cnt[1] != 0u && e1 > target);
     int L = -1, h = 0;
@@ -4528,7 +4564,7 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
         else if (l0) { L = 63 - __clzll((unsigned long long)l0); }
     }
     if (L < 0) { R = 0.0; gs = -1; return true; }
-    gs = L + WAVE * h;
+    gs = __shfl(h ? og[1] : og[0], L);
     R = cumS[gs];
     // the chosen orientation's legal rows, recomputed from the {B, C} rows (coop_ok_rows,
     // every lane's column holds the same rows): ok0 / ok1 then die once the moves are
@@ -4766,8 +4802,10 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         uint32_t cnt[2];
         double es[2];
         uint32_t okA[20], okB[20];  // hroll: this lane's orientations' legal rows (balanced pass)
-        if (hroll) coop_ok_counts(rows_lds, avail, lane, okA, okB, cnt);
-        else coop_orients<false>(rows_lds, avail, lane, hs, edge_w, cnt, es);
+        int og[2];
+        const uint32_t nlive = coop_live_orients(avail, lane, coop_rank[wv], og);
+        if (hroll) coop_ok_counts(rows_lds, og, nlive, okA, okB, cnt);
+        else coop_orients<false>(rows_lds, og, nlive, hs, edge_w, cnt, es);
         const CoopScan sc = coop_scan(cnt, lane);
         const uint32_t total = sc.total;
         SECT(2);
@@ -4812,16 +4850,16 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
             NoMark cmark;
 #endif
             if (!a.coop_balanced ||
-                !coop_heur_balanced(rows_lds - lane, my, lane, hs, edge_w, okA, okB, cnt, sc, st, m.mt_pos, h_pre0,
-                                    h_pre1, h_target, h_R, h_total, h_unc, gs, h_ok, cmark)) {
+                !coop_heur_balanced(rows_lds - lane, my, lane, hs, edge_w, og, okA, okB, cnt, sc, st, m.mt_pos,
+                                    h_pre0, h_pre1, h_target, h_R, h_total, h_unc, gs, h_ok, cmark)) {
                 // more legal moves than the list holds: per-lane orientation sums
-                es[0] = cnt[0] ? lane_orient_sum(lane, okA, rows_lds, hs, edge_w) : 0.0;
-                es[1] = cnt[1] ? lane_orient_sum(lane + WAVE, okB, rows_lds, hs, edge_w) : 0.0;
-                gs = coop_heur_pick(es, lane, st, m.mt_pos, h_pre0, h_pre1, h_target, h_R, h_total, h_unc);
+                es[0] = cnt[0] ? lane_orient_sum(og[0], okA, rows_lds, hs, edge_w) : 0.0;
+                es[1] = cnt[1] ? lane_orient_sum(og[1], okB, rows_lds, hs, edge_w) : 0.0;
+                gs = coop_heur_pick(es, og, lane, st, m.mt_pos, h_pre0, h_pre1, h_target, h_R, h_total, h_unc);
                 if (gs >= 0) coop_ok_rows(gs, rows_lds, lane, h_ok);
             }
         } else {
-            gs = coop_find(sc, k, kk);
+            gs = coop_find(sc, og, k, kk);
         }
         FsLane* T = &L->A;  // the node board at expansion, the rollout's sim board after it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
