@@ -1778,6 +1778,9 @@ __device__ __forceinline__ bool fs_run_ops(FsetRef t, int16_t* tmp, const int32_
             real &= real - 1ull;
             const int op = s - 9 * ((s * 57) >> 9);
             const int key = key_of(s);
+            // (a wave-parallel version -- op hashes loaded up front, one lane per slot of
+            // the first linear probe run, ballot for the stop -- measured 3 % slower:
+            // most chains stop at their first slot; profiles/r06/sweeps/r06w)
             if (!fs_op_h(t, tmp, (int16_t)key, (unsigned)(op - 1) < 4u, t.hash[key], ltmp)) return false;
         }
         return true;
@@ -4906,6 +4909,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
         int32_t cells[5];
         piece_cells(gs, ar, ac, pm, cells);
         const uint64_t real = frontier_ops(rows_lds, slab, p, (m.first >> p) & 1u, gs, ar, ac, pm);
+        SECT(8);
         const bool expand = m.mode == MC_EXPAND;
         uint32_t c = 0;
         bool ok = true;
@@ -4933,8 +4937,15 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
                 inpl = staged;
             }
         }
-        if (expand) ok &= mc_place_staged<true, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, NoMark(), inpl);
-        else ok &= mc_place_staged<false, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, NoMark(), inpl);
+#ifdef BK_SECTION_PROF
+        // 9 slab rows, 10 set ops, 11 write-back / copy
+        auto pmark = [&](int i) { SECT(i == 4 ? 9 : 10); };
+#else
+        NoMark pmark;
+#endif
+        if (expand) ok &= mc_place_staged<true, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, pmark, inpl);
+        else ok &= mc_place_staged<false, 2>(m, slab, p, gs, ar, &L->A, htab, pm, cells, real, lk, sq, pmark, inpl);
+        SECT(11);
         if (expand) {
             if (!ok) { m.status |= BK_MCTS_EFSET; m.mode = MC_SELECT; continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;

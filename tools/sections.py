@@ -142,8 +142,9 @@ def run_coop():
     L = N.load()
     buf = (C.c_uint64 * 16)()
     names = {0: "tree", 1: "derive+rows", 2: "lane orientations+scan", 3: "draw+pick (rest)",
-             4: "locate / heuristic walk", 5: "frontier ops+place+expand", 6: "heuristic: list moves",
-             7: "heuristic: e pass + scan"}
+             4: "locate / heuristic walk", 5: "expansion / rollout tail", 6: "heuristic: list moves",
+             7: "heuristic: e pass + scan", 8: "piece cells + frontier ops windows", 9: "place: slab rows",
+             10: "place: set ops", 11: "place: write-back / copy"}
     for policy in (N.MCTS_ROLLOUT_HEURISTIC, N.MCTS_ROLLOUT_RANDOM):
         roots, sets = frontier_roots(gpu, 512, 24, seed=11)
         b = MctsBatch(gpu, roots, sets, iterations=64, seed0=3)
