@@ -4264,13 +4264,47 @@ __global__ void k_mcts_h(MctsArgs a);
 // 755 vs 832 games/s, profiles/r05/sweeps/r05g).
 #define COOP_AREA ROLL_WORDS_STAGE(BK_FS_STAGE_MCTS)  // per-wave per-lane area (rows / staged table)
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const uint32_t u = __shfl_up(v, o);
-        v += lane >= o ? u : 0u;
-    }
+// Wave-wide scans and broadcasts of the cooperative kernels (all 64 lanes active).  The
+// inclusive prefix sum runs on DPP: row_shr 1 / 2 / 4 / 8 inside each 16-lane row, then
+// row_bcast 15 and row_bcast 31 add the earlier rows' totals -- six ALU-latency steps,
+// where a __shfl_up ladder is six dependent ds_bpermute round trips through the LDS
+// crossbar (two per step for a double).  Lanes whose DPP source is outside the row, or
+// whose row is masked off, read the identity (old = 0).  A broadcast from a uniform lane
+// (found by a ballot) is a v_readlane into a scalar register, not a ds_bpermute.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = dpp_u32<CTRL, ROWS>((uint32_t)b), hi = dpp_u32<CTRL, ROWS>((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint64_t)lo));
+}
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+#define DPP_WAVE_SHR1 0x138
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int) {
+    v += dpp_u32<DPP_ROW_SHR(1), 0xF>(v);
+    v += dpp_u32<DPP_ROW_SHR(2), 0xF>(v);
+    v += dpp_u32<DPP_ROW_SHR(4), 0xF>(v);
+    v += dpp_u32<DPP_ROW_SHR(8), 0xF>(v);
+    v += dpp_u32<DPP_ROW_BCAST15, 0xA>(v);
+    v += dpp_u32<DPP_ROW_BCAST31, 0xC>(v);
     return v;
+}
+
+__device__ __forceinline__ uint32_t lane_bcast(uint32_t v, int l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ int lane_bcast(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ double lane_bcast(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint64_t)lo));
 }
 
 // legal-move counts (and with E the e sums, HeuristicAgent pass A) of this lane's
@@ -4324,12 +4358,13 @@ __device__ __forceinline__ void coop_orients(const uint2* rows, const int (&og)[
     }
 }
 
-__device__ __forceinline__ double wave_incl_scan_f64(double v, int lane) {
-#pragma unroll
-    for (int o = 1; o < WAVE; o <<= 1) {
-        const double u = __shfl_up(v, o);
-        v += lane >= o ? u : 0.0;
-    }
+__device__ __forceinline__ double wave_incl_scan_f64(double v, int) {
+    v += dpp_f64<DPP_ROW_SHR(1), 0xF>(v);
+    v += dpp_f64<DPP_ROW_SHR(2), 0xF>(v);
+    v += dpp_f64<DPP_ROW_SHR(4), 0xF>(v);
+    v += dpp_f64<DPP_ROW_SHR(8), 0xF>(v);
+    v += dpp_f64<DPP_ROW_BCAST15, 0xA>(v);
+    v += dpp_f64<DPP_ROW_BCAST31, 0xC>(v);
     return v;
 }
 
@@ -4343,9 +4378,9 @@ __device__ __forceinline__ CoopScan coop_scan(const uint32_t (&cnt)[2], int lane
     s.c0 = cnt[0];
     s.c1 = cnt[1];
     s.i0 = wave_incl_scan(cnt[0], lane);
-    const uint32_t t0 = __shfl(s.i0, WAVE - 1);
+    const uint32_t t0 = lane_bcast(s.i0, WAVE - 1);
     s.i1 = wave_incl_scan(cnt[1], lane) + t0;
-    s.total = __shfl(s.i1, WAVE - 1);
+    s.total = lane_bcast(s.i1, WAVE - 1);
     return s;
 }
 
@@ -4358,12 +4393,12 @@ __device__ __forceinline__ int coop_find(const CoopScan& s, const int (&og)[2], 
     uint32_t before = k;
     if (b0) {
         const int L = __ffsll((unsigned long long)b0) - 1;
-        g = __shfl(og[0], L);
-        before = __shfl(s.i0 - s.c0, L);
+        g = lane_bcast(og[0], L);
+        before = lane_bcast(s.i0 - s.c0, L);
     } else if (b1) {
         const int L = __ffsll((unsigned long long)b1) - 1;
-        g = __shfl(og[1], L);
-        before = __shfl(s.i1 - s.c1, L);
+        g = lane_bcast(og[1], L);
+        before = lane_bcast(s.i1 - s.c1, L);
     }
     kk = k - before;
     return g;
@@ -4379,8 +4414,8 @@ __device__ __forceinline__ int coop_heur_pick(const double (&es)[2], const int (
                                               uint32_t pre0, uint32_t pre1, double& target, double& R,
                                               double& total, bool& uncertain) {
     const double i0 = wave_incl_scan_f64(es[0], lane);
-    const double i1 = wave_incl_scan_f64(es[1], lane) + __shfl(i0, WAVE - 1);
-    total = __shfl(i1, WAVE - 1);
+    const double i1 = wave_incl_scan_f64(es[1], lane) + lane_bcast(i0, WAVE - 1);
+    total = lane_bcast(i1, WAVE - 1);
     // HeuristicAgent's draw (random_sample): the two words were loaded ahead (pre) when
     // the state holds them without a twist
     double u;
@@ -4404,8 +4439,8 @@ __device__ __forceinline__ int coop_heur_pick(const double (&es)[2], const int (
         else if (l0) { L = 63 - __clzll((unsigned long long)l0); }
     }
     if (L < 0) { R = 0.0; return -1; }
-    R = __shfl(h ? i1 - es[1] : i0 - es[0], L);
-    return __shfl(h ? og[1] : og[0], L);
+    R = lane_bcast(h ? i1 - es[1] : i0 - es[0], L);
+    return lane_bcast(h ? og[1] : og[0], L);
 }
 
 // legal anchor rows and counts of this lane's orientations g = lane + 64 h (rows = {B, C}
@@ -4532,11 +4567,11 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
             e = heur_e(n, cd, cc, cell / 20, cell % 20, own, hs, edge_w);
         }
         const double incl = wave_incl_scan_f64(e, lane) + carry;
-        const double up = __shfl_up(incl, 1);
+        const double up = dpp_f64<DPP_WAVE_SHR1, 0xF>(incl);
         const double excl = lane ? up : carry;
         if (in && gn != g) cumE[g] = incl;
         if (in && gp != g) cumS[g] = excl;
-        carry = __shfl(incl, WAVE - 1);
+        carry = lane_bcast(incl, WAVE - 1);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -4567,7 +4602,7 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
         else if (l0) { L = 63 - __clzll((unsigned long long)l0); }
     }
     if (L < 0) { R = 0.0; gs = -1; return true; }
-    gs = __shfl(h ? og[1] : og[0], L);
+    gs = lane_bcast(h ? og[1] : og[0], L);
     R = cumS[gs];
     // the chosen orientation's legal rows, recomputed from the {B, C} rows (coop_ok_rows,
     // every lane's column holds the same rows): ok0 / ok1 then die once the moves are
@@ -4639,11 +4674,11 @@ __device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows
         const CoopScan sc = coop_scan(cnt, lane);
         const uint64_t b0 = __ballot(kk < sc.i0 && kk >= sc.i0 - sc.c0);
         const uint64_t b1 = __ballot(kk < sc.i1 && kk >= sc.i1 - sc.c1);
-        if (b0) { hit = __ffsll((unsigned long long)b0) - 1; before = __shfl(sc.i0 - sc.c0, hit); }
-        else if (b1) { hit = __ffsll((unsigned long long)b1) - 1; hh = 1; before = __shfl(sc.i1 - sc.c1, hit); }
+        if (b0) { hit = __ffsll((unsigned long long)b0) - 1; before = lane_bcast(sc.i0 - sc.c0, hit); }
+        else if (b1) { hit = __ffsll((unsigned long long)b1) - 1; hh = 1; before = lane_bcast(sc.i1 - sc.c1, hit); }
     } else {
         const double i0 = wave_incl_scan_f64(es[0], lane);
-        const double i1 = wave_incl_scan_f64(es[1], lane) + __shfl(i0, WAVE - 1);
+        const double i1 = wave_incl_scan_f64(es[1], lane) + lane_bcast(i0, WAVE - 1);
         const uint64_t b0 = __ballot(es[0] > 0.0 && R + i0 > target);
         const uint64_t b1 = __ballot(es[1] > 0.0 && R + i1 > target);
         if (b0) { hit = __ffsll((unsigned long long)b0) - 1; }
@@ -4655,12 +4690,12 @@ __device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows
             if (l1) { hit = 63 - __clzll((unsigned long long)l1); hh = 1; }
             else if (l0) { hit = 63 - __clzll((unsigned long long)l0); }
         }
-        if (hit >= 0) lo = R + __shfl(hh ? i1 - es[1] : i0 - es[0], hit);
+        if (hit >= 0) lo = R + lane_bcast(hh ? i1 - es[1] : i0 - es[0], hit);
     }
     if (hit < 0) { out_r = -1; out_c = 0; return true; }
     // every lane resolves the chosen slot (identical work and result)
-    const int fh = __shfl(hh ? f[1] : f[0], hit);
-    const uint32_t nk = __shfl(hh ? newk[1] : newk[0], hit);
+    const int fh = lane_bcast(hh ? f[1] : f[0], hit);
+    const uint32_t nk = lane_bcast(hh ? newk[1] : newk[0], hit);
     const int fr = fh / 20, fc = fh - 20 * (fh / 20);
     int found_r = -1, found_c = 0, last_r = -1, last_c = 0;
     uint32_t rem = kk - before;
