@@ -106,6 +106,12 @@ def parse(argv=None):
     ap.add_argument("--search-streams", type=int, default=None,
                     help="config4: MCTS searches in flight on this many streams while the other games play on "
                          "(ArenaOptions.search_streams, 1..16; default: the driver's 8)")
+    ap.add_argument("--handback", action="store_true",
+                    help="config4: hand each search's move back as it finishes (ArenaOptions.handback), not when "
+                         "its launch ends")
+    ap.add_argument("--job-games", type=int, default=None,
+                    help="config4: at most this many searches per bk_mcts launch (ArenaOptions.job_games; "
+                         "default: one launch per round)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="config4: HIP hardware queues of this rank (GPU_MAX_HW_QUEUES, <= 32; default 16), so the "
                          "search streams, the FastMCTS handle and the main stream do not share in-order queues "
@@ -861,6 +867,10 @@ def run_config4(args, world, rank, local, dist):
 
     from reinforcementlearning_blokus_amd.mcts.mcts_agent import SEARCH_TOTALS, reset_search_totals
     opts = {} if args.search_streams is None else {"search_streams": args.search_streams}
+    if args.job_games is not None:
+        opts["job_games"] = args.job_games
+    if args.handback:
+        opts["handback"] = True
     for _ in range(args.warmup):
         run_games_batched(cfg, mine[:64], device=local, **opts)
     barrier_sync(dist)
@@ -919,7 +929,8 @@ def run_config4(args, world, rank, local, dist):
                    "games": total, "mcts_sims_per_s": all_sims / elapsed, "moves_per_s": all_moves / elapsed,
                    "uncertified_heuristic_rank0": phases.get("uncertified_heuristic"),
                    "rank0_phase_seconds": phases, "host_cores_per_rank": host,
-                   "search_streams": args.search_streams or 8, "pipelined": True,
+                   "search_streams": args.search_streams or 8, "job_games": args.job_games, "pipelined": True,
+                   "handback": args.handback,
                    "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "HIP default"),
                    "parallelism": f"dp{world} (games sharded r mod {world})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

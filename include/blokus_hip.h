@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define BK_ABI_VERSION 6
+#define BK_ABI_VERSION 7
 #define BK_BOARD 20
 #define BK_CELLS 400
 #define BK_PLAYERS 4
@@ -460,6 +460,14 @@ typedef struct bk_mcts_cfg {
                                   asynchronous search per handle at a time            */
 } bk_mcts_cfg;
 #define BK_MCTS_ASYNC 1
+/* BK_MCTS_STATE_ROWS (ABI 7, BK_MEM_DEVICE only): mt_state, tt_keys, tt_vals and tt_count
+   hold one row per agent (n_zobrist rows), search g using row zobrist_index[g]: the MT
+   state is copied in at the search's start and back at its end, the TT probed and filled
+   in place, all with system-scope (L2-bypassing) accesses -- so a launch needs no gather /
+   scatter of agent state, and a later launch may search with an agent as soon as its
+   earlier search is done (bk_mcts_set_done) even while that launch still runs.  No two
+   searches of one launch may share a row. */
+#define BK_MCTS_STATE_ROWS 2
 #define BK_MCTS_ROLLOUT_RANDOM 0    /* RandomAgent (agents/random_agent.py:49)            */
 #define BK_MCTS_ROLLOUT_HEURISTIC 1 /* HeuristicAgent (agents/heuristic_agent.py:39-244),
                                        MCTSAgent's default (mcts/mcts_agent.py:275-281);
@@ -529,6 +537,23 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
 #define BK_DIAG_K_COOP 3      /* k_mcts_coop */
 #define BK_DIAG_K_COOP_H 4    /* k_mcts_coop_h */
 int bk_debug_mcts_failure(bk_handle h, uint32_t* out, int32_t n);
+
+/*
+ * Per-search completion (ABI 7; no reference counterpart -- arena_runner.py:578-777 runs
+ * one game at a time).  bk_mcts_set_done(h, done): every later bk_mcts launch on h stores,
+ * once search g's agent rows are written back, done[g] = best_move (bits 0..31) |
+ * iterations_run (32..55) | status (56..62) | 1 << 63 -- one 64-bit store; NULL turns it
+ * off.  With done in memory from bk_host_alloc (mapped, coherent host memory), a host
+ * polls done[] while the launch runs and takes each search's move as soon as it is final:
+ * a launch lasts as long as its longest search (config 4: 2.3x the mean), its games need
+ * not.  The caller zeroes done[0..n_games) before each launch; `out` is complete when the
+ * launch ends.
+ * bk_host_alloc: `bytes` of pinned, device-mapped, coherent host memory (the device
+ * uses the same address), or NULL; bk_host_free releases it.
+ */
+int bk_mcts_set_done(bk_handle h, uint64_t* done);
+void* bk_host_alloc(size_t bytes);
+int bk_host_free(void* p);
 
 /* Average duration (ms) of the most recent bk_rollout/bk_movegen kernel on the handle
    stream, measured with HIP events around that launch. */

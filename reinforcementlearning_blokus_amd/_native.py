@@ -35,7 +35,7 @@ EXPORTS = (
     "bk_fset_init", "bk_fset_place", "bk_fset_copy", "bk_fset_list", "bk_rollout_frontier",
     "bk_mcts", "bk_debug_sections", "bk_pow_half_fix", "bk_debug_fastmcts_select", "bk_arena_advance",
     "bk_arena_step", "bk_mt_cursor_init", "bk_set_tuning", "bk_get_tuning", "bk_debug_fset_op",
-    "bk_debug_mcts_failure",
+    "bk_debug_mcts_failure", "bk_mcts_set_done", "bk_host_alloc", "bk_host_free",
 )
 # bk_debug_mcts_failure record (include/blokus_hip.h BK_DIAG_*)
 DIAG_WORDS = 64
@@ -97,6 +97,7 @@ class BkMctsCfg(C.Structure):
                 ("time_limit_us", C.c_int32), ("iter_stop", C.c_int32), ("resume", C.c_int32),
                 ("rollout_policy", C.c_int32), ("flags", C.c_int32)]
 MCTS_ASYNC = 1  # bk_mcts_cfg.flags: enqueue only (device buffers)
+MCTS_STATE_ROWS = 2  # bk_mcts_cfg.flags: mt / tt rows indexed by zobrist_index (agent rows, in place)
 
 
 assert C.sizeof(BkMctsCfg) == 48
@@ -123,7 +124,7 @@ RESULT_DTYPE = np.dtype([("scores", "<i2", (4,)), ("winner_mask", "u1"), ("statu
                          ("draws", "<u4"), ("reserved", "<u4", (2,))])
 assert STATE_DTYPE.itemsize == 256 and RESULT_DTYPE.itemsize == 32
 
-ABI_VERSION = 6  # include/blokus_hip.h BK_ABI_VERSION
+ABI_VERSION = 7  # include/blokus_hip.h BK_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -193,12 +194,42 @@ def load():
             "bk_debug_fset_op": (C.c_int, [vp, C.c_int32, C.c_int32, C.c_int32]),
             "bk_debug_mcts_failure": (C.c_int, [vp, vp, C.c_int32]),
             "bk_get_tuning": (C.c_int, [vp, C.c_int32, P(C.c_int64)]),
+            "bk_mcts_set_done": (C.c_int, [vp, vp]),
+            "bk_host_alloc": (C.c_void_p, [C.c_size_t]),
+            "bk_host_free": (C.c_int, [vp]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         _lib = L
         return L
+
+
+class HostBuffer:
+    """Pinned, device-mapped, coherent host memory (bk_host_alloc): the device writes it
+    at the same address while the host reads it through `array` (a numpy view)."""
+
+    def __init__(self, nbytes: int, dtype=np.uint8):
+        L = load()
+        self._L = L
+        self.nbytes = int(nbytes)
+        self.ptr = L.bk_host_alloc(self.nbytes)
+        if not self.ptr:
+            raise MemoryError(f"bk_host_alloc({self.nbytes}) failed")
+        raw = (C.c_uint8 * self.nbytes).from_address(self.ptr)
+        self.array = np.frombuffer(raw, dtype=np.uint8).view(dtype)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self._L.bk_host_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter shutdown
+            pass
 
 
 def orient_table():
@@ -355,6 +386,12 @@ class Handle:
 
     def synchronize(self):
         self.check(self._L.bk_synchronize(self._h), "bk_synchronize")
+
+    def set_done(self, ptr: int | None):
+        """bk_mcts_set_done: later bk_mcts launches on this handle store search g's result
+        word in done[g] as it finishes (ptr: a uint64 array the device can write, e.g. a
+        HostBuffer); None turns it off."""
+        self.check(self._L.bk_mcts_set_done(self._h, C.c_void_p(ptr or 0)), "bk_mcts_set_done")
 
     def mcts_failure(self):
         """The handle's bk_mcts failure record (bk_debug_mcts_failure) as a dict, or None if

@@ -712,9 +712,83 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
     capture_dir = opts.capture_dir or ""
     fast_eng = BlokusGPU(device) if pipeline else gpu
     inflight = np.zeros(n, bool)
+    # per-search hand-back: each slot's launches write their out records and done flags
+    # into mapped host memory the loop polls (bk_mcts_set_done); the agents' MT / TT rows
+    # are updated in place, so a handed-back game may search again while its launch's
+    # other searches still run.  (A TT past 500,000 entries is reset between searches,
+    # mcts_agent.py:338-339: only possible at > 11,000 iterations -- those runs keep the
+    # launch-end path.)
+    early = bool(pipeline and opts.handback and not capture_dir and am and cap <= 500000)
+    hb_done: Dict[int, Any] = {}
+
+    def mcts_launch_early(slot, games, aid, iters, roll, c, use_tt, policy):
+        eng, js = engines[slot], jstreams[slot]
+        k = len(games)
+        if slot not in hb_done:
+            hb_done[slot] = N.HostBuffer(8 * n, np.uint64)
+        done_a = hb_done[slot].array
+        done_a[:k] = 0  # (the slot's previous launch has ended)
+        eng.handle.set_done(hb_done[slot].ptr)
+        if int(aid.max()) >= am or int(aid.min()) < 0:
+            raise RuntimeError(f"MCTS agent rows out of range: {aid.min()}..{aid.max()} of {am}")
+        ga_d = up(np.stack([games, aid]).astype(np.int64))
+        gi_d, aid_d = ga_d[0], ga_d[1]
+        roots_d = states_d.index_select(0, gi_d).contiguous()
+        sets_g = sets_d.index_select(0, gi_d).contiguous()
+        players = roots_d[:, 241] & 3
+        zi_d = aid_d.to(torch.int32)
+        if iters not in log_tables:
+            log_tables[iters] = up(mcts_log_table(iters))
+        ready = torch.cuda.Event()
+        ready.record(stream)
+        js.wait_event(ready)
+        with torch.cuda.stream(js):
+            nodes = torch.empty((k, mcts_node_cap(iters) * N.MCTS_NODE_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            o_d = torch.zeros((k, N.MCTS_OUT_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            eng.mcts_device(roots_d, sets_g, players, None, zob_d, zi_d, mtm_d, log_tables[iters], nodes, o_d,
+                            iterations=iters, tt_keys=ttk_d if use_tt else None, tt_vals=ttv_d if use_tt else None,
+                            tt_count=ttc_d if use_tt else None, max_rollout_moves=roll, exploration=c,
+                            rollout_policy=policy, asynchronous=True, state_rows=True)
+            done = torch.cuda.Event()
+            done.record(js)
+        for t in (ga_d, roots_d, sets_g, players, zi_d):
+            t.record_stream(js)
+        inflight[games] = True
+        jobs.append({"slot": slot, "games": games, "aid": aid, "done": done, "t0": time.perf_counter(),
+                     "nodes": nodes, "o_d": o_d, "cap": None, "seq": tl["mcts_jobs_launched"],
+                     "key": (iters, roll, c, use_tt, policy), "inflight_at_launch": len(jobs), "early": True,
+                     "flags": done_a[:k], "left": np.ones(k, bool)})
+        tl["mcts_jobs_launched"] += 1
+
+    def handback(job, ks, words=None):
+        """Moves of the job's searches ks (their result words, bk_mcts_set_done): the
+        games play on."""
+        w = job["flags"][ks] if words is None else words
+        status = (w >> np.uint64(56)) & np.uint64(0x7F)
+        if (status & ~np.uint64(N.MCTS_EUNCERT)).any():
+            jobs.remove(job)
+            mcts_finish(job)  # waits for the launch and raises with its failure record
+            return
+        games, aid = job["games"][ks], job["aid"][ks]
+        prof["uncertified_heuristic"] += int(np.count_nonzero(status & np.uint64(N.MCTS_EUNCERT)))
+        its = ((w >> np.uint64(32)) & np.uint64(0xFFFFFF)).astype(np.int64)
+        best = (w & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+        last_iters[aid] = its
+        for i, a, mv, it in zip(games.tolist(), aid.tolist(), best.tolist(), its.tolist()):
+            forced[i] = int(mv)
+            e = per_agent[i][mcts[a]["name"]]
+            e["total_simulations"] += float(it)
+            e["moves_with_simulations"] += 1
+        inflight[games] = False
+        job["left"][ks] = False
+        tl["handback_games"] += len(ks)
+        tl["handback_s"] += (time.perf_counter() - job["t0"]) * len(ks)
 
     def mcts_launch(games, pls, aid, iters, roll, c, use_tt, policy):
         slot = free_slots.pop(0)
+        if early:
+            mcts_launch_early(slot, games, aid, iters, roll, c, use_tt, policy)
+            return
         eng, js = engines[slot], jstreams[slot]
         ga_d = up(np.stack([games, aid]).astype(np.int64))  # one copy in; nothing comes back
         gi_d, aid_d = ga_d[0], ga_d[1]
@@ -788,15 +862,27 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             raise RuntimeError(f"bk_mcts: {int(np.count_nonzero(bad))} searches stopped early, status bits "
                                f"{int(np.bitwise_or.reduce(bad)) if bad.any() else 0}; failure record {rec}; "
                                f"synchronize: {sync_err}{where}")
-        prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
         its = o["iterations_run"].astype(np.int64)
         kms, kplies = eng.last_kernel_ms(), int(o["rollout_plies"].astype(np.int64).sum())
+        if len(games):  # a launch lasts as long as its longest search: its work against the mean
+            pl = o["rollout_plies"].astype(np.float64)
+            tl["job_plies_max_over_mean"] += float(pl.max() / max(pl.mean(), 1.0))
         for t in (SEARCH_TOTALS, SEARCH_TOTALS["by_kernel"].setdefault(
                 eng.last_kernel(), {"launches": 0, "kernel_ms": 0.0, "sims": 0, "rollout_plies": 0})):
             t["launches"] += 1
             t["kernel_ms"] += kms
             t["sims"] += int(its.sum())
             t["rollout_plies"] += kplies
+        if job.get("early"):
+            rest = np.flatnonzero(job["left"])
+            if len(rest):  # (the launch has ended: its out records are complete)
+                oo = o[rest]
+                handback(job, rest, (oo["best_move"].astype(np.int64) & 0xFFFFFFFF).astype(np.uint64) |
+                         (oo["iterations_run"].astype(np.uint64) << np.uint64(32)) |
+                         (oo["status"].astype(np.uint64) << np.uint64(56)) | np.uint64(1 << 63))
+            free_slots.append(job["slot"])
+            return
+        prof["uncertified_heuristic"] += int(np.count_nonzero(o["status"] & N.MCTS_EUNCERT))
         last_iters[aid] = its
         for i, a, mv, it in zip(games.tolist(), aid.tolist(), o["best_move"].tolist(), its.tolist()):
             forced[i] = int(mv)
@@ -864,15 +950,23 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
             e["moves_with_simulations"] += 1
 
     def drain():
-        done_m = [j for j in jobs if j["done"].query()]
-        for j in done_m:
-            jobs.remove(j)
-            mcts_finish(j)
-        return bool(done_m)
+        moved = False
+        for j in list(jobs):
+            if j.get("early"):
+                new = np.flatnonzero((j["flags"] >> np.uint64(63)).astype(bool) & j["left"])
+                if len(new):
+                    handback(j, new)
+                    moved = True
+            if j in jobs and j["done"].query():
+                jobs.remove(j)
+                mcts_finish(j)
+                moved = True
+        return moved
 
     stops_q = np.zeros(n, np.int64)  # the FastMCTS seats' quick_index (stop info)
     # host-side timeline: jobs' launch -> completion seen, games inside a search per step
-    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "search_games_per_step": 0, "mcts_jobs_launched": 0}
+    tl = {"mcts_jobs": 0, "mcts_job_s": 0.0, "mcts_job_games": 0, "search_games_per_step": 0, "mcts_jobs_launched": 0,
+          "job_plies_max_over_mean": 0.0, "handback_games": 0, "handback_s": 0.0}
     try:
         while active.any():
             prof["rounds"] += 1
@@ -979,12 +1073,21 @@ def _run_games_device(run_config: RunConfig, idx: List[int], seats: List[Mapping
         prof["timeline"] = {"mcts_jobs": tl["mcts_jobs"],
                             "mcts_job_ms_mean": 1e3 * tl["mcts_job_s"] / max(1, tl["mcts_jobs"]),
                             "mcts_games_per_job": tl["mcts_job_games"] / max(1, tl["mcts_jobs"]),
+                            "job_plies_max_over_mean": tl["job_plies_max_over_mean"] / max(1, tl["mcts_jobs"]),
+                            "handback": early,
+                            "handback_ms_mean": 1e3 * tl["handback_s"] / max(1, tl["handback_games"]),
                             "games_in_search_per_step": tl["search_games_per_step"] / max(1, prof["rounds"])}
         stream.synchronize()
     finally:
         if stream is not caller:
             stream.synchronize()
             torch.cuda.set_stream(caller)
+        for j in jobs:  # (an exception left launches running: they still write the buffers)
+            j["done"].synchronize()
+        for e in engines:
+            e.handle.set_done(None)
+        for b in hb_done.values():
+            b.close()
     dt = time.perf_counter() - t0
     prof["total_s"] = dt
     prof["host_s"] = dt - prof["setup_s"] - prof["advance_s"] - prof["mcts_s"] - prof["fast_s"] - prof["wait_s"]
@@ -1042,9 +1145,16 @@ class ArenaOptions:
     * reserve_cus: search streams may not use this many CUs (bk_stream_create; slower).
     * high_priority: the per-step kernels on a high-priority stream.
     * serial_worker: host-staged driver's searches on the calling thread (profiling).
-    * capture_dir: keep each search launch's inputs; save and replay a failed one."""
+    * capture_dir: keep each search launch's inputs; save and replay a failed one.
+    * handback: with pipeline, each search's move goes back to its game as soon as that
+      search is done (bk_mcts_set_done result words in mapped host memory, agent state
+      rows updated in place: BK_MCTS_STATE_ROWS), not when its launch's longest search
+      (2.3x the mean at config 4) ends.  Off by default: measured slower -- the games'
+      searches then overlap more and each runs ~4x longer (1,160 vs 1,219 games/s at
+      1,024 games, profiles/r06/sweeps/r06ai).  Ignored with capture_dir."""
     device_driver: bool = True
     pipeline: bool = True
+    handback: bool = False
     search_streams: int = 8
     job_games: int = 1_000_000
     reserve_cus: int = 0

@@ -111,6 +111,16 @@ static const int bk_sections_registered = (bk_register_sections(bk_read_sections
 #define WAVE 64
 #define BLOCK 256
 #define ROWMASK 0x000FFFFFu  // columns 0..19
+
+// Lane-pair exchanges (k_mcts_pair: lanes 2q, 2q + 1 share a search) on DPP quad_perm --
+// ALU latency, where __shfl is a ds_bpermute round trip.  Both lanes of the pair must be
+// active (they run in lockstep wherever these are used).
+__device__ __forceinline__ int pair_other(int v) {  // the partner's value (lane ^ 1)
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
+}
+__device__ __forceinline__ int pair_even(int v) {  // the even lane's value (lane & ~1)
+    return __builtin_amdgcn_update_dpp(0, v, 0xA0, 0xF, 0xF, false);  // quad_perm [0, 0, 2, 2]
+}
 #define OFFBOARD 0xFFF00000u // columns 20..31
 // word views of int16 frontier tables: may_alias, or type-based alias analysis lets the
 // compiler move them across int16 accesses of the same bytes
@@ -832,7 +842,7 @@ __device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2*
         rows[(r0 + i) * WAVE].y = okv[i];
         arows |= okv[i] ? (1u << (r0 + i + 4)) : 0u;
     }
-    arows |= (uint32_t)__shfl_xor((int)arows, 1);
+    arows |= (uint32_t)pair_other((int)arows);
     const int H = (int)((info >> 16) & 0xFFu);
     const uint32_t hmask = (1u << H) - 1u;
     uint32_t rev[5] = {0u, 0u, 0u, 0u, 0u};
@@ -879,7 +889,7 @@ __device__ __forceinline__ void locate_frontier_pair(int gs, uint32_t kk, uint2*
                 hm[t] = (d < H && ar >= 0) ? (rows[(ar < 0 ? 0 : ar) * WAVE].y & ((rt[t] << fc) >> 4)) : 0u;
                 tot += __builtin_popcount(hm[t]);
             }
-            const uint32_t both = tot + (uint32_t)__shfl_xor((int)tot, 1);
+            const uint32_t both = tot + (uint32_t)pair_other((int)tot);
             if (cnt + both > kk) { hit_f = f; continue; }
 #pragma unroll
             for (int t = 0; t < 3; ++t)
@@ -3412,6 +3422,17 @@ struct MctsArgs {
     uint32_t launch_seq;   // this launch's number on the handle (recorded in a failure record)
     uint32_t kernel_id;    // BK_DIAG_K_*: which search kernel runs (recorded in a failure record)
     uint32_t* started;     // one bit per search of the launch, set when a wave starts it (mc_mark_started)
+    // BK_MCTS_STATE_ROWS: search g's agent state is row zidx[g] of mt_rows / tt_* (the
+    // agent's own rows): the MT state is copied into mt[g] (the handle's scratch) at the
+    // search's start and back at its end, the TT is probed and filled in place -- all
+    // with system-scope loads and stores, which bypass the XCDs' L2s, so a search that
+    // starts while an earlier launch still runs (on another XCD) sees the agent's rows as
+    // that launch's finished search left them, with no L2 writeback
+    int32_t state_rows;
+    uint32_t* mt_rows;
+    // bk_mcts_set_done: done[g] = the search's result word (mc_done_word) once its agent
+    // rows are written back (bit 63 set; one 64-bit store to mapped host memory)
+    uint64_t* done;
 };
 
 struct Mc {
@@ -3424,6 +3445,7 @@ struct Mc {
     int32_t root_player, root_cp;
     int32_t cur, player, plies, score0;
     uint32_t status, mt_pos, first, tt_slot;
+    int32_t row;        // the search's MT / TT row (g, or zidx[g] with BK_MCTS_STATE_ROWS)
     bool tt_miss;
     Quad used, cells;
     uint64_t hash, t0;
@@ -3655,10 +3677,45 @@ __device__ __forceinline__ bool mc_mark_started(const MctsArgs& a, int32_t g, ui
     return true;
 }
 
-__device__ __forceinline__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab) {
+// System-scope (L2-bypassing) accesses of the agent rows under BK_MCTS_STATE_ROWS
+template <typename T>
+__device__ __forceinline__ T sys_ld(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void sys_st(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t tt_key_ld(const MctsArgs& a, const uint64_t* p) {
+    return a.state_rows ? sys_ld(p) : *p;
+}
+__device__ __forceinline__ double tt_val_ld(const MctsArgs& a, const double* p) {
+    return a.state_rows ? __longlong_as_double((long long)sys_ld(reinterpret_cast<const uint64_t*>(p))) : *p;
+}
+
+// lane / nl: the lanes sharing the search (the cooperative kernels: 0..63 of 64), which
+// split the agent row copies
+__device__ __forceinline__ void mc_start_game(const MctsArgs& a, Mc& m, McLane* L, int32_t g, const uint64_t* htab,
+                                              int lane = 0, int nl = 1) {
     m.game = g;
     m.mode = MC_SELECT;
-    m.tt_cnt = a.cfg.use_tt ? a.tt_count[g] : 0;
+    m.row = a.state_rows ? a.zidx[g] : g;
+    if (a.state_rows) {  // the agent's MT state into the search's working copy
+        const uint32_t* src = a.mt_rows + (size_t)m.row * (FM_N + 1);
+        uint32_t* dst = a.mt + (size_t)g * (FM_N + 1);
+        for (int i0 = lane; i0 < FM_N + 1; i0 += 8 * nl) {  // 8 loads in flight per lane
+            uint32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = i0 + j * nl < FM_N + 1 ? sys_ld(src + i0 + j * nl) : 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i0 + j * nl < FM_N + 1) dst[i0 + j * nl] = v[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the other lanes' copies are visible
+        m.tt_cnt = a.cfg.use_tt ? sys_ld(a.tt_count + m.row) : 0;
+    } else {
+        m.tt_cnt = a.cfg.use_tt ? a.tt_count[g] : 0;
+    }
     m.root_player = a.players[g] & 3;
     m.root_cp = a.roots[g].current_player & 3;
     m.mt_pos = a.mt[(size_t)g * (FM_N + 1) + FM_N];
@@ -3706,7 +3763,14 @@ __device__ __forceinline__ int32_t mc_child_slot(bk_mcts_node* pool, bk_mcts_nod
     return nd->child0 + (int32_t)ne;
 }
 
-__device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m) {
+// the host's per-search result word (bk_mcts_set_done): best_move in bits 0..31,
+// iterations_run in 32..55, status in 56..62, bit 63 set
+__device__ __forceinline__ uint64_t mc_done_word(const bk_mcts_out& o) {
+    return (uint64_t)(uint32_t)o.best_move | ((uint64_t)((uint32_t)o.iterations_run & 0xFFFFFFu) << 32) |
+           ((uint64_t)(o.status & 0x7Fu) << 56) | (1ull << 63);
+}
+
+__device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m, int lane = 0, int nl = 1) {
     const int32_t g = m.game;
     const bk_mcts_node* pool = a.nodes + (size_t)g * a.cfg.node_cap;
     const bk_mcts_node root = pool[0];
@@ -3730,21 +3794,41 @@ __device__ __forceinline__ void mc_finish_game(const MctsArgs& a, Mc& m) {
     o.status = m.status;
     o.rollout_plies = m.rplies;
     a.out[g] = o;
-    a.mt[(size_t)g * (FM_N + 1) + FM_N] = m.mt_pos;
-    if (a.cfg.use_tt) a.tt_count[g] = m.tt_cnt;
+    if (a.state_rows) {  // the working MT state back into the agent's row, write-through
+        uint32_t* mt = a.mt + (size_t)g * (FM_N + 1);
+        if (lane == 0) mt[FM_N] = m.mt_pos;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        uint32_t* dst = a.mt_rows + (size_t)m.row * (FM_N + 1);
+        for (int i0 = lane; i0 < FM_N + 1; i0 += 8 * nl) {
+            uint32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = i0 + j * nl < FM_N + 1 ? mt[i0 + j * nl] : 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (i0 + j * nl < FM_N + 1) sys_st(dst + i0 + j * nl, v[j]);
+        }
+        if (a.cfg.use_tt) sys_st(a.tt_count + m.row, (int32_t)m.tt_cnt);
+    } else {
+        a.mt[(size_t)g * (FM_N + 1) + FM_N] = m.mt_pos;
+        if (a.cfg.use_tt) a.tt_count[g] = m.tt_cnt;
+    }
+    if (a.done) {  // after every store above (and the TT's) has completed: the wave's vmcnt
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sys_st(a.done + g, mc_done_word(o));
+    }
     m.game = -1;
 }
 
 // TT probe for m.hash: hit -> reward; miss -> remembers the free slot for the insert
 __device__ __forceinline__ bool mc_tt_lookup(const MctsArgs& a, Mc& m, double& reward) {
     const uint64_t mask = (uint64_t)a.cfg.tt_cap - 1u;
-    const uint64_t* keys = a.tt_keys + (size_t)m.game * a.cfg.tt_cap;
-    const double* vals = a.tt_vals + (size_t)m.game * a.cfg.tt_cap;
+    const uint64_t* keys = a.tt_keys + (size_t)m.row * a.cfg.tt_cap;
+    const double* vals = a.tt_vals + (size_t)m.row * a.cfg.tt_cap;
     uint64_t i = m.hash & mask;
     for (;;) {
-        const double v = vals[i];
+        const double v = tt_val_ld(a, vals + i);
         if (v != v) break;
-        if (keys[i] == m.hash) { reward = v; return true; }
+        if (tt_key_ld(a, keys + i) == m.hash) { reward = v; return true; }
         i = (i + 1) & mask;
     }
     m.tt_slot = (uint32_t)i;
@@ -3762,8 +3846,15 @@ __device__ __forceinline__ void mc_complete(const MctsArgs& a, Mc& m, McLane* L,
             if ((uint32_t)m.tt_cnt + 2u > (uint32_t)a.cfg.tt_cap) {
                 m.status |= BK_MCTS_ETT;
             } else {
-                a.tt_keys[(size_t)m.game * a.cfg.tt_cap + m.tt_slot] = m.hash;
-                a.tt_vals[(size_t)m.game * a.cfg.tt_cap + m.tt_slot] = reward;
+                uint64_t* kp = a.tt_keys + (size_t)m.row * a.cfg.tt_cap + m.tt_slot;
+                double* vp = a.tt_vals + (size_t)m.row * a.cfg.tt_cap + m.tt_slot;
+                if (a.state_rows) {
+                    sys_st(kp, m.hash);
+                    sys_st(reinterpret_cast<uint64_t*>(vp), (uint64_t)__double_as_longlong(reward));
+                } else {
+                    *kp = m.hash;
+                    *vp = reward;
+                }
                 m.tt_cnt++;
             }
         }
@@ -3986,11 +4077,10 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         const bk_fset* ofs = nullptr;  // PAIR: the pair's node / sim tables and the mover's mask
         uint32_t omask = 0xFFFFu;
         if constexpr (PAIR) {
-            const int o = lane & ~1;
-            c_idle = __shfl((int)idle, o) != 0;
-            cp = __shfl(p, o);
-            c_first = (uint32_t)__shfl((int)c_first, o);
-            c_used = (uint32_t)__shfl((int)c_used, o);
+            c_idle = pair_even((int)idle) != 0;
+            cp = pair_even(p);
+            c_first = (uint32_t)pair_even((int)c_first);
+            c_used = (uint32_t)pair_even((int)c_used);
             c_base = a.slab + (size_t)(slot & ~1u) * SLAB_WORDS;
             ofs = &a.lanes[slot & ~1u].A.s;
             omask = ofs->mask[cp];
@@ -4025,7 +4115,7 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         }
         const uint32_t avail = c_idle ? 0u : (~c_used & 0x1FFFFFu);
         uint32_t total = movegen_counts<true, PAIR>(P, avail, my, lane);
-        if constexpr (PAIR) total += (uint32_t)__shfl_xor((int)total, 1);
+        if constexpr (PAIR) total += (uint32_t)pair_other((int)total);
         SECT(9);
         // PAIR: the odd lane of a busy pair stays for the pair's locate (below)
         if (!PAIR && idle) continue;
@@ -4092,10 +4182,10 @@ __device__ __forceinline__ void mcts_body(const MctsArgs& a) {
         SECT(10);
         if constexpr (PAIR) {
             // both lanes of a busy pair: the even lane's orientation, rank and table
-            const int o = lane & ~1;
-            const bool pact = __shfl((int)act, o) != 0;
-            const int pgs = __shfl(gs, o);
-            const uint32_t pkk = (uint32_t)__shfl((int)kk, o);
+            const int o = lane & ~1;  // the pair's even lane (its LDS column)
+            const bool pact = pair_even((int)act) != 0;
+            const int pgs = pair_even(gs);
+            const uint32_t pkk = (uint32_t)pair_even((int)kk);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA stage has landed
             if (pact) {
                 uint2* prow = reinterpret_cast<uint2*>(my) + o;
@@ -4784,13 +4874,13 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
                 uint32_t twice = 0;
                 if (lane == 0) twice = mc_mark_started(a, next, (uint32_t)next) ? 1u : 0u;
                 twice = __shfl(twice, 0);
-                mc_start_game(a, m, L, next, htab);
+                mc_start_game(a, m, L, next, htab, lane, WAVE);
                 if (twice) m.status |= BK_MCTS_EINTERNAL;
                 root_mc = (int)a.roots[next].move_count;  // (constant for the search)
             }
             const bool timed_out = a.cfg.time_limit_us > 0 && wall_clock64() - m.t0 >= a.limit_ticks;
             const bool chunk_end = a.cfg.iter_stop > 0 && m.it >= a.cfg.iter_stop;
-            if (m.it >= a.cfg.iterations || chunk_end || timed_out || MC_FATAL(m.status)) { mc_finish_game(a, m); continue; }
+            if (m.it >= a.cfg.iterations || chunk_end || timed_out || MC_FATAL(m.status)) { mc_finish_game(a, m, lane, WAVE); continue; }
             const uint64_t* Z = a.zobrist + (size_t)a.zidx[m.game] * MC_ZOB;
             if (mc_select(a, m, L, Z)) { mc_sim_terminal(a, m, L); continue; }
             if (MC_FATAL(m.status)) continue;
@@ -5047,6 +5137,8 @@ struct bk_handle_s {
     uint32_t* d_counter = nullptr;
     uint32_t* d_diag = nullptr;        // bk_mcts failure record (mc_diag), sticky until reported
     void* d_started = nullptr; size_t d_started_cap = 0;  // bk_mcts: searches started (mc_mark_started)
+    uint64_t* mcts_done = nullptr;  // bk_mcts_set_done: per-search result words
+    void* d_mtwork = nullptr; size_t d_mtwork_cap = 0;  // BK_MCTS_STATE_ROWS: the searches' MT copies
     uint32_t diag_host[BK_DIAG_WORDS] = {0};  // the last record bk_synchronize reported
     bool diag_seen = false;
     uint32_t mcts_launches = 0;
@@ -5136,12 +5228,15 @@ static int take_diag(bk_handle h) {
     return set_err(h, BK_ECHECK, "bk_mcts: %s; bk_debug_mcts_failure has the record", msg);
 }
 
+// A handle's scratch grows in stream order on the handle's current stream
+// (hipFreeAsync / hipMallocAsync): hipFree would wait for the whole device, stalling
+// every other stream's launches (the arena's search streams regrow as job sizes vary).
 static int grow(bk_handle h, void** p, size_t* cap, size_t need) {
     if (need <= *cap) return BK_OK;
-    if (*p) (void)hipFree(*p);
+    if (*p) (void)hipFreeAsync(*p, h->cur);
     *p = nullptr; *cap = 0;
-    size_t n = need + need / 4 + 256;
-    HIPCHK(h, hipMalloc(p, n));
+    size_t n = need + need / 2 + 256;
+    HIPCHK(h, hipMallocAsync(p, n, h->cur));
     *cap = n;
     return BK_OK;
 }
@@ -5227,7 +5322,7 @@ int bk_destroy(bk_handle h) {
     if (h->busy) (void)hipStreamSynchronize(h->busy_stream);
     if (h->own) (void)hipStreamSynchronize(h->own);
     void* bufs[] = {h->d_in, h->d_out, h->d_aux, h->d_aux2, h->d_slab, h->d_fin, h->d_fout, h->d_fslab,
-                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh, h->d_diag, h->d_started};
+                    h->d_mc, h->d_mclane, h->d_step, h->d_counter, h->d_rh, h->d_diag, h->d_started, h->d_mtwork};
     for (void* b : bufs) if (b) (void)hipFree(b);
     if (h->ev0) (void)hipEventDestroy(h->ev0);
     if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -5294,6 +5389,24 @@ int bk_debug_mcts_failure(bk_handle h, uint32_t* out, int32_t n) {
     const int32_t k = n < BK_DIAG_WORDS ? n : BK_DIAG_WORDS;
     for (int32_t i = 0; i < n; ++i) out[i] = i < k && h->diag_seen ? h->diag_host[i] : 0u;
     return h->diag_seen ? 1 : 0;
+}
+
+int bk_mcts_set_done(bk_handle h, uint64_t* done) {
+    if (!h) return BK_EINVAL;
+    h->mcts_done = done;
+    return BK_OK;
+}
+
+void* bk_host_alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    memset(p, 0, bytes);
+    return p;
+}
+
+int bk_host_free(void* p) {
+    if (!p) return BK_OK;
+    return hipHostFree(p) == hipSuccess ? BK_OK : BK_EHIP;
 }
 
 int bk_last_error(bk_handle h, char* buf, size_t len) {
@@ -6061,6 +6174,8 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
         return set_err(h, BK_EINVAL, "bk_mcts: bad cfg (iterations/max_rollout_moves/node_cap/iter_stop/resume)%s", "");
     if (cfg->resume && !nodes)
         return set_err(h, BK_EINVAL, "bk_mcts: resume needs the caller's nodes buffer%s", "");
+    if ((cfg->flags & BK_MCTS_STATE_ROWS) && mem != BK_MEM_DEVICE)
+        return set_err(h, BK_EINVAL, "bk_mcts: BK_MCTS_STATE_ROWS needs BK_MEM_DEVICE buffers%s", "");
     if (cfg->use_tt && (!tt_keys || !tt_vals || !tt_count || cfg->tt_cap < 2 || (cfg->tt_cap & (cfg->tt_cap - 1))))
         return set_err(h, BK_EINVAL, "bk_mcts: use_tt needs tt buffers and a power-of-two tt_cap%s", "");
     if (mem == BK_MEM_HOST) {
@@ -6177,6 +6292,14 @@ int bk_mcts(bk_handle h, const bk_state* roots, const bk_fset* root_sets, const 
                (uint64_t)cfg->time_limit_us * (uint64_t)khz / 1000u, tree_batch, spread, 1, 1};
     a.diag = h->d_diag;
     a.launch_seq = ++h->mcts_launches;
+    a.state_rows = (cfg->flags & BK_MCTS_STATE_ROWS) ? 1 : 0;
+    a.done = h->mcts_done;
+    if (a.state_rows) {  // the searches work on copies of their agents' MT rows
+        rc = grow(h, &h->d_mtwork, &h->d_mtwork_cap, sizeof(uint32_t) * (FM_N + 1) * n);
+        if (rc) return rc;
+        a.mt_rows = a.mt;
+        a.mt = (uint32_t*)h->d_mtwork;
+    }
     {
         const size_t sb = sizeof(uint32_t) * (((size_t)n_games + 31) / 32 + 1);
         rc = grow(h, &h->d_started, &h->d_started_cap, sb);

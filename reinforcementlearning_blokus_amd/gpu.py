@@ -478,7 +478,8 @@ class BlokusGPU:
                     out, *, iterations: int, tt_keys=None, tt_vals=None, tt_count=None, rewards=None,
                     hit_flags=None, max_rollout_moves: int = 50, exploration: float = 1.414, chunk: int = 0,
                     on_chunk=None, stop_after: int | None = None, rollout_policy: int = N.MCTS_ROLLOUT_RANDOM,
-                    resume_from: int | None = None, time_limit_us: int = 0, asynchronous: bool = False):
+                    resume_from: int | None = None, time_limit_us: int = 0, asynchronous: bool = False,
+                    state_rows: bool = False, out_ptr: int | None = None):
         """bk_mcts with every buffer a torch CUDA tensor on this device (zero copy,
         BK_MEM_DEVICE, torch's current stream): the config-5 path, where the trees
         (nodes[n, node_cap]), TTs and RNG states of 65,536 searches stay in HBM.
@@ -494,22 +495,31 @@ class BlokusGPU:
         the first iteration boundary past it (no chunking).  Raises if any search reports
         a nonzero status.  asynchronous: one launch, enqueued on torch's current stream
         and not waited for (BK_MCTS_ASYNC); the caller checks the statuses in `out` and
-        calls synchronize() once the stream has passed it."""
+        calls synchronize() once the stream has passed it.  state_rows (BK_MCTS_STATE_ROWS):
+        mt_state / tt_* are the agents' rows [agents, ...], search g using row
+        zobrist_index[g] (BK_MCTS_STATE_ROWS).  out_ptr: write the out records there instead
+        (memory the device can write; `out` is then ignored)."""
         import torch
         n = roots.shape[0]
         use_tt = tt_keys is not None
         node_cap = nodes.shape[1] // N.MCTS_NODE_DTYPE.itemsize
+        rows = mt_state.shape[0] if state_rows else n  # agent rows, or one per search
+        if state_rows and rows < zobrist.shape[0]:  # zobrist_index < n_zobrist: every row it names exists
+            raise ValueError(f"state_rows: {rows} mt_state rows for {zobrist.shape[0]} zobrist rows")
         tensors = dict(roots=(roots, torch.uint8, (n, 256)), root_sets=(root_sets, torch.uint8, (n, N.FSET_DTYPE.itemsize)),
                        players=(players, torch.uint8, (n,)),
-                       zobrist_index=(zobrist_index, torch.int32, (n,)), mt_state=(mt_state, torch.int32, (n, 625)),
-                       nodes=(nodes, torch.uint8, (n, node_cap * N.MCTS_NODE_DTYPE.itemsize)),
-                       out=(out, torch.uint8, (n, N.MCTS_OUT_DTYPE.itemsize)))
+                       zobrist_index=(zobrist_index, torch.int32, (n,)), mt_state=(mt_state, torch.int32, (rows, 625)),
+                       nodes=(nodes, torch.uint8, (n, node_cap * N.MCTS_NODE_DTYPE.itemsize)))
+        if out_ptr is None:
+            tensors.update(out=(out, torch.uint8, (n, N.MCTS_OUT_DTYPE.itemsize)))
+        else:
+            assert asynchronous and not (chunk or stop_after or resume_from), "out_ptr: one asynchronous launch"
         if root_hash is not None:  # None: ZobristHash.hash_board computed on the device (k_root_hash)
             tensors.update(root_hash=(root_hash, torch.int64, (n,)))
         if use_tt:
             cap = tt_keys.shape[1]
-            tensors.update(tt_keys=(tt_keys, torch.int64, (n, cap)), tt_vals=(tt_vals, torch.float64, (n, cap)),
-                           tt_count=(tt_count, torch.int32, (n,)))
+            tensors.update(tt_keys=(tt_keys, torch.int64, (rows, cap)), tt_vals=(tt_vals, torch.float64, (rows, cap)),
+                           tt_count=(tt_count, torch.int32, (rows,)))
         if rewards is not None:
             tensors.update(rewards=(rewards, torch.float64, (n, iterations)),
                            hit_flags=(hit_flags, torch.uint8, (n, iterations)))
@@ -529,10 +539,12 @@ class BlokusGPU:
             resume = int(j > 0 or resume_from is not None)
             cfg = N.BkMctsCfg(iterations, max_rollout_moves, float(exploration), int(use_tt), node_cap,
                               tt_keys.shape[1] if use_tt else 0, int(time_limit_us), stop, resume,
-                              int(rollout_policy), N.MCTS_ASYNC if asynchronous else 0)
+                              int(rollout_policy), (N.MCTS_ASYNC if asynchronous else 0) |
+                              (N.MCTS_STATE_ROWS if state_rows else 0))
             self.handle.mcts(d(roots), d(root_sets), d(players), d(root_hash), n, cfg, d(zobrist), zobrist.shape[0],
                              d(zobrist_index), d(mt_state), d(tt_keys), d(tt_vals), d(tt_count), d(log_table),
-                             log_table.shape[0], d(nodes), d(rewards), d(hit_flags), d(out), N.MEM_DEVICE)
+                             log_table.shape[0], d(nodes), d(rewards), d(hit_flags),
+                             out_ptr if out_ptr is not None else d(out), N.MEM_DEVICE)
             if on_chunk is not None:
                 on_chunk(stop or iterations)
         if asynchronous:

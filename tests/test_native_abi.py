@@ -12,7 +12,7 @@ from tests.conftest import ROOT, load_golden
 
 def declared_symbols():
     text = open(os.path.join(ROOT, "include", "blokus_hip.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\s*\*)\s*(bk_\w+)\s*\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|const char\s*\*|void\s*\*)\s*(bk_\w+)\s*\(", text, flags=re.M)))
 
 
 def test_header_and_binding_agree():
@@ -23,7 +23,7 @@ def test_library_exports_every_symbol():
     lib = N.load()
     for name in declared_symbols():
         assert hasattr(lib, name), name
-    assert lib.bk_abi_version() == N.ABI_VERSION == 6
+    assert lib.bk_abi_version() == N.ABI_VERSION == 7
     assert lib.bk_tables_version() >= 1
 
 
@@ -48,6 +48,8 @@ def test_invalid_arguments_rejected_without_gpu():
     assert lib.bk_orient_info(91, None, None, None, None) == N.EINVAL
     assert lib.bk_set_tuning(None, 0, 1) == N.EINVAL
     assert lib.bk_get_tuning(None, 0, None) == N.EINVAL
+    assert lib.bk_mcts_set_done(None, None) == N.EINVAL
+    assert lib.bk_host_free(None) == N.OK
 
 
 def test_environment_read_only_at_handle_creation():
