@@ -4709,12 +4709,17 @@ __device__ __forceinline__ bool coop_heur_balanced(const uint2* rows, uint32_t* 
 // rank holds each key's slot (0x7FFF elsewhere; wave-private LDS).  Count mode (E =
 // false): the kk-th new anchor in (slot, cell) order.  E: the anchor whose cumulative e
 // from R first exceeds target, certified as in heur_walk_frontier (the prefix sums differ
-// from the serial ones by rounding only, far inside the margin).  Tables of more than 128
-// slots return false: the caller walks serially.
+// from the serial ones by rounding only, far inside the margin): the new anchors are
+// listed in (slot, cell) order in `list` (wave-private LDS), their e values computed one
+// per lane and wave-scanned from R -- one heur_e per lane for a list of <= 64 anchors,
+// where the per-slot sums cost the busiest lane one heur_e per anchor of its two slots,
+// and resolving the chosen slot up to five more.  Tables of more than 128 slots return
+// false: the caller walks serially.
 template <bool E>
 __device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows, const int16_t* key, int mask,
                                           int16_t* rank, int lane, const HeurShared* hs, int edge_w, double target,
-                                          double R, double total, int& out_r, int& out_c, bool& uncertain) {
+                                          double R, double total, int& out_r, int& out_c, bool& uncertain,
+                                          uint16_t* list = nullptr) {
     if (mask > 2 * WAVE - 1) return false;
     int n;
     uint32_t cd[5], cc[5];
@@ -4736,7 +4741,6 @@ __device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     uint32_t cnt[2] = {0u, 0u}, newk[2] = {0u, 0u};  // newk bit k: cell k's anchor is new here
-    double es[2] = {0.0, 0.0};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (f[h] < 0) continue;
@@ -4753,59 +4757,81 @@ __device__ __forceinline__ bool coop_walk(int gs, uint32_t kk, const uint2* rows
             if (!fresh) continue;
             newk[h] |= 1u << k;
             ++cnt[h];
-            if constexpr (E) es[h] += heur_e(n, cd, cc, ar, acl, rows, hs, edge_w);
         }
+    }
+    if constexpr (E) {
+        const CoopScan sc = coop_scan(cnt, lane);
+        const uint32_t na = sc.total;
+        if (na == 0u) { out_r = -1; out_c = 0; return true; }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // this lane's new anchors at their list positions
+            uint32_t pos = h ? sc.i1 - sc.c1 : sc.i0 - sc.c0;
+            if (!newk[h]) continue;
+            const int fr = f[h] / 20, fc = f[h] - 20 * (f[h] / 20);
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                if ((newk[h] >> k) & 1u) list[pos++] = (uint16_t)((fr - (int)cd[k]) * 20 + fc - (int)cc[k]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double carry = R, lo = R, e_hit = 0.0;
+        int cell_hit = -1;
+#pragma unroll 1
+        for (uint32_t b0 = 0; b0 < na; b0 += WAVE) {
+            const uint32_t j = b0 + (uint32_t)lane;
+            int cell = 0;
+            double e = 0.0;
+            if (j < na) {
+                cell = list[j];
+                e = heur_e(n, cd, cc, cell / 20, cell - 20 * (cell / 20), rows, hs, edge_w);
+            }
+            const double incl = wave_incl_scan_f64(e, lane) + carry;
+            const double up = dpp_f64<DPP_WAVE_SHR1, 0xF>(incl);
+            const double excl = lane ? up : carry;
+            const uint64_t b = __ballot(j < na && incl > target);
+            if (b) {
+                const int L = __ffsll((unsigned long long)b) - 1;
+                cell_hit = lane_bcast(cell, L);
+                e_hit = lane_bcast(e, L);
+                lo = lane_bcast(excl, L);
+                break;
+            }
+            carry = lane_bcast(incl, WAVE - 1);
+            if (b0 + WAVE >= na) {  // rounding put the target past the last anchor: the last one, uncertified
+                const int L = (int)((na - 1u) & (WAVE - 1));
+                cell_hit = lane_bcast(cell, L);
+                e_hit = lane_bcast(e, L);
+                lo = lane_bcast(excl, L);
+                uncertain = true;
+            }
+        }
+        if (!(target - lo > HEUR_MARGIN * total && lo + e_hit - target > HEUR_MARGIN * total)) uncertain = true;
+        out_r = cell_hit / 20;
+        out_c = cell_hit - 20 * (cell_hit / 20);
+        return true;
     }
     // the slot holding the answer, then the anchor inside it in cell order
     int hit = -1, hh = 0;
     uint32_t before = 0;
-    double lo = R;
-    if constexpr (!E) {
+    {
         const CoopScan sc = coop_scan(cnt, lane);
         const uint64_t b0 = __ballot(kk < sc.i0 && kk >= sc.i0 - sc.c0);
         const uint64_t b1 = __ballot(kk < sc.i1 && kk >= sc.i1 - sc.c1);
         if (b0) { hit = __ffsll((unsigned long long)b0) - 1; before = lane_bcast(sc.i0 - sc.c0, hit); }
         else if (b1) { hit = __ffsll((unsigned long long)b1) - 1; hh = 1; before = lane_bcast(sc.i1 - sc.c1, hit); }
-    } else {
-        const double i0 = wave_incl_scan_f64(es[0], lane);
-        const double i1 = wave_incl_scan_f64(es[1], lane) + lane_bcast(i0, WAVE - 1);
-        const uint64_t b0 = __ballot(es[0] > 0.0 && R + i0 > target);
-        const uint64_t b1 = __ballot(es[1] > 0.0 && R + i1 > target);
-        if (b0) { hit = __ffsll((unsigned long long)b0) - 1; }
-        else if (b1) { hit = __ffsll((unsigned long long)b1) - 1; hh = 1; }
-        else {  // rounding put the target past the last anchor: the last one, uncertified
-            uncertain = true;
-            target = 1e300;
-            const uint64_t l1 = __ballot(newk[1] != 0u), l0 = __ballot(newk[0] != 0u);
-            if (l1) { hit = 63 - __clzll((unsigned long long)l1); hh = 1; }
-            else if (l0) { hit = 63 - __clzll((unsigned long long)l0); }
-        }
-        if (hit >= 0) lo = R + lane_bcast(hh ? i1 - es[1] : i0 - es[0], hit);
     }
     if (hit < 0) { out_r = -1; out_c = 0; return true; }
     // every lane resolves the chosen slot (identical work and result)
     const int fh = lane_bcast(hh ? f[1] : f[0], hit);
     const uint32_t nk = lane_bcast(hh ? newk[1] : newk[0], hit);
     const int fr = fh / 20, fc = fh - 20 * (fh / 20);
-    int found_r = -1, found_c = 0, last_r = -1, last_c = 0;
+    int found_r = -1, found_c = 0;
     uint32_t rem = kk - before;
-    double acc = lo, last_lo = lo, last_e = 0.0;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
         if (found_r >= 0 || !((nk >> k) & 1u)) continue;
-        const int ar = fr - (int)cd[k], acl = fc - (int)cc[k];
-        if constexpr (!E) {
-            if (rem == 0u) { found_r = ar; found_c = acl; } else { --rem; }
-        } else {
-            const double e = heur_e(n, cd, cc, ar, acl, rows, hs, edge_w);
-            last_r = ar; last_c = acl; last_lo = acc; last_e = e;
-            if (acc + e > target) { found_r = ar; found_c = acl; } else { acc += e; }
-        }
-    }
-    if constexpr (E) {
-        if (found_r < 0) { uncertain = true; found_r = last_r; found_c = last_c; }
-        if (!(target - last_lo > HEUR_MARGIN * total && last_lo + last_e - target > HEUR_MARGIN * total))
-            uncertain = true;
+        if (rem == 0u) { found_r = fr - (int)cd[k]; found_c = fc - (int)cc[k]; } else { --rem; }
     }
     out_r = found_r;
     out_c = found_c;
@@ -5003,7 +5029,7 @@ __device__ __forceinline__ void mcts_coop_body(const MctsArgs& a) {
 #pragma unroll
                 for (int r = 0; r < 20; ++r) rows_lds[r * WAVE].y = h_ok[r];
                 if (!coop_walk<true>(gs, 0u, rows_lds, tkey, (int)tmask, rank, lane, hs, edge_w, h_target,
-                                     h_R, h_total, ar, ac, h_unc))
+                                     h_R, h_total, ar, ac, h_unc, reinterpret_cast<uint16_t*>(my + COOP_ML_DWORD)))
                     heur_walk_frontier(gs, h_ok, rows_lds, tkey, (int)tmask, hs, edge_w, h_target, h_R,
                                        h_total, ar, ac, h_unc);
             } else {
