@@ -4562,14 +4562,23 @@ __device__ __forceinline__ void coop_ok_counts(const uint2* rows, const int (&og
 }
 
 // orientation g's legal moves (rows ok) into the move list from index idx: naive order
+// The 20 rows are packed into seven 64-bit words of cell bits (r * 20 + c) first, so the
+// divergent bit loops run 7 times (each as long as its busiest lane) instead of 20
 __device__ __forceinline__ void coop_list_moves(uint16_t* ml, uint32_t idx, uint32_t g, const uint32_t (&ok)[20]) {
+    uint64_t P[7] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
 #pragma unroll
     for (int r = 0; r < 20; ++r) {
-        uint32_t w = ok[r];
+        const int off = 20 * r, q = off / 64, sh = off % 64;
+        P[q] |= (uint64_t)ok[r] << sh;
+        if (sh > 44) P[q + 1] |= (uint64_t)ok[r] >> (64 - sh);
+    }
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        uint64_t w = P[q];
         while (w) {
-            const uint32_t x = (uint32_t)__builtin_ctz(w);
-            w &= w - 1u;
-            ml[idx++] = (uint16_t)(g * 400u + (uint32_t)r * 20u + x);
+            const uint32_t x = (uint32_t)__builtin_ctzll(w);
+            w &= w - 1ull;
+            ml[idx++] = (uint16_t)(g * 400u + 64u * (uint32_t)q + x);
         }
     }
 }
