@@ -3207,14 +3207,40 @@ __device__ __forceinline__ double py_random(uint32_t* mt, int& idx, int lane) {
     return ((double)a * 67108864.0 + (double)b) * (1.0 / 9007199254740992.0);
 }
 
-// wave argmax of (value, index): larger value wins, ties -> smaller index
+// wave argmax of (value, index): larger value wins, ties -> smaller index (a total
+// order, so any reduction order gives the same winner).  Inside each 16-lane row on DPP
+// (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: ALU latency), then the
+// four rows' winners by v_readlane -- where a __shfl_xor ladder is 18 dependent
+// ds_bpermute round trips per reduction (FastMCTS runs one per iteration).  All 64 lanes
+// active; every lane gets the result.
+template <int CTRL>
+__device__ __forceinline__ void argmax_dpp_step(double& v, int& j) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32), (int)(uint32_t)(b >> 32), CTRL,
+                                                              0xF, 0xF, false);
+    const int oj = __builtin_amdgcn_update_dpp(j, j, CTRL, 0xF, 0xF, false);
+    const double ov = __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint64_t)lo));
+    if (ov > v || (ov == v && oj < j)) { v = ov; j = oj; }
+}
 __device__ __forceinline__ void wave_argmax(double& v, int& j) {
+    argmax_dpp_step<0xB1>(v, j);   // quad_perm [1, 0, 3, 2]
+    argmax_dpp_step<0x4E>(v, j);   // quad_perm [2, 3, 0, 1]
+    argmax_dpp_step<0x141>(v, j);  // row_half_mirror
+    argmax_dpp_step<0x140>(v, j);  // row_mirror
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    double bv = v;
+    int bj = j;
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        const double ov = __shfl_xor(v, o);
-        const int oj = __shfl_xor(j, o);
-        if (ov > v || (ov == v && oj < j)) { v = ov; j = oj; }
+    for (int r = 0; r < 4; ++r) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 16 * r);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 16 * r);
+        const double ov = __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint64_t)lo));
+        const int oj = __builtin_amdgcn_readlane(j, 16 * r);
+        if (r == 0 || ov > bv || (ov == bv && oj < bj)) { bv = ov; bj = oj; }
     }
+    v = bv;
+    j = bj;
 }
 
 struct PowFix {  // bk_pow_half_fix tables: CPython's (2 log N / v) ** 0.5 vs sqrt
@@ -3255,6 +3281,7 @@ __device__ __forceinline__ int fm_select(const uint32_t* visits, const double* t
     return bj;
 }
 
+#define FM_LOG_LDS 1024
 struct FastMctsArgs {
     int32_t n_games;
     const int32_t* offset;
@@ -3275,11 +3302,15 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
     __shared__ uint32_t visits[BK_FASTMCTS_MAX_CHILDREN];
     __shared__ double total[BK_FASTMCTS_MAX_CHILDREN];
     __shared__ uint32_t mt[FM_N];
+    __shared__ double ltab[FM_LOG_LDS];  // the log table's first rows: one LDS read per iteration
     const int lane = threadIdx.x;
     const int game = blockIdx.x;
     if (game >= a.n_games) return;
     const int n = a.offset[game + 1] - a.offset[game];
     const int iters = a.iterations[game];
+    const int nlt = iters + 1 < a.log_len ? (iters + 1 < FM_LOG_LDS ? iters + 1 : FM_LOG_LDS)
+                                          : (a.log_len < FM_LOG_LDS ? a.log_len : FM_LOG_LDS);
+    for (int k = lane; k < nlt; k += WAVE) ltab[k] = a.log_table[k];
     const double base = a.base[game];
     uint32_t* st = a.mt_state + (size_t)game * (FM_N + 1);
     for (int k = lane; k < FM_N; k += WAVE) mt[k] = st[k];
@@ -3298,7 +3329,8 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
         if (nch < n) {
             sel = nch++;  // expand: untried_moves.pop() -> child nch <-> legal[n - 1 - nch]
         } else {
-            sel = fm_select(visits, total, nch, lane, 2.0 * a.log_table[root_visits], root_visits, a.c, a.fix);
+            const double lg = (int)root_visits < nlt ? ltab[root_visits] : a.log_table[root_visits];
+            sel = fm_select(visits, total, nch, lane, 2.0 * lg, root_visits, a.c, a.fix);
         }
         // NaN base: the cached legal list was empty -> reward 0.0 and no draw
         // (fast_mcts_agent.py:255-257)
