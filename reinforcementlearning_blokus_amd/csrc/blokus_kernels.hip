@@ -3324,23 +3324,96 @@ __global__ __launch_bounds__(WAVE) void k_fastmcts(FastMctsArgs a) {
     int nch = 0;
     uint32_t root_visits = 0;
     int it = 0;
-    for (; it < iters; ++it) {
-        int sel;
-        if (nch < n) {
-            sel = nch++;  // expand: untried_moves.pop() -> child nch <-> legal[n - 1 - nch]
-        } else {
-            const double lg = (int)root_visits < nlt ? ltab[root_visits] : a.log_table[root_visits];
-            sel = fm_select(visits, total, nch, lane, 2.0 * lg, root_visits, a.c, a.fix);
+    if (n <= 2 * WAVE) {
+        // Roots of <= 128 children (all of config 4's): child j's visits / total live in
+        // lane j % 64's registers (slot j / 64), so an iteration is the UCB terms, the DPP
+        // argmax and one register update by the child's lane -- no LDS round trip or
+        // barrier.  The rewards do not depend on the selection: base + random() * 0.1 of
+        // the stream's next two words each iteration, so they are drawn up to a twist ahead,
+        // one per lane (fm_rew), and the generator's position is set back to what the
+        // iterations actually consumed.
+        __shared__ double fm_rew[FM_N / 2];
+        const bool draw = base == base;  // NaN base: reward 0.0 and no draw (fast_mcts_agent.py:255-257)
+        uint32_t v0 = 0u, v1 = 0u;
+        double t0 = 0.0, t1 = 0.0;
+        int rptr = 0, ravail = 0, ridx = idx;  // fm_rew[rptr..ravail) drawn from word ridx on
+        for (; it < iters; ++it) {
+            int sel;
+            if (nch < n) {
+                sel = nch++;  // expand: untried_moves.pop() -> child nch <-> legal[n - 1 - nch]
+            } else {
+                const double lg = (int)root_visits < nlt ? ltab[root_visits] : a.log_table[root_visits];
+                const double L2 = 2.0 * lg;
+                double best = -1.0 / 0.0;
+                int bj = 0x7fffffff;
+                if (lane < nch) { best = t0 / (double)v0 + fm_explore(a.c, L2, v0, root_visits, a.fix); bj = lane; }
+                if (lane + WAVE < nch) {
+                    const double u = t1 / (double)v1 + fm_explore(a.c, L2, v1, root_visits, a.fix);
+                    if (u > best) { best = u; bj = lane + WAVE; }
+                }
+                wave_argmax(best, bj);
+                sel = bj;
+            }
+            double reward = 0.0;
+            if (draw) {
+                if (rptr == ravail) {  // the next draws (py_random's order, lazy twist)
+                    idx = ridx;
+                    if (idx >= FM_N) { py_twist(mt, lane); idx = 0; }
+                    const int m = (FM_N - idx) / 2;
+                    __syncthreads();
+                    if (m == 0) {  // one word left: this draw straddles the twist
+                        const double r = py_random(mt, idx, lane);
+                        if (lane == 0) fm_rew[0] = base + r * 0.1;
+                        ravail = 1;
+                    } else {
+                        for (int l = lane; l < m; l += WAVE) {
+                            uint32_t x = mt[idx + 2 * l], y = mt[idx + 2 * l + 1];
+                            x ^= x >> 11; x ^= (x << 7) & 0x9d2c5680u; x ^= (x << 15) & 0xefc60000u; x ^= x >> 18;
+                            y ^= y >> 11; y ^= (y << 7) & 0x9d2c5680u; y ^= (y << 15) & 0xefc60000u; y ^= y >> 18;
+                            const double r = ((double)(x >> 5) * 67108864.0 + (double)(y >> 6)) *
+                                             (1.0 / 9007199254740992.0);
+                            fm_rew[l] = base + r * 0.1;
+                        }
+                        ravail = m;
+                        idx += 2 * m;
+                    }
+                    ridx = idx;
+                    rptr = 0;
+                    __syncthreads();
+                }
+                reward = fm_rew[rptr++];
+            }
+            if (lane == (sel & (WAVE - 1))) {
+                if (sel < WAVE) { v0 += 1u; t0 += reward; }
+                else { v1 += 1u; t1 += reward; }
+            }
+            root_visits += 1u;
         }
-        // NaN base: the cached legal list was empty -> reward 0.0 and no draw
-        // (fast_mcts_agent.py:255-257)
-        const double reward = (base == base) ? base + py_random(mt, idx, lane) * 0.1 : 0.0;
-        if (lane == 0) {
-            visits[sel] += 1u;
-            total[sel] += reward;
-        }
+        // the words the iterations consumed: the generator stops there (unused draws are
+        // not taken)
+        if (draw) idx = ridx - 2 * (ravail - rptr);  // (a straddling draw is always consumed)
+        if (lane < n) { visits[lane] = v0; total[lane] = t0; }
+        if (lane + WAVE < n) { visits[lane + WAVE] = v1; total[lane + WAVE] = t1; }
         __syncthreads();
-        root_visits += 1u;
+    } else {
+        for (; it < iters; ++it) {
+            int sel;
+            if (nch < n) {
+                sel = nch++;  // expand: untried_moves.pop() -> child nch <-> legal[n - 1 - nch]
+            } else {
+                const double lg = (int)root_visits < nlt ? ltab[root_visits] : a.log_table[root_visits];
+                sel = fm_select(visits, total, nch, lane, 2.0 * lg, root_visits, a.c, a.fix);
+            }
+            // NaN base: the cached legal list was empty -> reward 0.0 and no draw
+            // (fast_mcts_agent.py:255-257)
+            const double reward = (base == base) ? base + py_random(mt, idx, lane) * 0.1 : 0.0;
+            if (lane == 0) {
+                visits[sel] += 1u;
+                total[sel] += reward;
+            }
+            __syncthreads();
+            root_visits += 1u;
+        }
     }
     if (a.visits_out) {
         int32_t* vo = a.visits_out + a.offset[game];
